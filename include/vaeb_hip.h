@@ -1,0 +1,127 @@
+/*
+ * vaeb_hip.h -- C ABI of the MI355X-native VAEB SGVB training step (libvaeb_hip.so).
+ *
+ * The reference's operator boundary is the pair of Theano compiled functions built in
+ * VAEB.getGradient (/root/reference/VAEB.py:408-422): `update(index) -> SGVB/B`
+ * (mutating theta, the Adagrad accumulators and the RNG stream in place) and
+ * `validate(x) -> SGVB` (forward-only sum).  This header exports those two operations
+ * plus the state transfers the Python `VAEB` class needs (VAEB.py:132-242), as plain
+ * `extern "C"` functions over host pointers and sizes.  No torch types appear here.
+ *
+ * Conventions
+ *  - Every function returns int: 0 = ok, < 0 = error; vaeb_last_error() returns a
+ *    thread-local message for the last failing call on this thread.
+ *  - The caller owns host buffers (copied in/out during the call); the library owns all
+ *    device memory.  One context per GPU/rank; calls on one context must be serialised.
+ *  - Parameters are flat float32 in the reference order
+ *    [W3,W4,W5,W1,W2,(W6),b3,b4,b5,b1,b2,(b6)] (VAEB.py:111-115), each row-major (C order).
+ */
+#ifndef VAEB_HIP_H
+#define VAEB_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum vaeb_decoder   { VAEB_DEC_BERNOULLI = 0, VAEB_DEC_GAUSSIAN = 1 };   /* --continuous, VAEB.py:256 */
+enum vaeb_estimator { VAEB_EST_LB = 0, VAEB_EST_LA = 1, VAEB_EST_FV = 2 };/* VAEB.py:378-383 */
+enum vaeb_objective { VAEB_OBJ_SUM_PRIOR = 0,                             /* VAEB.py:386-390 */
+                      VAEB_OBJ_MEAN_MAP = 1 };                            /* VAEBfullbayes.py:142,183 */
+enum vaeb_eps_mode  { VAEB_EPS_PHILOX = 0, VAEB_EPS_HOST = 1 };
+enum vaeb_status    { VAEB_OK = 0, VAEB_ERR_ARG = -1, VAEB_ERR_HIP = -2, VAEB_ERR_STATE = -3,
+                      VAEB_ERR_COMM = -4, VAEB_ERR_NOMEM = -5 };
+
+typedef struct vaeb_config {
+    int32_t D;            /* input size (784 MNIST, 560 Frey)                         */
+    int32_t H;            /* hidden units (--hidden_unit, VAEB.py:542-552)             */
+    int32_t Z;            /* latent size (--n_latent)                                  */
+    int32_t B;            /* rows this rank processes per step                          */
+    int32_t B_global;     /* rows of one global minibatch (= B * world for weak scaling) */
+    int32_t row_offset;   /* first row of this rank inside the global minibatch          */
+    int32_t L;            /* samples per datapoint (--L)                                 */
+    int32_t decoder;      /* enum vaeb_decoder                                           */
+    int32_t estimator;    /* enum vaeb_estimator                                         */
+    int32_t objective;    /* enum vaeb_objective                                         */
+    float   lr;           /* --learning_rate (VAEB.py:31)                                */
+    float   adagrad_eps;  /* 1e-6 (VAEB.py:144)                                          */
+    int32_t device;       /* HIP device ordinal                                          */
+    int32_t max_eval_rows;/* largest x passed to vaeb_validate in one device chunk       */
+    int32_t use_graph;    /* 1: replay the step as a captured hipGraph                   */
+    int32_t keep_grads;   /* 1: also store each step's data gradient (vaeb_get_grads)    */
+    int32_t reserved[6];
+} vaeb_config;
+
+typedef struct vaeb_ctx vaeb_ctx;
+
+const char* vaeb_last_error(void);
+int vaeb_version(int32_t* major, int32_t* minor);
+
+/* Lifetime */
+int vaeb_create(const vaeb_config* cfg, vaeb_ctx** out);
+int vaeb_destroy(vaeb_ctx* ctx);
+int vaeb_num_params(const vaeb_ctx* ctx, int64_t* n);
+
+/* Training data: copied into a device-resident store owned by ctx (replaces the
+ * th.shared x_train of VAEB.py:184).  Row-major float32 [n_rows x D]. */
+int vaeb_set_data(vaeb_ctx* ctx, const float* x, int64_t n_rows);
+
+/* Parameters / optimizer state in reference order.  For the FV estimator the
+ * "params" are the fixed data-term theta (VAEB.py:117-119) and the variational
+ * (mu_theta, sigma_theta) pairs are transferred with vaeb_{set,get}_fv_state. */
+int vaeb_set_params(vaeb_ctx* ctx, const float* flat, int64_t n);
+int vaeb_get_params(vaeb_ctx* ctx, float* flat, int64_t n);
+int vaeb_set_adagrad_state(vaeb_ctx* ctx, const float* flat, int64_t n);
+int vaeb_get_adagrad_state(vaeb_ctx* ctx, float* flat, int64_t n);
+/* FV: mu, sigma and their accumulators, each n = num_params floats. */
+int vaeb_set_fv_state(vaeb_ctx* ctx, const float* mu, const float* sigma,
+                      const float* acc_mu, const float* acc_sigma, int64_t n);
+int vaeb_get_fv_state(vaeb_ctx* ctx, float* mu, float* sigma,
+                      float* acc_mu, float* acc_sigma, int64_t n);
+
+/* Noise for the reparameterisation (VAEB.py:41-47).  PHILOX: counter-based normals
+ * keyed by (seed, step, global row, l, j), world-size invariant.  HOST: the caller
+ * pushes eps [L x rows x Z] before each update/validate chunk (parity mode). */
+int vaeb_set_eps_mode(vaeb_ctx* ctx, int32_t mode, uint64_t seed);
+int vaeb_push_eps(vaeb_ctx* ctx, const float* eps, int64_t rows, int32_t L);
+int vaeb_set_step(vaeb_ctx* ctx, int64_t step);   /* Philox step counter */
+
+/* One SGVB step on the contiguous minibatch `batch_index` (VAEB.py:413), synchronous
+ * like the reference: writes SGVB / B_global to *out_elbo_per_row. */
+int vaeb_update(vaeb_ctx* ctx, int32_t batch_index, float* out_elbo_per_row);
+/* Throughput mode: enqueue one step, no host sync.  The ELBO stays on device and is
+ * accumulated; read (and reset) the epoch mean with vaeb_epoch_elbo. */
+int vaeb_update_async(vaeb_ctx* ctx, int32_t batch_index);
+/* Enqueue a whole list of steps (an epoch's batch order) with one call. */
+int vaeb_update_many(vaeb_ctx* ctx, const int32_t* batch_indices, int32_t n);
+int vaeb_epoch_elbo(vaeb_ctx* ctx, double* out_sum, int64_t* out_steps);
+int vaeb_synchronize(vaeb_ctx* ctx);
+
+/* Forward-only SGVB sum over n rows of host x (VAEB.py:418-422). */
+int vaeb_validate(vaeb_ctx* ctx, const float* x, int64_t n, double* out_sum);
+/* Decoder means y for host x with z = mu (n_samples <= 0 branch of VAEB.reconstruct,
+ * VAEB.py:267-270): writes [n x D]. */
+int vaeb_reconstruct(vaeb_ctx* ctx, const float* x, int64_t n, float* out_y);
+
+/* Data parallel (one ctx per rank): the library owns an RCCL communicator; the 128-byte
+ * unique id is produced on rank 0 and broadcast by the host (e.g. torch.distributed). */
+int vaeb_comm_unique_id(uint8_t out_id[128]);
+int vaeb_comm_init(vaeb_ctx* ctx, const uint8_t id[128], int32_t rank, int32_t world);
+
+/* Introspection for parity tests: last step's data gradients (reference order, before
+ * the prior) and named device activations ("h","mu","lv","z","hd","dA2","dA3",...). */
+int vaeb_get_grads(vaeb_ctx* ctx, float* flat, int64_t n);
+int vaeb_get_activation(vaeb_ctx* ctx, const char* name, float* out, int64_t n);
+
+/* Measurement: runs n_steps eager steps with HIP events around every launch on the
+ * context's stream; writes the average device time (ms) and the kernel id of each
+ * launch slot of one step.  vaeb_kernel_name maps a kernel id to its name. */
+int vaeb_profile_steps(vaeb_ctx* ctx, int32_t n_steps, float* out_ms_per_kernel,
+                       int32_t* out_kernel_ids, int32_t max_kernels, int32_t* out_n_kernels);
+int vaeb_kernel_name(int32_t kernel_id, char* out, int32_t cap);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* VAEB_HIP_H */

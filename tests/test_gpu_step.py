@@ -1,0 +1,239 @@
+"""Parity of the HIP SGVB step (libvaeb_hip.so, through the C ABI) against the CPU
+oracle (oracle/vaeb_oracle.py, float64) on identical theta / acc / x / eps.
+
+Tolerances (stated per SURVEY 8(d)):
+  * ELBO (SGVB/B): relative error <= 1e-4 (observed ~1e-6)
+  * data gradients: norm-wise relative error <= 1e-4 per parameter tensor
+  * theta' after Adagrad: |diff| <= 1e-3 * lr for all but a 1e-4 fraction of elements
+    (the first Adagrad step is ~lr*sign(g); elements with |g| ~ 1e-6 may flip), and
+    never more than 2 * lr
+  * forward activations: absolute error <= 1e-5
+"""
+import numpy as np
+import pytest
+
+from oracle import vaeb_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+EST = {"LB": 0, "LA": 1, "FV": 2}
+OBJ = {"sum_prior": 0, "mean_map": 1}
+
+
+def make_ctx(cfg, B, keep_grads=True, use_graph=True, max_eval_rows=1000):
+    from vaeb_amd import _lib
+    return _lib.Context(cfg.D, cfg.H, cfg.Z, B, L=cfg.L, decoder=int(cfg.continuous), estimator=EST[cfg.estimator],
+                        objective=OBJ[cfg.objective], lr=cfg.lr, keep_grads=keep_grads, use_graph=use_graph,
+                        max_eval_rows=max_eval_rows)
+
+
+def data_for(cfg, n, seed=0):
+    if cfg.continuous:
+        return O.synthetic_frey(n=n, D=cfg.D, seed=seed)
+    return O.synthetic_mnist(n=n, D=cfg.D, seed=seed)
+
+
+def rel(a, b):
+    return float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30))
+
+
+def check_theta(new, ref, lr):
+    d = np.abs(new - ref)
+    assert d.max() <= 2 * lr + 1e-7, d.max()
+    frac = float((d > 1e-3 * lr).mean())
+    assert frac <= 1e-4, frac
+
+
+CASES = [
+    ("mnist20", dict(D=784, H=500, Z=20), 100),
+    ("odd_shapes", dict(D=37, H=19, Z=3), 13),
+    ("frey2_gauss", dict(D=560, H=200, Z=2, continuous=True), 100),
+    ("mnist_LA_L2", dict(D=784, H=500, Z=20, estimator="LA", L=2), 100),
+    ("mnist_LB_L3_odd", dict(D=50, H=33, Z=7, L=3), 21),
+    ("frey_LA", dict(D=560, H=200, Z=5, continuous=True, estimator="LA", L=2), 100),
+    ("mean_map_frey10", dict(D=560, H=200, Z=10, continuous=True, objective="mean_map"), 100),
+    ("mean_map_mnist", dict(D=784, H=500, Z=10, objective="mean_map"), 100),
+]
+
+
+@pytest.mark.parametrize("name,kw,B", CASES, ids=[c[0] for c in CASES])
+def test_single_step_parity(name, kw, B):
+    cfg = O.Config(**kw)
+    x = data_for(cfg, 4 * B)
+    params = O.init_params(cfg)
+    rng = np.random.default_rng(3)
+    # non-zero biases so every bias path is exercised
+    params = [p if p.ndim == 2 else (0.01 * rng.standard_normal(p.shape)).astype(np.float32) for p in params]
+    acc = [np.zeros_like(p) for p in params]
+    eps = rng.standard_normal((cfg.L, B, cfg.Z)).astype(np.float32)
+    idx = 2
+    xb = x[idx * B:(idx + 1) * B]
+
+    ctx = make_ctx(cfg, B)
+    ctx.set_data(x)
+    ctx.set_params(O.flatten(params))
+    ctx.set_adagrad_state(O.flatten(acc))
+    ctx.set_eps_mode(1)
+    ctx.push_eps(eps)
+    elbo = ctx.update(idx)
+
+    p64 = [p.astype(np.float64) for p in params]
+    a64 = [a.astype(np.float64) for a in acc]
+    ref_elbo, ref_p, ref_a, aux = O.step(p64, a64, xb.astype(np.float64), eps.astype(np.float64), cfg)
+    assert abs(elbo - ref_elbo) <= 1e-4 * abs(ref_elbo), (elbo, ref_elbo)
+
+    # forward activations
+    h = ctx.activation("h", ((B + 15) // 16 * 16) * cfg.H).reshape(-1, cfg.H)[:B]
+    assert np.abs(h - aux["h"]).max() <= 1e-5
+    mu = ctx.activation("mu", ((B + 15) // 16 * 16) * cfg.Z).reshape(-1, cfg.Z)[:B]
+    assert np.abs(mu - aux["mu"]).max() <= 1e-5
+
+    g = ctx.get_grads()
+    for (n, s), gg, rr in zip(O.param_shapes(cfg), O.unflatten(g, cfg), aux["data_grads"]):
+        assert rel(gg.reshape(s), rr) <= 1e-4, (n, rel(gg.reshape(s), rr))
+
+    newp = ctx.get_params()
+    check_theta(newp, O.flatten(ref_p), cfg.lr)
+    newa = ctx.get_adagrad_state()
+    assert rel(newa, O.flatten(ref_a)) <= 1e-4
+
+
+def test_trajectory_50_steps_mnist():
+    """50 consecutive steps (graph replay, device-resident batch order) track the oracle."""
+    cfg = O.Config(D=784, H=500, Z=20)
+    B = 100
+    x = data_for(cfg, 1000)
+    params = O.init_params(cfg)
+    acc = [np.zeros_like(p) for p in params]
+    ctx = make_ctx(cfg, B, keep_grads=False)
+    ctx.set_data(x)
+    ctx.set_params(O.flatten(params))
+    ctx.set_eps_mode(1)
+    rng = np.random.default_rng(11)
+    order = rng.permutation(10)
+    p, a = [q.astype(np.float64) for q in params], [q.astype(np.float64) for q in acc]
+    elbos, refs = [], []
+    for t in range(50):
+        b = int(order[t % 10])
+        eps = rng.standard_normal((1, B, cfg.Z)).astype(np.float32)
+        ctx.push_eps(eps)
+        elbos.append(ctx.update(b))
+        e, p, a, _ = O.step(p, a, x[b * B:(b + 1) * B].astype(np.float64), eps.astype(np.float64), cfg)
+        refs.append(e)
+    elbos, refs = np.array(elbos), np.array(refs)
+    assert np.all(np.abs(elbos - refs) <= 1e-3 * np.abs(refs)), np.abs(elbos - refs).max()
+    newp = ctx.get_params()
+    assert np.abs(newp - O.flatten(p)).max() <= 5e-3
+
+
+@pytest.mark.parametrize("continuous", [False, True])
+def test_validate_matches_oracle(continuous):
+    cfg = O.Config(D=560, H=200, Z=2, continuous=True) if continuous else O.Config(D=784, H=500, Z=20)
+    n = 2500
+    x = data_for(cfg, n, seed=5)
+    params = O.init_params(cfg)
+    rng = np.random.default_rng(2)
+    eps = rng.standard_normal((1, n, cfg.Z)).astype(np.float32)
+    ctx = make_ctx(cfg, 100, max_eval_rows=1000)  # 3 device chunks
+    ctx.set_data(x[:1000])
+    ctx.set_params(O.flatten(params))
+    ctx.set_eps_mode(1)
+    ctx.push_eps(eps)
+    v = ctx.validate(x)
+    ref = O.validate([q.astype(np.float64) for q in params], x.astype(np.float64), eps.astype(np.float64), cfg)
+    assert abs(v - ref) <= 1e-4 * abs(ref), (v, ref)
+
+
+def test_reconstruct_matches_oracle():
+    cfg = O.Config(D=784, H=500, Z=20)
+    x = data_for(cfg, 300, seed=9)
+    params = O.init_params(cfg)
+    ctx = make_ctx(cfg, 100)
+    ctx.set_data(x)
+    ctx.set_params(O.flatten(params))
+    y = ctx.reconstruct(x)
+    out = O.forward_backward([q.astype(np.float64) for q in params], x.astype(np.float64),
+                             np.zeros((1, 300, cfg.Z)), cfg, need_grad=False)
+    assert np.abs(y - out["y"]).max() <= 1e-5
+
+
+def test_fv_literal_step():
+    cfg = O.Config(D=560, H=200, Z=2, continuous=True, estimator="FV")
+    B = 100
+    x = data_for(cfg, 1500)
+    theta = O.init_params(cfg)
+    rng = np.random.default_rng(4)
+    theta = [(t + 0.05 * rng.standard_normal(t.shape)).astype(np.float32) for t in theta]
+    mu = [t.copy() for t in theta]
+    sig = [np.full_like(t, 1e-3) for t in theta]
+    am = [np.zeros_like(t) for t in theta]
+    as_ = [np.zeros_like(t) for t in theta]
+    ctx = make_ctx(cfg, B)
+    ctx.set_data(x)
+    ctx.set_params(O.flatten(theta))
+    ctx.set_fv_state(O.flatten(mu), O.flatten(sig), O.flatten(am), O.flatten(as_))
+    ctx.set_eps_mode(1)
+    m64, s64 = [q.astype(np.float64) for q in mu], [q.astype(np.float64) for q in sig]
+    am64, as64 = [q.astype(np.float64) for q in am], [q.astype(np.float64) for q in as_]
+    t64 = [q.astype(np.float64) for q in theta]
+    for t in range(3):
+        eps = rng.standard_normal((1, B, cfg.Z)).astype(np.float32)
+        ctx.push_eps(eps)
+        e = ctx.update(t)
+        ref, m64, s64, am64, as64, _ = O.fv_step(t64, m64, s64, am64, as64, x[t * B:(t + 1) * B].astype(np.float64),
+                                                 eps.astype(np.float64), cfg)
+        assert abs(e - ref) <= 1e-4 * abs(ref), (t, e, ref)
+    gm, gs, gam, gas = ctx.get_fv_state()
+    assert np.abs(gm - O.flatten(m64)).max() <= 1e-6
+    assert np.abs(gs - O.flatten(s64)).max() <= 1e-7
+    # theta itself is never updated on the literal FV path (SURVEY 8(c) pin 2)
+    assert np.array_equal(ctx.get_params(), O.flatten(theta))
+
+
+def test_philox_eps_is_standard_normal_and_deterministic():
+    cfg = O.Config(D=784, H=500, Z=20)
+    x = data_for(cfg, 1000)
+    ctx = make_ctx(cfg, 100)
+    ctx.set_data(x)
+    ctx.set_params(O.flatten(O.init_params(cfg)))
+    ctx.set_eps_mode(0, seed=10)
+    ctx.set_step(0)
+    ctx.update(0)
+    e1 = ctx.activation("eps", 112 * 20).reshape(112, 20)[:100]
+    ctx.set_step(0)
+    ctx.set_params(O.flatten(O.init_params(cfg)))
+    ctx.update(0)
+    e2 = ctx.activation("eps", 112 * 20).reshape(112, 20)[:100]
+    assert np.array_equal(e1, e2)
+    ctx.update(0)
+    e3 = ctx.activation("eps", 112 * 20).reshape(112, 20)[:100]
+    assert not np.array_equal(e1, e3)
+    big = []
+    for _ in range(20):
+        ctx.update(1)
+        big.append(ctx.activation("eps", 112 * 20).reshape(112, 20)[:100].ravel())
+    big = np.concatenate(big)
+    assert abs(big.mean()) < 0.02 and abs(big.std() - 1) < 0.02
+
+
+def test_epoch_throughput_mode_matches_sync_mode():
+    """update_many (graph replay, no host sync) == per-step update (same Philox noise)."""
+    cfg = O.Config(D=784, H=500, Z=20)
+    x = data_for(cfg, 5000)
+    order = np.random.default_rng(0).permutation(50).astype(np.int32)
+    res = []
+    for mode in ("sync", "many"):
+        ctx = make_ctx(cfg, 100, keep_grads=False)
+        ctx.set_data(x)
+        ctx.set_params(O.flatten(O.init_params(cfg)))
+        ctx.set_eps_mode(0, seed=10)
+        ctx.set_step(0)
+        if mode == "sync":
+            tot = sum(ctx.update(int(b)) for b in order)
+        else:
+            ctx.update_many(order)
+            tot, n = ctx.epoch_elbo()
+            assert n == len(order)
+        res.append((tot, ctx.get_params()))
+    assert abs(res[0][0] - res[1][0]) <= 1e-5 * abs(res[0][0])
+    assert np.array_equal(res[0][1], res[1][1])

@@ -1,0 +1,256 @@
+"""ctypes binding of libvaeb_hip.so (include/vaeb_hip.h).
+
+The library is built in-tree (vaeb_amd/libvaeb_hip.so, see __graft_entry__.build()).
+There is no CPU fallback: if the shared object is missing or a call fails, an error is
+raised.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libvaeb_hip.so")
+
+DEC_BERNOULLI, DEC_GAUSSIAN = 0, 1
+EST_LB, EST_LA, EST_FV = 0, 1, 2
+OBJ_SUM_PRIOR, OBJ_MEAN_MAP = 0, 1
+EPS_PHILOX, EPS_HOST = 0, 1
+
+# Every symbol declared in include/vaeb_hip.h (checked by tests/test_abi.py).
+EXPORTS = [
+    "vaeb_last_error", "vaeb_version", "vaeb_create", "vaeb_destroy", "vaeb_num_params",
+    "vaeb_set_data", "vaeb_set_params", "vaeb_get_params", "vaeb_set_adagrad_state",
+    "vaeb_get_adagrad_state", "vaeb_set_fv_state", "vaeb_get_fv_state", "vaeb_set_eps_mode",
+    "vaeb_push_eps", "vaeb_set_step", "vaeb_update", "vaeb_update_async", "vaeb_update_many",
+    "vaeb_epoch_elbo", "vaeb_synchronize", "vaeb_validate", "vaeb_reconstruct",
+    "vaeb_comm_unique_id", "vaeb_comm_init", "vaeb_get_grads", "vaeb_get_activation",
+    "vaeb_profile_steps", "vaeb_kernel_name",
+]
+
+
+class VaebConfig(ctypes.Structure):
+    _fields_ = [
+        ("D", ctypes.c_int32), ("H", ctypes.c_int32), ("Z", ctypes.c_int32), ("B", ctypes.c_int32),
+        ("B_global", ctypes.c_int32), ("row_offset", ctypes.c_int32), ("L", ctypes.c_int32),
+        ("decoder", ctypes.c_int32), ("estimator", ctypes.c_int32), ("objective", ctypes.c_int32),
+        ("lr", ctypes.c_float), ("adagrad_eps", ctypes.c_float), ("device", ctypes.c_int32),
+        ("max_eval_rows", ctypes.c_int32), ("use_graph", ctypes.c_int32), ("keep_grads", ctypes.c_int32),
+        ("reserved", ctypes.c_int32 * 6),
+    ]
+
+
+class VaebError(RuntimeError):
+    pass
+
+
+_lib = None
+
+_F = ctypes.POINTER(ctypes.c_float)
+_I64 = ctypes.c_int64
+_P = ctypes.c_void_p
+
+
+def load():
+    """Load the HIP library (raises if it has not been built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise VaebError(f"{LIB_PATH} not found: build it with `python -c 'import __graft_entry__ as g; g.build()'`")
+    lib = ctypes.CDLL(LIB_PATH)
+    sig = {
+        "vaeb_last_error": ([], ctypes.c_char_p),
+        "vaeb_version": ([ctypes.POINTER(ctypes.c_int32)] * 2, ctypes.c_int),
+        "vaeb_create": ([ctypes.POINTER(VaebConfig), ctypes.POINTER(_P)], ctypes.c_int),
+        "vaeb_destroy": ([_P], ctypes.c_int),
+        "vaeb_num_params": ([_P, ctypes.POINTER(_I64)], ctypes.c_int),
+        "vaeb_set_data": ([_P, _F, _I64], ctypes.c_int),
+        "vaeb_set_params": ([_P, _F, _I64], ctypes.c_int),
+        "vaeb_get_params": ([_P, _F, _I64], ctypes.c_int),
+        "vaeb_set_adagrad_state": ([_P, _F, _I64], ctypes.c_int),
+        "vaeb_get_adagrad_state": ([_P, _F, _I64], ctypes.c_int),
+        "vaeb_set_fv_state": ([_P, _F, _F, _F, _F, _I64], ctypes.c_int),
+        "vaeb_get_fv_state": ([_P, _F, _F, _F, _F, _I64], ctypes.c_int),
+        "vaeb_set_eps_mode": ([_P, ctypes.c_int32, ctypes.c_uint64], ctypes.c_int),
+        "vaeb_push_eps": ([_P, _F, _I64, ctypes.c_int32], ctypes.c_int),
+        "vaeb_set_step": ([_P, _I64], ctypes.c_int),
+        "vaeb_update": ([_P, ctypes.c_int32, _F], ctypes.c_int),
+        "vaeb_update_async": ([_P, ctypes.c_int32], ctypes.c_int),
+        "vaeb_update_many": ([_P, ctypes.POINTER(ctypes.c_int32), ctypes.c_int32], ctypes.c_int),
+        "vaeb_epoch_elbo": ([_P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_I64)], ctypes.c_int),
+        "vaeb_synchronize": ([_P], ctypes.c_int),
+        "vaeb_validate": ([_P, _F, _I64, ctypes.POINTER(ctypes.c_double)], ctypes.c_int),
+        "vaeb_reconstruct": ([_P, _F, _I64, _F], ctypes.c_int),
+        "vaeb_comm_unique_id": ([ctypes.POINTER(ctypes.c_uint8)], ctypes.c_int),
+        "vaeb_comm_init": ([_P, ctypes.POINTER(ctypes.c_uint8), ctypes.c_int32, ctypes.c_int32], ctypes.c_int),
+        "vaeb_get_grads": ([_P, _F, _I64], ctypes.c_int),
+        "vaeb_get_activation": ([_P, ctypes.c_char_p, _F, _I64], ctypes.c_int),
+        "vaeb_profile_steps": ([_P, ctypes.c_int32, _F, ctypes.POINTER(ctypes.c_int32), ctypes.c_int32,
+                                ctypes.POINTER(ctypes.c_int32)], ctypes.c_int),
+        "vaeb_kernel_name": ([ctypes.c_int32, ctypes.c_char_p, ctypes.c_int32], ctypes.c_int),
+    }
+    for name, (args, res) in sig.items():
+        fn = getattr(lib, name)
+        fn.argtypes = args
+        fn.restype = res
+    _lib = lib
+    return lib
+
+
+def check(rc):
+    if rc != 0:
+        msg = _lib.vaeb_last_error().decode(errors="replace") if _lib is not None else "?"
+        raise VaebError(f"libvaeb_hip error {rc}: {msg}")
+
+
+def fptr(a: np.ndarray):
+    assert a.dtype == np.float32 and a.flags["C_CONTIGUOUS"]
+    return a.ctypes.data_as(_F)
+
+
+class Context:
+    """Thin RAII wrapper over one vaeb_ctx (one GPU / rank)."""
+
+    def __init__(self, D, H, Z, B, L=1, decoder=DEC_BERNOULLI, estimator=EST_LB, objective=OBJ_SUM_PRIOR,
+                 lr=0.01, adagrad_eps=1e-6, device=0, B_global=None, row_offset=0, max_eval_rows=10000,
+                 use_graph=True, keep_grads=False):
+        self.lib = load()
+        cfg = VaebConfig()
+        cfg.D, cfg.H, cfg.Z, cfg.B, cfg.L = D, H, Z, B, L
+        cfg.B_global = B if B_global is None else B_global
+        cfg.row_offset = row_offset
+        cfg.decoder, cfg.estimator, cfg.objective = decoder, estimator, objective
+        cfg.lr, cfg.adagrad_eps = lr, adagrad_eps
+        cfg.device, cfg.max_eval_rows = device, max_eval_rows
+        cfg.use_graph, cfg.keep_grads = int(bool(use_graph)), int(bool(keep_grads))
+        self.cfg = cfg
+        self.h = _P()
+        check(self.lib.vaeb_create(ctypes.byref(cfg), ctypes.byref(self.h)))
+        n = _I64()
+        check(self.lib.vaeb_num_params(self.h, ctypes.byref(n)))
+        self.P = n.value
+
+    def close(self):
+        if getattr(self, "h", None) is not None and self.h.value:
+            self.lib.vaeb_destroy(self.h)
+            self.h = _P()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---- state
+    def set_data(self, x):
+        x = np.ascontiguousarray(x, np.float32)
+        check(self.lib.vaeb_set_data(self.h, fptr(x), x.shape[0]))
+
+    def set_params(self, flat):
+        flat = np.ascontiguousarray(flat, np.float32)
+        check(self.lib.vaeb_set_params(self.h, fptr(flat), flat.size))
+
+    def get_params(self):
+        out = np.empty(self.P, np.float32)
+        check(self.lib.vaeb_get_params(self.h, fptr(out), out.size))
+        return out
+
+    def set_adagrad_state(self, flat):
+        flat = np.ascontiguousarray(flat, np.float32)
+        check(self.lib.vaeb_set_adagrad_state(self.h, fptr(flat), flat.size))
+
+    def get_adagrad_state(self):
+        out = np.empty(self.P, np.float32)
+        check(self.lib.vaeb_get_adagrad_state(self.h, fptr(out), out.size))
+        return out
+
+    def get_grads(self):
+        out = np.empty(self.P, np.float32)
+        check(self.lib.vaeb_get_grads(self.h, fptr(out), out.size))
+        return out
+
+    def set_fv_state(self, mu, sigma, acc_mu, acc_sigma):
+        arrs = [np.ascontiguousarray(a, np.float32) for a in (mu, sigma, acc_mu, acc_sigma)]
+        check(self.lib.vaeb_set_fv_state(self.h, *[fptr(a) for a in arrs], arrs[0].size))
+
+    def get_fv_state(self):
+        arrs = [np.empty(self.P, np.float32) for _ in range(4)]
+        check(self.lib.vaeb_get_fv_state(self.h, *[fptr(a) for a in arrs], self.P))
+        return arrs
+
+    def activation(self, name, n):
+        out = np.empty(n, np.float32)
+        check(self.lib.vaeb_get_activation(self.h, name.encode(), fptr(out), n))
+        return out
+
+    # ---- noise
+    def set_eps_mode(self, mode, seed=10):
+        check(self.lib.vaeb_set_eps_mode(self.h, mode, seed))
+
+    def push_eps(self, eps):
+        eps = np.ascontiguousarray(eps, np.float32)
+        L, rows, _ = eps.shape
+        check(self.lib.vaeb_push_eps(self.h, fptr(eps), rows, L))
+
+    def set_step(self, step):
+        check(self.lib.vaeb_set_step(self.h, int(step)))
+
+    # ---- steps
+    def update(self, index):
+        out = ctypes.c_float()
+        check(self.lib.vaeb_update(self.h, int(index), ctypes.byref(out)))
+        return out.value
+
+    def update_many(self, indices):
+        idx = np.ascontiguousarray(indices, np.int32)
+        check(self.lib.vaeb_update_many(self.h, idx.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), idx.size))
+
+    def epoch_elbo(self):
+        s = ctypes.c_double()
+        n = _I64()
+        check(self.lib.vaeb_epoch_elbo(self.h, ctypes.byref(s), ctypes.byref(n)))
+        return s.value, n.value
+
+    def synchronize(self):
+        check(self.lib.vaeb_synchronize(self.h))
+
+    def validate(self, x):
+        x = np.ascontiguousarray(x, np.float32)
+        out = ctypes.c_double()
+        check(self.lib.vaeb_validate(self.h, fptr(x), x.shape[0], ctypes.byref(out)))
+        return out.value
+
+    def reconstruct(self, x):
+        x = np.ascontiguousarray(x, np.float32)
+        y = np.empty((x.shape[0], self.cfg.D), np.float32)
+        check(self.lib.vaeb_reconstruct(self.h, fptr(x), x.shape[0], fptr(y)))
+        return y
+
+    # ---- data parallel
+    @staticmethod
+    def comm_unique_id():
+        lib = load()
+        buf = (ctypes.c_uint8 * 128)()
+        check(lib.vaeb_comm_unique_id(buf))
+        return bytes(buf)
+
+    def comm_init(self, uid: bytes, rank, world):
+        buf = (ctypes.c_uint8 * 128).from_buffer_copy(uid)
+        check(self.lib.vaeb_comm_init(self.h, buf, rank, world))
+
+    # ---- measurement
+    def profile_steps(self, n_steps):
+        ms = np.zeros(16, np.float32)
+        ids = np.zeros(16, np.int32)
+        nk = ctypes.c_int32()
+        check(self.lib.vaeb_profile_steps(self.h, n_steps, fptr(ms), ids.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)),
+                                          16, ctypes.byref(nk)))
+        out = []
+        for k in range(nk.value):
+            buf = ctypes.create_string_buffer(64)
+            check(self.lib.vaeb_kernel_name(int(ids[k]), buf, 64))
+            out.append((buf.value.decode(), float(ms[k])))
+        return out

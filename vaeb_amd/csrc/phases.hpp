@@ -1,0 +1,357 @@
+// phases.hpp -- the SGVB step (VAEB.update, /root/reference/VAEB.py:408-415) as eight
+// fused MFMA phases.  Each struct is one launch: operand loaders + fused epilogue.
+//
+//  P1 enc     h   = tanh(X W3 + b3)                                  VAEB.py:246
+//  P2 heads   mu  = h W4 + b4, lv = h W5 + b5  (two accumulators)    VAEB.py:248-249
+//             -> eps (Philox or injected), z = mu + exp(lv/2) eps,   VAEB.py:42-45
+//                per-row KL (LB, VAEB.py:343) or prior-logQ (LA, :322-325) partials
+//  P3 dechid  hd  = tanh(z W1 + b1)                                  VAEB.py:254
+//  P4 decout  a2  = hd W2 + b2 (+ a6 = hd W6 + b6 Gaussian)          VAEB.py:257-263
+//             -> per-row log p(x|z) partials (VAEB.py:302-313) and dA2 (+ dA6)
+//  P5 dhd     dA1 = (dA2 W2^T (+ dA6 W6^T)) * (1 - hd^2)
+//  P6 dz      dZ  = dA1 W1^T
+//  P7 dh      [dMu|dLv] formed on the fly from dZ (sum over the L samples) and the
+//             KL / LA direct terms;  dA3 = ([dMu|dLv] [W4|W5]^T) * (1 - h^2)
+//  P8 wgrad   grouped TN GEMMs dW = act^T delta with a ones-row for the bias
+//             gradient, fused prior (-theta, VAEB.py:386-390) + Adagrad
+//             (VAEB.py:426-444), plus one workgroup that reduces the ELBO partials.
+#pragma once
+#include "tile_engine.hpp"
+
+namespace vaeb {
+
+enum : int { DEC_BERNOULLI = 0, DEC_GAUSSIAN = 1 };
+enum : int { EST_LB = 0, EST_LA = 1, EST_FV = 2 };
+enum : int { MODE_TRAIN = 0, MODE_EVAL = 1, MODE_RECON = 2 };
+constexpr float kHalfLog2Pi = 0.91893853320467274178f;
+
+struct StepArgs {
+    int D, H, Z, L;
+    int Mb;    // valid rows of this launch (batch rows of this rank)
+    int Mbp;   // rows padded to 16
+    int Me;    // L * Mbp decoder rows
+    int dec, est, mode;
+    float sc;  // loss scale: 1 (sum objective) or 1/B_global (mean objective)
+    // parameters (reference order arena)
+    const float *W3, *W4, *W5, *W1, *W2, *W6, *b3, *b4, *b5, *b1, *b2, *b6;
+    // input rows: x = xbase + order[*cursor] * batch_stride  (order == nullptr: xbase)
+    const float* xbase;
+    const int* order;
+    const int* cursor;
+    int* cur_batch;        // written by P1 (resolved order[*cursor]); read by later phases
+    int64_t batch_stride;
+    int64_t row_base_mul;  // global-row id of local row i = order[*cursor]*row_base_mul + row_base_add + i
+    int64_t row_base_add;
+    // noise
+    int eps_mode;          // 0 philox, 1 host buffer, 2 zero (reconstruct)
+    uint64_t seed;
+    const int64_t* step;   // Philox step counter (device)
+    uint32_t domain;       // 0 training, 1 validation
+    const float* eps_in;   // host-pushed [L][Mb][Z] (+ eps_in_off rows)
+    int64_t eps_in_ld;     // rows per l-plane of eps_in
+    // activations / deltas ([rows][cols] row-major; pad rows written as 0)
+    float *h, *mu, *lv, *eps, *z, *hd, *y, *dA2, *dA6, *dA1, *dZ, *dMuLv, *dA3;
+    // ELBO partials: [rows][col tiles]
+    float *kl_part, *la_part, *lp_part;
+    int nctZ, nctD;
+};
+
+// P1 resolves the minibatch index from the device-side batch order; every later phase
+// of the step reads the resolved copy (the cursor advances inside P8 / the optimizer).
+DEV const float* x_rows_p1(const StepArgs& a) {
+    return a.order ? a.xbase + (int64_t)a.order[*a.cursor] * a.batch_stride : a.xbase;
+}
+DEV const float* x_rows(const StepArgs& a) {
+    return a.order ? a.xbase + (int64_t)(*a.cur_batch) * a.batch_stride : a.xbase;
+}
+DEV int64_t global_row0(const StepArgs& a) {
+    return (a.order ? (int64_t)(*a.cur_batch) * a.row_base_mul : 0) + a.row_base_add;
+}
+
+// ----------------------------------------------------------------------------- P1
+struct PEnc {
+    StepArgs a;
+    const float* x;
+    int M, N, K;
+    DEV void prepare() { x = x_rows_p1(a); }
+    DEV f32x4 a4(int m, int k) const { return ld4_kc(x, a.D, m, k, a.Mb, a.D, (a.D & 3) == 0); }
+    DEV f32x4 b4(int n, int k, int) const { return ld4_mc(a.W3, a.H, n, k, a.H, a.D); }
+    template <int NB>
+    DEV void epilogue(int m0, int n0, const f32x4 (&acc)[NB]) const {
+        const int lane = threadIdx.x & 63;
+        if (a.order && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) *a.cur_batch = a.order[*a.cursor];
+        const int n = n0 + (lane & 15);
+        if (n >= a.H) return;
+        const float b = a.b3[n];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int m = m0 + 4 * (lane >> 4) + r;
+            a.h[(int64_t)m * a.H + n] = (m < a.Mb) ? tanhf(acc[0][r] + b) : 0.f;
+        }
+    }
+};
+
+// ----------------------------------------------------------------------------- P2
+struct PHeads {
+    StepArgs a;
+    int M, N, K;
+    DEV void prepare() {}
+    DEV f32x4 a4(int m, int k) const { return ld4_kc(a.h, a.H, m, k, a.Mbp, a.H, (a.H & 3) == 0); }
+    DEV f32x4 b4(int n, int k, int w) const { return ld4_mc(w ? a.W5 : a.W4, a.Z, n, k, a.Z, a.H); }
+    template <int NB>
+    DEV void epilogue(int m0, int n0, const f32x4 (&acc)[NB]) const {
+        const int lane = threadIdx.x & 63;
+        const int n = n0 + (lane & 15);
+        const bool ncol = n < a.Z;
+        const int ct = n0 >> 4;
+        const int64_t grow0 = global_row0(a);
+        const int64_t stp = a.step ? *a.step : 0;
+        const uint64_t c23 = (uint64_t)stp ^ ((uint64_t)a.domain << 63);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int m = m0 + 4 * (lane >> 4) + r;
+            const bool valid = ncol && m < a.Mb;
+            float mu = 0.f, lv = 0.f;
+            if (valid) { mu = acc[0][r] + a.b4[n]; lv = acc[NB - 1][r] + a.b5[n]; }
+            if (ncol) {
+                a.mu[(int64_t)m * a.Z + n] = mu;
+                a.lv[(int64_t)m * a.Z + n] = lv;
+            }
+            const float sd = expf(0.5f * lv);
+            float kl = valid ? 0.5f * (1.f + lv - mu * mu - expf(lv)) : 0.f;
+            for (int l = 0; l < a.L; ++l) {
+                float e = 0.f;
+                if (valid) {
+                    if (a.eps_mode == 0)
+                        e = philox_normal(a.seed, (uint32_t)(grow0 + m), (uint32_t)(l * a.Z + n), c23);
+                    else if (a.eps_mode == 1)
+                        e = a.eps_in[((int64_t)l * a.eps_in_ld + m) * a.Z + n];
+                }
+                const float z = valid ? mu + sd * e : 0.f;
+                if (ncol) {
+                    const int64_t o = ((int64_t)l * a.Mbp + m) * a.Z + n;
+                    a.eps[o] = e;
+                    a.z[o] = z;
+                }
+                if (a.est == EST_LA) {
+                    // (-1/2 log2pi - z^2/2) - (-1/2 log2pi - lv/2 - (z-mu)^2/(2 exp lv))
+                    const float d = z - mu;
+                    float f = valid ? (-0.5f * z * z) - (-0.5f * lv - 0.5f * d * d / expf(lv)) : 0.f;
+                    f = sum16(f);
+                    if ((lane & 15) == 0) a.la_part[((int64_t)l * a.Mbp + m) * a.nctZ + ct] = f;
+                }
+            }
+            if (a.est != EST_LA) {
+                kl = sum16(kl);
+                if ((lane & 15) == 0) a.kl_part[(int64_t)m * a.nctZ + ct] = kl;
+            }
+        }
+    }
+};
+
+// ----------------------------------------------------------------------------- P3
+struct PDecHid {
+    StepArgs a;
+    int M, N, K;
+    DEV void prepare() {}
+    DEV f32x4 a4(int m, int k) const { return ld4_kc(a.z, a.Z, m, k, a.Me, a.Z, (a.Z & 3) == 0); }
+    DEV f32x4 b4(int n, int k, int) const { return ld4_mc(a.W1, a.H, n, k, a.H, a.Z); }
+    template <int NB>
+    DEV void epilogue(int m0, int n0, const f32x4 (&acc)[NB]) const {
+        const int lane = threadIdx.x & 63;
+        const int n = n0 + (lane & 15);
+        if (n >= a.H) return;
+        const float b = a.b1[n];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int m = m0 + 4 * (lane >> 4) + r;
+            const bool valid = (m % a.Mbp) < a.Mb;
+            a.hd[(int64_t)m * a.H + n] = valid ? tanhf(acc[0][r] + b) : 0.f;
+        }
+    }
+};
+
+// ----------------------------------------------------------------------------- P4
+struct PDecOut {
+    StepArgs a;
+    const float* x;
+    int M, N, K;
+    DEV void prepare() { x = x_rows(a); }
+    DEV f32x4 a4(int m, int k) const { return ld4_kc(a.hd, a.H, m, k, a.Me, a.H, (a.H & 3) == 0); }
+    DEV f32x4 b4(int n, int k, int w) const { return ld4_mc(w ? a.W6 : a.W2, a.D, n, k, a.D, a.H); }
+    template <int NB>
+    DEV void epilogue(int m0, int n0, const f32x4 (&acc)[NB]) const {
+        const int lane = threadIdx.x & 63;
+        const int n = n0 + (lane & 15);
+        const bool ncol = n < a.D;
+        const int ct = n0 >> 4;
+        const float sl = a.sc / (float)a.L;
+        const float b2 = ncol ? a.b2[n] : 0.f;
+        const float b6 = (ncol && a.dec == DEC_GAUSSIAN) ? a.b6[n] : 0.f;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int m = m0 + 4 * (lane >> 4) + r;
+            const int i = m % a.Mbp;
+            const bool valid = ncol && i < a.Mb;
+            float lp = 0.f, d2 = 0.f, d6 = 0.f, yv = 0.f;
+            if (valid) {
+                const float xv = x[(int64_t)i * a.D + n];
+                const float a2 = acc[0][r] + b2;
+                yv = sigmoidf(a2);
+                if (a.dec == DEC_GAUSSIAN) {
+                    const float a6 = acc[NB - 1][r] + b6;
+                    const float rr = xv - yv;
+                    const float e = expf(-a6);
+                    lp = -kHalfLog2Pi - 0.5f * a6 - 0.5f * rr * rr * e;
+                    d2 = rr * e * yv * (1.f - yv) * sl;
+                    d6 = (-0.5f + 0.5f * rr * rr * e) * sl;
+                } else {
+                    lp = xv * a2 - softplusf(a2);
+                    d2 = (xv - yv) * sl;
+                }
+            }
+            if (ncol) {
+                const int64_t o = (int64_t)m * a.D + n;
+                if (a.mode == MODE_TRAIN) {
+                    a.dA2[o] = d2;
+                    if (a.dec == DEC_GAUSSIAN) a.dA6[o] = d6;
+                } else if (a.mode == MODE_RECON) {
+                    a.y[o] = yv;
+                }
+            }
+            lp = sum16(lp);
+            if ((lane & 15) == 0) a.lp_part[(int64_t)m * a.nctD + ct] = lp;
+        }
+    }
+};
+
+// ----------------------------------------------------------------------------- P5
+struct PDhd {
+    StepArgs a;
+    int M, N, K;  // K = D (Bernoulli) or 2D (Gaussian: [dA2|dA6] . [W2|W6]^T)
+    DEV void prepare() {}
+    // k in [D, 2D) addresses the Gaussian half; chunks past K read zeros.
+    DEV f32x4 a4(int m, int k) const {
+        if (k < a.D) return ld4_kc(a.dA2, a.D, m, k, a.Me, a.D, (a.D & 3) == 0);
+        if (k >= K) return zero4();
+        return ld4_kc(a.dA6, a.D, m, k - a.D, a.Me, a.D, (a.D & 3) == 0);
+    }
+    DEV f32x4 b4(int n, int k, int) const {
+        if (k < a.D) return ld4_kc(a.W2, a.D, n, k, a.H, a.D, (a.D & 3) == 0);
+        if (k >= K) return zero4();
+        return ld4_kc(a.W6, a.D, n, k - a.D, a.H, a.D, (a.D & 3) == 0);
+    }
+    template <int NB>
+    DEV void epilogue(int m0, int n0, const f32x4 (&acc)[NB]) const {
+        const int lane = threadIdx.x & 63;
+        const int n = n0 + (lane & 15);
+        if (n >= a.H) return;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int m = m0 + 4 * (lane >> 4) + r;
+            const int64_t o = (int64_t)m * a.H + n;
+            const float hd = a.hd[o];
+            a.dA1[o] = ((m % a.Mbp) < a.Mb) ? acc[0][r] * (1.f - hd * hd) : 0.f;
+        }
+    }
+};
+
+// ----------------------------------------------------------------------------- P6
+struct PDz {
+    StepArgs a;
+    int M, N, K;
+    DEV void prepare() {}
+    DEV f32x4 a4(int m, int k) const { return ld4_kc(a.dA1, a.H, m, k, a.Me, a.H, (a.H & 3) == 0); }
+    DEV f32x4 b4(int n, int k, int) const { return ld4_kc(a.W1, a.H, n, k, a.Z, a.H, (a.H & 3) == 0); }
+    template <int NB>
+    DEV void epilogue(int m0, int n0, const f32x4 (&acc)[NB]) const {
+        const int lane = threadIdx.x & 63;
+        const int n = n0 + (lane & 15);
+        if (n >= a.Z) return;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int m = m0 + 4 * (lane >> 4) + r;
+            a.dZ[(int64_t)m * a.Z + n] = ((m % a.Mbp) < a.Mb) ? acc[0][r] : 0.f;
+        }
+    }
+};
+
+// ----------------------------------------------------------------------------- P7
+struct PDh {
+    StepArgs a;
+    int M, N, K;  // K = 2Z
+    DEV void prepare() {}
+    // [dMu | dLv](i, k) from dZ, mu, lv, eps, z (LA variant).
+    DEV float dmulv(int i, int k) const {
+        const int Z = a.Z;
+        const bool isv = k >= Z;
+        const int j = isv ? k - Z : k;
+        const int64_t o = (int64_t)i * Z + j;
+        const float mu = a.mu[o], lv = a.lv[o];
+        const float sd = expf(0.5f * lv);
+        const float sl = a.sc / (float)a.L;
+        float g = 0.f, t = 0.f;
+        for (int l = 0; l < a.L; ++l) {
+            const int64_t ol = ((int64_t)l * a.Mbp + i) * Z + j;
+            const float dz = a.dZ[ol];
+            const float e = a.eps[ol];
+            if (!isv) {
+                g += dz;
+                if (a.est == EST_LA) t += -a.z[ol];
+            } else {
+                g += dz * 0.5f * sd * e;
+                if (a.est == EST_LA) t += 0.5f - 0.5f * a.z[ol] * sd * e;
+            }
+        }
+        if (a.est == EST_LA) return g + sl * t;
+        return isv ? g + a.sc * 0.5f * (1.f - expf(lv)) : g - a.sc * mu;
+    }
+    DEV f32x4 a4(int m, int k) const {
+        f32x4 v = zero4();
+        const int K2 = 2 * a.Z;
+        if (m < a.Mb) {
+            if (k + 0 < K2) v.x = dmulv(m, k + 0);
+            if (k + 1 < K2) v.y = dmulv(m, k + 1);
+            if (k + 2 < K2) v.z = dmulv(m, k + 2);
+            if (k + 3 < K2) v.w = dmulv(m, k + 3);
+        }
+        // the column-tile-0 wave publishes [dMu|dLv] (pad rows as 0) for the
+        // weight-gradient phase
+        if (m < a.Mbp && blockIdx.y == 0 && ((threadIdx.x >> 6) == 0)) {
+            float* o = a.dMuLv + (int64_t)m * K2;
+            if (k + 0 < K2) o[k + 0] = v.x;
+            if (k + 1 < K2) o[k + 1] = v.y;
+            if (k + 2 < K2) o[k + 2] = v.z;
+            if (k + 3 < K2) o[k + 3] = v.w;
+        }
+        return v;
+    }
+    DEV f32x4 b4(int n, int k, int) const {
+        f32x4 v = zero4();
+        if (n >= a.H) return v;
+        const int Z = a.Z;
+        float t[4];
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            const int kk = k + s;
+            t[s] = kk < Z ? a.W4[(int64_t)n * Z + kk] : (kk < 2 * Z ? a.W5[(int64_t)n * Z + kk - Z] : 0.f);
+        }
+        v.x = t[0]; v.y = t[1]; v.z = t[2]; v.w = t[3];
+        return v;
+    }
+    template <int NB>
+    DEV void epilogue(int m0, int n0, const f32x4 (&acc)[NB]) const {
+        const int lane = threadIdx.x & 63;
+        const int n = n0 + (lane & 15);
+        if (n >= a.H) return;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int m = m0 + 4 * (lane >> 4) + r;
+            const int64_t o = (int64_t)m * a.H + n;
+            const float h = a.h[o];
+            a.dA3[o] = (m < a.Mb) ? acc[0][r] * (1.f - h * h) : 0.f;
+        }
+    }
+};
+
+}  // namespace vaeb

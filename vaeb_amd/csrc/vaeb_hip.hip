@@ -1,0 +1,757 @@
+// vaeb_hip.hip -- C ABI (include/vaeb_hip.h) over the gfx950 SGVB step kernels.
+//
+// One context = one GPU (one rank).  All state lives in device memory owned here:
+// a flat parameter arena in the reference order (VAEB.py:111-115) with matching
+// Adagrad-accumulator and gradient arenas, the device-resident training set
+// (th.shared x_train, VAEB.py:184), activation/delta buffers, and a small control
+// block (batch order, cursor, Philox step, ELBO accumulators) so a step needs no host
+// round trip and can be replayed as a hipGraph.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/vaeb_hip.h"
+#include "kernels_aux.hpp"
+
+using namespace vaeb;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                      \
+    do {                                                                                   \
+        hipError_t e_ = (expr);                                                            \
+        if (e_ != hipSuccess)                                                              \
+            return fail(VAEB_ERR_HIP, "%s failed: %s (%s:%d)", #expr, hipGetErrorString(e_), \
+                        __FILE__, __LINE__);                                               \
+    } while (0)
+
+#define CHECK_LAUNCH()                                                                     \
+    do {                                                                                   \
+        hipError_t e_ = hipGetLastError();                                                 \
+        if (e_ != hipSuccess)                                                              \
+            return fail(VAEB_ERR_HIP, "kernel launch failed: %s (%s:%d)",                  \
+                        hipGetErrorString(e_), __FILE__, __LINE__);                        \
+    } while (0)
+
+inline int r16(int x) { return (x + 15) & ~15; }
+inline int cdiv(int64_t a, int64_t b) { return (int)((a + b - 1) / b); }
+
+// Control block layout (ints): [0] cursor, [1] resolved batch, [2..] batch order.
+constexpr int kOrderCap = 1 << 20;
+constexpr int kFvParts = 512;
+constexpr int kGraphSteps = 32;
+constexpr int kMaxProfKernels = 16;
+
+const char* kKernelNames[] = {"p1_enc", "p2_heads", "p3_dechid", "p4_decout", "p5_dhd", "p6_dz",
+                              "p7_dh", "p8_wgrad", "allreduce", "adagrad", "fv_update", "elbo"};
+
+}  // namespace
+
+struct vaeb_ctx {
+    vaeb_config c{};
+    hipStream_t s = nullptr;
+    int64_t P = 0;
+    int nparams = 0;
+    int64_t off[12] = {};   // arena offsets, reference order
+    // arenas
+    float *theta = nullptr, *acc = nullptr, *grad = nullptr;
+    float *fvmu = nullptr, *fvsg = nullptr, *fvam = nullptr, *fvas = nullptr, *fv_part = nullptr;
+    // data
+    float* data = nullptr;
+    int64_t nrows = 0;
+    float* xeval = nullptr;
+    // control
+    int* ictl = nullptr;          // cursor, cur_batch, order[kOrderCap]
+    int64_t* step = nullptr;
+    float* elbo_out = nullptr;
+    double* epoch = nullptr;      // [2]
+    double* eval_acc = nullptr;   // [2]
+    // noise
+    int eps_mode = VAEB_EPS_PHILOX;
+    uint64_t seed = 10;
+    float* eps_in = nullptr;
+    int64_t eps_in_cap = 0, eps_rows = 0;
+    // activations
+    int cap = 0;                  // padded row capacity (per l plane)
+    float *h = nullptr, *mu = nullptr, *lv = nullptr, *eps = nullptr, *z = nullptr, *hd = nullptr,
+          *y = nullptr, *dA2 = nullptr, *dA6 = nullptr, *dA1 = nullptr, *dZ = nullptr,
+          *dMuLv = nullptr, *dA3 = nullptr, *kl_part = nullptr, *lp_part = nullptr;
+    // host staging (pinned)
+    int* h_ctl = nullptr;
+    float* h_elbo = nullptr;
+    double* h_d2 = nullptr;
+    hipEvent_t ctl_ev = nullptr;
+    // graphs
+    hipGraphExec_t g1 = nullptr, gS = nullptr;
+    bool graph_failed = false;
+    // comm
+    ncclComm_t comm = nullptr;
+    int rank = 0, world = 1;
+    // profiling
+    hipEvent_t pev[kMaxProfKernels + 1] = {};
+    int prof_n = 0;
+    std::vector<int> prof_ids;
+};
+
+namespace {
+
+bool gaussian(const vaeb_ctx* c) { return c->c.decoder == VAEB_DEC_GAUSSIAN; }
+
+StepArgs make_args(vaeb_ctx* c, int Mb, int mode, const float* xbase, bool train) {
+    StepArgs a{};
+    const vaeb_config& g = c->c;
+    a.D = g.D; a.H = g.H; a.Z = g.Z; a.L = g.L;
+    a.Mb = Mb; a.Mbp = r16(Mb); a.Me = g.L * a.Mbp;
+    a.dec = g.decoder; a.est = g.estimator; a.mode = mode;
+    a.sc = (g.objective == VAEB_OBJ_MEAN_MAP) ? 1.0f / (float)g.B_global : 1.0f;
+    const float* t = c->theta;
+    const bool gs = gaussian(c);
+    // reference order: W3,W4,W5,W1,W2,(W6),b3,b4,b5,b1,b2,(b6)
+    a.W3 = t + c->off[0]; a.W4 = t + c->off[1]; a.W5 = t + c->off[2]; a.W1 = t + c->off[3];
+    a.W2 = t + c->off[4];
+    const int bo = gs ? 6 : 5;
+    a.W6 = gs ? t + c->off[5] : nullptr;
+    a.b3 = t + c->off[bo + 0]; a.b4 = t + c->off[bo + 1]; a.b5 = t + c->off[bo + 2];
+    a.b1 = t + c->off[bo + 3]; a.b2 = t + c->off[bo + 4];
+    a.b6 = gs ? t + c->off[bo + 5] : nullptr;
+    a.xbase = xbase;
+    if (train) {
+        a.order = c->ictl + 2;
+        a.cursor = c->ictl;
+        a.cur_batch = c->ictl + 1;
+        a.batch_stride = (int64_t)g.B_global * g.D;
+        a.row_base_mul = g.B_global;
+        a.row_base_add = g.row_offset;
+        a.domain = 0;
+    } else {
+        a.order = nullptr; a.cursor = nullptr; a.cur_batch = c->ictl + 1;
+        a.batch_stride = 0; a.row_base_mul = 0; a.row_base_add = 0;
+        a.domain = 1;
+    }
+    a.eps_mode = (mode == MODE_RECON) ? 2 : (c->eps_mode == VAEB_EPS_HOST ? 1 : 0);
+    a.seed = c->seed;
+    a.step = c->step;
+    a.eps_in = c->eps_in;
+    a.eps_in_ld = c->eps_rows;
+    a.h = c->h; a.mu = c->mu; a.lv = c->lv; a.eps = c->eps; a.z = c->z; a.hd = c->hd; a.y = c->y;
+    a.dA2 = c->dA2; a.dA6 = c->dA6; a.dA1 = c->dA1; a.dZ = c->dZ; a.dMuLv = c->dMuLv; a.dA3 = c->dA3;
+    a.kl_part = c->kl_part; a.la_part = c->kl_part; a.lp_part = c->lp_part;
+    a.nctZ = cdiv(g.Z, 16);
+    a.nctD = cdiv(g.D, 16);
+    return a;
+}
+
+template <int WM, int WN, int KS, int NB, class P>
+void launch_tile(hipStream_t s, const P& p) {
+    dim3 grid(cdiv(p.M, 16 * WM), cdiv(p.N, 16 * WN));
+    hipLaunchKernelGGL((tile_kernel<WM, WN, KS, NB, P>), grid, dim3(256), 0, s, p);
+}
+
+struct Prof {
+    vaeb_ctx* c;
+    bool on;
+    int k = 0;
+    void mark(int id) {
+        if (!on) return;
+        hipEventRecord(c->pev[k], c->s);
+        if (k < (int)c->prof_ids.size()) c->prof_ids[k] = id; else c->prof_ids.push_back(id);
+        ++k;
+    }
+};
+
+ElboArgs base_elbo(vaeb_ctx* c, const StepArgs& a) {
+    ElboArgs e{};
+    e.lp_part = c->lp_part; e.n_lp = (int64_t)a.Me * a.nctD;
+    e.kl_part = c->kl_part;
+    e.n_kl = (int64_t)(c->c.estimator == VAEB_EST_LA ? a.Me : a.Mbp) * a.nctZ;
+    e.L = c->c.L; e.est = c->c.estimator;
+    e.data_mul = 1.0;
+    e.inv_bglob = 1.0 / (double)c->c.B_global;
+    return e;
+}
+
+// Forward phases P1..P4 for any mode.
+int enqueue_forward(vaeb_ctx* c, const StepArgs& a, Prof& pr) {
+    hipStream_t s = c->s;
+    pr.mark(0);
+    launch_tile<1, 1, 4, 1>(s, PEnc{a, nullptr, a.Mbp, a.H, a.D});
+    CHECK_LAUNCH();
+    pr.mark(1);
+    launch_tile<1, 1, 4, 2>(s, PHeads{a, a.Mbp, a.Z, a.H});
+    CHECK_LAUNCH();
+    pr.mark(2);
+    launch_tile<1, 4, 1, 1>(s, PDecHid{a, a.Me, a.H, a.Z});
+    CHECK_LAUNCH();
+    pr.mark(3);
+    if (gaussian(c)) launch_tile<1, 1, 4, 2>(s, PDecOut{a, nullptr, a.Me, a.D, a.H});
+    else launch_tile<1, 1, 4, 1>(s, PDecOut{a, nullptr, a.Me, a.D, a.H});
+    CHECK_LAUNCH();
+    return 0;
+}
+
+OptArgs make_opt(vaeb_ctx* c, bool update, bool store) {
+    OptArgs o{};
+    o.theta = c->theta; o.acc = c->acc; o.grad = c->grad;
+    o.lr = c->c.lr; o.eps = c->c.adagrad_eps;
+    const bool mean = c->c.objective == VAEB_OBJ_MEAN_MAP;
+    o.prior = mean ? 0.f : 1.f;
+    o.decay = mean ? c->c.lr * c->c.adagrad_eps : 0.f;
+    o.update = update ? 1 : 0;
+    o.store_grad = store ? 1 : 0;
+    return o;
+}
+
+int enqueue_train_step(vaeb_ctx* c, bool prof) {
+    Prof pr{c, prof};
+    const vaeb_config& g = c->c;
+    hipStream_t s = c->s;
+    StepArgs a = make_args(c, g.B, g.estimator == VAEB_EST_FV ? MODE_EVAL : MODE_TRAIN, c->data, true);
+    if (int rc = enqueue_forward(c, a, pr)) return rc;
+    ElboArgs e = base_elbo(c, a);
+    e.elbo_out = c->elbo_out; e.epoch = c->epoch; e.cursor = c->ictl; e.step = c->step;
+
+    if (g.estimator == VAEB_EST_FV) {
+        pr.mark(10);
+        hipLaunchKernelGGL(fv_kernel, dim3(kFvParts), dim3(256), 0, s, c->fvmu, c->fvsg, c->fvam, c->fvas,
+                           c->P, g.lr, g.adagrad_eps, 1, c->fv_part);
+        CHECK_LAUNCH();
+        pr.mark(11);
+        e.fv_part = c->fv_part; e.n_fv = kFvParts;
+        e.data_mul = (double)g.B;
+        hipLaunchKernelGGL(elbo_kernel, dim3(1), dim3(256), 0, s, e);
+        CHECK_LAUNCH();
+        pr.mark(-1);
+        c->prof_n = pr.k;
+        return 0;
+    }
+    pr.mark(4);
+    launch_tile<1, 1, 4, 1>(s, PDhd{a, a.Me, a.H, gaussian(c) ? 2 * a.D : a.D});
+    CHECK_LAUNCH();
+    pr.mark(5);
+    launch_tile<1, 1, 4, 1>(s, PDz{a, a.Me, a.Z, a.H});
+    CHECK_LAUNCH();
+    pr.mark(6);
+    launch_tile<1, 4, 1, 1>(s, PDh{a, a.Mbp, a.H, 2 * a.Z});
+    CHECK_LAUNCH();
+
+    // P8: grouped weight gradients (+ fused prior/Adagrad when single rank)
+    const bool dp = c->comm != nullptr && c->world > 1;
+    WGradArgs w{};
+    const int bo = gaussian(c) ? 6 : 5;
+    auto add = [&](int gi, const float* at, int ld_at, int klim, int at_is_x, int rowsW, const float* b0,
+                   const float* b1, int ld_b, int nb, int N, int K, int pW0, int pb0, int pW1, int pb1) {
+        WGroup& G = w.g[gi];
+        G.at = at; G.ld_at = ld_at; G.klim_at = klim; G.at_is_x = at_is_x; G.rowsW = rowsW;
+        G.bm0 = b0; G.bm1 = b1; G.ld_b = ld_b; G.nb = nb; G.N = N; G.K = K;
+        G.offW0 = c->off[pW0]; G.offb0 = c->off[pb0];
+        G.offW1 = pW1 >= 0 ? c->off[pW1] : 0; G.offb1 = pb1 >= 0 ? c->off[pb1] : 0;
+        G.tiles_n = cdiv(N, 32);
+        const int tiles_m = cdiv(rowsW + 1, 32);
+        G.wg_begin = gi == 0 ? 0 : w.g[gi - 1].wg_end;
+        G.wg_end = G.wg_begin + tiles_m * G.tiles_n;
+    };
+    // G4 first: the largest group ([hd|1]^T [dA2 (|dA6)]) -> W2,b2 (W6,b6)
+    add(0, c->hd, a.H, a.Me, 0, a.H, c->dA2, gaussian(c) ? c->dA6 : nullptr, a.D, gaussian(c) ? 2 : 1,
+        a.D, a.Me, 4, bo + 4, gaussian(c) ? 5 : -1, gaussian(c) ? bo + 5 : -1);
+    // G1: [X|1]^T dA3 -> W3,b3
+    add(1, nullptr, a.D, a.Mb, 1, a.D, c->dA3, nullptr, a.H, 1, a.H, a.Mbp, 0, bo + 0, -1, -1);
+    // G3: [z|1]^T dA1 -> W1,b1
+    add(2, c->z, a.Z, a.Me, 0, a.Z, c->dA1, nullptr, a.H, 1, a.H, a.Me, 3, bo + 3, -1, -1);
+    // G2: [h|1]^T [dMu|dLv] -> (W4,b4), (W5,b5)
+    add(3, c->h, a.H, a.Mbp, 0, a.H, c->dMuLv, c->dMuLv + a.Z, 2 * a.Z, 2, a.Z, a.Mbp, 1, bo + 1, 2, bo + 2);
+    w.ngroups = 4;
+    w.total_wgs = w.g[3].wg_end;
+    w.opt = make_opt(c, !dp, dp || g.keep_grads != 0);
+    w.elbo = e;
+    if (dp) { w.elbo.dp_slot = c->grad + c->P; w.elbo.elbo_out = nullptr; w.elbo.cursor = nullptr; w.elbo.step = nullptr; }
+    w.xbase = c->data; w.cur_batch = c->ictl + 1; w.batch_stride = a.batch_stride;
+    pr.mark(7);
+    hipLaunchKernelGGL(wgrad_kernel, dim3(w.total_wgs + 1), dim3(256), 0, s, w);
+    CHECK_LAUNCH();
+    if (dp) {
+        pr.mark(8);
+        ncclResult_t r = ncclAllReduce(c->grad, c->grad, (size_t)c->P + 1, ncclFloat, ncclSum, c->comm, s);
+        if (r != ncclSuccess) return fail(VAEB_ERR_COMM, "ncclAllReduce: %s", ncclGetErrorString(r));
+        pr.mark(9);
+        OptArgs o = make_opt(c, true, false);
+        ElboArgs e2 = e;
+        hipLaunchKernelGGL(adagrad_kernel, dim3(512), dim3(256), 0, s, o, c->P, e2);
+        CHECK_LAUNCH();
+    }
+    pr.mark(-1);
+    c->prof_n = pr.k;
+    return 0;
+}
+
+void free_graphs(vaeb_ctx* c) {
+    if (c->g1) hipGraphExecDestroy(c->g1);
+    if (c->gS) hipGraphExecDestroy(c->gS);
+    c->g1 = c->gS = nullptr;
+}
+
+int capture(vaeb_ctx* c, int nsteps, hipGraphExec_t* out) {
+    hipGraph_t gr = nullptr;
+    HIP_TRY(hipStreamBeginCapture(c->s, hipStreamCaptureModeThreadLocal));
+    int rc = 0;
+    for (int i = 0; i < nsteps && rc == 0; ++i) rc = enqueue_train_step(c, false);
+    hipError_t e = hipStreamEndCapture(c->s, &gr);
+    if (rc) { if (gr) hipGraphDestroy(gr); return rc; }
+    if (e != hipSuccess) return fail(VAEB_ERR_HIP, "hipStreamEndCapture: %s", hipGetErrorString(e));
+    e = hipGraphInstantiate(out, gr, nullptr, nullptr, 0);
+    hipGraphDestroy(gr);
+    if (e != hipSuccess) return fail(VAEB_ERR_HIP, "hipGraphInstantiate: %s", hipGetErrorString(e));
+    return 0;
+}
+
+// Enqueue n steps (graph replay when enabled, else eager launches).
+int run_steps(vaeb_ctx* c, int n) {
+    if (c->c.use_graph && !c->graph_failed) {
+        if (!c->g1) {
+            int rc = capture(c, 1, &c->g1);
+            if (rc == 0 && !c->gS) rc = capture(c, kGraphSteps, &c->gS);
+            if (rc) { c->graph_failed = true; free_graphs(c); hipGetLastError(); }
+        }
+        if (!c->graph_failed) {
+            int i = 0;
+            for (; i + kGraphSteps <= n; i += kGraphSteps) HIP_TRY(hipGraphLaunch(c->gS, c->s));
+            for (; i < n; ++i) HIP_TRY(hipGraphLaunch(c->g1, c->s));
+            return 0;
+        }
+    }
+    for (int i = 0; i < n; ++i)
+        if (int rc = enqueue_train_step(c, false)) return rc;
+    return 0;
+}
+
+// Upload a batch order (cursor reset to 0) through the pinned staging buffer.
+int upload_order(vaeb_ctx* c, const int32_t* idx, int n) {
+    HIP_TRY(hipEventSynchronize(c->ctl_ev));
+    c->h_ctl[0] = 0;
+    c->h_ctl[1] = 0;
+    memcpy(c->h_ctl + 2, idx, sizeof(int) * (size_t)n);
+    HIP_TRY(hipMemcpyAsync(c->ictl, c->h_ctl, sizeof(int) * (size_t)(n + 2), hipMemcpyHostToDevice, c->s));
+    HIP_TRY(hipEventRecord(c->ctl_ev, c->s));
+    return 0;
+}
+
+int check_batches(vaeb_ctx* c, const int32_t* idx, int n) {
+    if (!c->data) return fail(VAEB_ERR_STATE, "vaeb_set_data has not been called");
+    const int64_t nb = c->nrows / c->c.B_global;
+    for (int i = 0; i < n; ++i)
+        if (idx[i] < 0 || idx[i] >= nb)
+            return fail(VAEB_ERR_ARG, "batch index %d out of range [0, %lld)", idx[i], (long long)nb);
+    return 0;
+}
+
+template <class T>
+int dalloc(T** p, size_t n) {
+    if (n == 0) n = 1;
+    hipError_t e = hipMalloc((void**)p, n * sizeof(T));
+    if (e != hipSuccess) return fail(VAEB_ERR_NOMEM, "hipMalloc(%zu) failed: %s", n * sizeof(T), hipGetErrorString(e));
+    hipMemset(*p, 0, n * sizeof(T));
+    return 0;
+}
+
+}  // namespace
+
+// =========================================================================== C ABI
+extern "C" {
+
+const char* vaeb_last_error(void) { return g_err.c_str(); }
+
+int vaeb_version(int32_t* major, int32_t* minor) {
+    if (major) *major = 0;
+    if (minor) *minor = 1;
+    return 0;
+}
+
+int vaeb_create(const vaeb_config* cfg, vaeb_ctx** out) {
+    if (!cfg || !out) return fail(VAEB_ERR_ARG, "null argument");
+    const vaeb_config& g = *cfg;
+    if (g.D <= 0 || g.H <= 0 || g.Z <= 0 || g.B <= 0 || g.L <= 0)
+        return fail(VAEB_ERR_ARG, "dimensions must be positive (D=%d H=%d Z=%d B=%d L=%d)", g.D, g.H, g.Z, g.B, g.L);
+    if (g.decoder < 0 || g.decoder > 1 || g.estimator < 0 || g.estimator > 2 || g.objective < 0 || g.objective > 1)
+        return fail(VAEB_ERR_ARG, "bad decoder/estimator/objective enum");
+    if (g.estimator == VAEB_EST_FV && g.L != 1)
+        return fail(VAEB_ERR_ARG, "the literal full-variational estimator supports L == 1 only (VAEB.py:361)");
+    auto* c = new vaeb_ctx();
+    c->c = g;
+    if (c->c.B_global <= 0) c->c.B_global = g.B;
+    if (c->c.adagrad_eps <= 0.f) c->c.adagrad_eps = 1e-6f;
+    if (c->c.max_eval_rows <= 0) c->c.max_eval_rows = 10000;
+    hipError_t e = hipSetDevice(g.device);
+    if (e != hipSuccess) { delete c; return fail(VAEB_ERR_HIP, "hipSetDevice(%d): %s", g.device, hipGetErrorString(e)); }
+    e = hipStreamCreateWithFlags(&c->s, hipStreamNonBlocking);
+    if (e != hipSuccess) { delete c; return fail(VAEB_ERR_HIP, "hipStreamCreate: %s", hipGetErrorString(e)); }
+    const int64_t D = g.D, H = g.H, Z = g.Z;
+    std::vector<int64_t> sz = {D * H, H * Z, H * Z, Z * H, H * D};
+    if (gaussian(c)) sz.push_back(H * D);
+    sz.insert(sz.end(), {H, Z, Z, H, D});
+    if (gaussian(c)) sz.push_back(D);
+    c->nparams = (int)sz.size();
+    int64_t o = 0;
+    for (int i = 0; i < c->nparams; ++i) { c->off[i] = o; o += sz[i]; }
+    c->P = o;
+    c->cap = std::max(r16(g.B), r16(c->c.max_eval_rows));
+    const int64_t R = c->cap, RL = (int64_t)c->cap * g.L;
+    int rc = 0;
+    rc = rc ? rc : dalloc(&c->theta, c->P);
+    rc = rc ? rc : dalloc(&c->acc, c->P);
+    rc = rc ? rc : dalloc(&c->grad, c->P + 1);
+    if (g.estimator == VAEB_EST_FV) {
+        rc = rc ? rc : dalloc(&c->fvmu, c->P);
+        rc = rc ? rc : dalloc(&c->fvsg, c->P);
+        rc = rc ? rc : dalloc(&c->fvam, c->P);
+        rc = rc ? rc : dalloc(&c->fvas, c->P);
+    }
+    rc = rc ? rc : dalloc(&c->fv_part, kFvParts);
+    rc = rc ? rc : dalloc(&c->xeval, (size_t)R * D);
+    rc = rc ? rc : dalloc(&c->ictl, kOrderCap + 2);
+    rc = rc ? rc : dalloc(&c->step, 1);
+    rc = rc ? rc : dalloc(&c->elbo_out, 1);
+    rc = rc ? rc : dalloc(&c->epoch, 2);
+    rc = rc ? rc : dalloc(&c->eval_acc, 2);
+    rc = rc ? rc : dalloc(&c->h, (size_t)R * H);
+    rc = rc ? rc : dalloc(&c->mu, (size_t)R * Z);
+    rc = rc ? rc : dalloc(&c->lv, (size_t)R * Z);
+    rc = rc ? rc : dalloc(&c->eps, (size_t)RL * Z);
+    rc = rc ? rc : dalloc(&c->z, (size_t)RL * Z);
+    rc = rc ? rc : dalloc(&c->hd, (size_t)RL * H);
+    rc = rc ? rc : dalloc(&c->y, (size_t)RL * D);
+    rc = rc ? rc : dalloc(&c->dA2, (size_t)RL * D);
+    if (gaussian(c)) rc = rc ? rc : dalloc(&c->dA6, (size_t)RL * D);
+    rc = rc ? rc : dalloc(&c->dA1, (size_t)RL * H);
+    rc = rc ? rc : dalloc(&c->dZ, (size_t)RL * Z);
+    rc = rc ? rc : dalloc(&c->dMuLv, (size_t)R * 2 * Z);
+    rc = rc ? rc : dalloc(&c->dA3, (size_t)R * H);
+    rc = rc ? rc : dalloc(&c->kl_part, (size_t)RL * cdiv(Z, 16));
+    rc = rc ? rc : dalloc(&c->lp_part, (size_t)RL * cdiv(D, 16));
+    if (rc) { vaeb_destroy(c); return rc; }
+    if (hipHostMalloc((void**)&c->h_ctl, sizeof(int) * (kOrderCap + 2), 0) != hipSuccess ||
+        hipHostMalloc((void**)&c->h_elbo, sizeof(float) * 4, 0) != hipSuccess ||
+        hipHostMalloc((void**)&c->h_d2, sizeof(double) * 4, 0) != hipSuccess) {
+        vaeb_destroy(c);
+        return fail(VAEB_ERR_NOMEM, "hipHostMalloc failed");
+    }
+    hipEventCreateWithFlags(&c->ctl_ev, hipEventDisableTiming);
+    hipEventRecord(c->ctl_ev, c->s);
+    for (auto& ev : c->pev) hipEventCreate(&ev);
+    if (hipDeviceSynchronize() != hipSuccess) { vaeb_destroy(c); return fail(VAEB_ERR_HIP, "device init failed"); }
+    *out = c;
+    return 0;
+}
+
+int vaeb_destroy(vaeb_ctx* c) {
+    if (!c) return 0;
+    if (c->s) hipStreamSynchronize(c->s);
+    free_graphs(c);
+    if (c->comm) ncclCommDestroy(c->comm);
+    float* fp[] = {c->theta, c->acc, c->grad, c->fvmu, c->fvsg, c->fvam, c->fvas, c->fv_part, c->data, c->xeval,
+                   c->elbo_out, c->eps_in, c->h, c->mu, c->lv, c->eps, c->z, c->hd, c->y, c->dA2, c->dA6, c->dA1,
+                   c->dZ, c->dMuLv, c->dA3, c->kl_part, c->lp_part};
+    for (float* p : fp) if (p) hipFree(p);
+    if (c->ictl) hipFree(c->ictl);
+    if (c->step) hipFree(c->step);
+    if (c->epoch) hipFree(c->epoch);
+    if (c->eval_acc) hipFree(c->eval_acc);
+    if (c->h_ctl) hipHostFree(c->h_ctl);
+    if (c->h_elbo) hipHostFree(c->h_elbo);
+    if (c->h_d2) hipHostFree(c->h_d2);
+    if (c->ctl_ev) hipEventDestroy(c->ctl_ev);
+    for (auto& ev : c->pev) if (ev) hipEventDestroy(ev);
+    if (c->s) hipStreamDestroy(c->s);
+    delete c;
+    return 0;
+}
+
+int vaeb_num_params(const vaeb_ctx* c, int64_t* n) {
+    if (!c || !n) return fail(VAEB_ERR_ARG, "null argument");
+    *n = c->P;
+    return 0;
+}
+
+int vaeb_set_data(vaeb_ctx* c, const float* x, int64_t n_rows) {
+    if (!c || !x || n_rows <= 0) return fail(VAEB_ERR_ARG, "bad data arguments");
+    HIP_TRY(hipStreamSynchronize(c->s));
+    if (c->data) { hipFree(c->data); c->data = nullptr; }
+    free_graphs(c);  // graphs hold the data pointer
+    c->graph_failed = false;
+    if (int rc = dalloc(&c->data, (size_t)n_rows * c->c.D)) return rc;
+    HIP_TRY(hipMemcpy(c->data, x, sizeof(float) * (size_t)n_rows * c->c.D, hipMemcpyHostToDevice));
+    c->nrows = n_rows;
+    return 0;
+}
+
+static int xfer(vaeb_ctx* c, float* dev, const float* hin, float* hout, int64_t n, int64_t want) {
+    if (!c || (!hin && !hout)) return fail(VAEB_ERR_ARG, "null argument");
+    if (!dev) return fail(VAEB_ERR_STATE, "state not allocated for this estimator");
+    if (n != want) return fail(VAEB_ERR_ARG, "size mismatch: got %lld, expected %lld", (long long)n, (long long)want);
+    HIP_TRY(hipStreamSynchronize(c->s));
+    if (hin) HIP_TRY(hipMemcpy(dev, hin, sizeof(float) * n, hipMemcpyHostToDevice));
+    else HIP_TRY(hipMemcpy(hout, dev, sizeof(float) * n, hipMemcpyDeviceToHost));
+    return 0;
+}
+
+int vaeb_set_params(vaeb_ctx* c, const float* f, int64_t n) { return xfer(c, c ? c->theta : nullptr, f, nullptr, n, c ? c->P : 0); }
+int vaeb_get_params(vaeb_ctx* c, float* f, int64_t n) { return xfer(c, c ? c->theta : nullptr, nullptr, f, n, c ? c->P : 0); }
+int vaeb_set_adagrad_state(vaeb_ctx* c, const float* f, int64_t n) { return xfer(c, c ? c->acc : nullptr, f, nullptr, n, c ? c->P : 0); }
+int vaeb_get_adagrad_state(vaeb_ctx* c, float* f, int64_t n) { return xfer(c, c ? c->acc : nullptr, nullptr, f, n, c ? c->P : 0); }
+int vaeb_get_grads(vaeb_ctx* c, float* f, int64_t n) { return xfer(c, c ? c->grad : nullptr, nullptr, f, n, c ? c->P : 0); }
+
+int vaeb_set_fv_state(vaeb_ctx* c, const float* mu, const float* sg, const float* am, const float* as, int64_t n) {
+    int rc = 0;
+    rc = rc ? rc : xfer(c, c ? c->fvmu : nullptr, mu, nullptr, n, c ? c->P : 0);
+    rc = rc ? rc : xfer(c, c ? c->fvsg : nullptr, sg, nullptr, n, c ? c->P : 0);
+    rc = rc ? rc : xfer(c, c ? c->fvam : nullptr, am, nullptr, n, c ? c->P : 0);
+    rc = rc ? rc : xfer(c, c ? c->fvas : nullptr, as, nullptr, n, c ? c->P : 0);
+    return rc;
+}
+
+int vaeb_get_fv_state(vaeb_ctx* c, float* mu, float* sg, float* am, float* as, int64_t n) {
+    int rc = 0;
+    rc = rc ? rc : xfer(c, c ? c->fvmu : nullptr, nullptr, mu, n, c ? c->P : 0);
+    rc = rc ? rc : xfer(c, c ? c->fvsg : nullptr, nullptr, sg, n, c ? c->P : 0);
+    rc = rc ? rc : xfer(c, c ? c->fvam : nullptr, nullptr, am, n, c ? c->P : 0);
+    rc = rc ? rc : xfer(c, c ? c->fvas : nullptr, nullptr, as, n, c ? c->P : 0);
+    return rc;
+}
+
+int vaeb_set_eps_mode(vaeb_ctx* c, int32_t mode, uint64_t seed) {
+    if (!c || (mode != VAEB_EPS_PHILOX && mode != VAEB_EPS_HOST)) return fail(VAEB_ERR_ARG, "bad eps mode");
+    HIP_TRY(hipStreamSynchronize(c->s));
+    if (mode != c->eps_mode) { free_graphs(c); c->graph_failed = false; }
+    c->eps_mode = mode;
+    c->seed = seed;
+    return 0;
+}
+
+int vaeb_push_eps(vaeb_ctx* c, const float* eps, int64_t rows, int32_t L) {
+    if (!c || !eps || rows <= 0) return fail(VAEB_ERR_ARG, "bad eps arguments");
+    if (L != c->c.L) return fail(VAEB_ERR_ARG, "eps L=%d does not match the model L=%d", L, c->c.L);
+    const int64_t n = rows * L * c->c.Z;
+    HIP_TRY(hipStreamSynchronize(c->s));
+    if (n > c->eps_in_cap) {
+        if (c->eps_in) hipFree(c->eps_in);
+        c->eps_in = nullptr;
+        free_graphs(c);
+        c->graph_failed = false;
+        if (int rc = dalloc(&c->eps_in, (size_t)n)) return rc;
+        c->eps_in_cap = n;
+    }
+    if (rows != c->eps_rows) { free_graphs(c); c->graph_failed = false; }
+    c->eps_rows = rows;
+    HIP_TRY(hipMemcpy(c->eps_in, eps, sizeof(float) * n, hipMemcpyHostToDevice));
+    return 0;
+}
+
+int vaeb_set_step(vaeb_ctx* c, int64_t step) {
+    if (!c) return fail(VAEB_ERR_ARG, "null ctx");
+    HIP_TRY(hipStreamSynchronize(c->s));
+    HIP_TRY(hipMemcpy(c->step, &step, sizeof(step), hipMemcpyHostToDevice));
+    return 0;
+}
+
+static int host_eps_ready(vaeb_ctx* c, int64_t rows) {
+    if (c->eps_mode == VAEB_EPS_HOST && c->eps_rows != rows)
+        return fail(VAEB_ERR_STATE, "host eps mode: pushed %lld rows, step needs %lld (call vaeb_push_eps)",
+                    (long long)c->eps_rows, (long long)rows);
+    return 0;
+}
+
+int vaeb_update(vaeb_ctx* c, int32_t batch_index, float* out) {
+    if (!c) return fail(VAEB_ERR_ARG, "null ctx");
+    if (int rc = check_batches(c, &batch_index, 1)) return rc;
+    if (int rc = host_eps_ready(c, c->c.B)) return rc;
+    if (int rc = upload_order(c, &batch_index, 1)) return rc;
+    if (int rc = run_steps(c, 1)) return rc;
+    HIP_TRY(hipMemcpyAsync(c->h_elbo, c->elbo_out, sizeof(float), hipMemcpyDeviceToHost, c->s));
+    HIP_TRY(hipStreamSynchronize(c->s));
+    if (out) *out = c->h_elbo[0];
+    return 0;
+}
+
+int vaeb_update_many(vaeb_ctx* c, const int32_t* idx, int32_t n) {
+    if (!c || (!idx && n > 0) || n < 0) return fail(VAEB_ERR_ARG, "bad arguments");
+    if (int rc = check_batches(c, idx, n)) return rc;
+    if (int rc = host_eps_ready(c, c->c.B)) return rc;
+    for (int32_t done = 0; done < n;) {
+        const int32_t m = std::min<int32_t>(n - done, kOrderCap);
+        if (int rc = upload_order(c, idx + done, m)) return rc;
+        if (int rc = run_steps(c, m)) return rc;
+        done += m;
+    }
+    return 0;
+}
+
+int vaeb_update_async(vaeb_ctx* c, int32_t batch_index) { return vaeb_update_many(c, &batch_index, 1); }
+
+int vaeb_epoch_elbo(vaeb_ctx* c, double* out_sum, int64_t* out_steps) {
+    if (!c) return fail(VAEB_ERR_ARG, "null ctx");
+    HIP_TRY(hipMemcpyAsync(c->h_d2, c->epoch, 2 * sizeof(double), hipMemcpyDeviceToHost, c->s));
+    HIP_TRY(hipMemsetAsync(c->epoch, 0, 2 * sizeof(double), c->s));
+    HIP_TRY(hipStreamSynchronize(c->s));
+    if (out_sum) *out_sum = c->h_d2[0];
+    if (out_steps) *out_steps = (int64_t)c->h_d2[1];
+    return 0;
+}
+
+int vaeb_synchronize(vaeb_ctx* c) {
+    if (!c) return fail(VAEB_ERR_ARG, "null ctx");
+    HIP_TRY(hipStreamSynchronize(c->s));
+    return 0;
+}
+
+// Forward-only passes over host rows in device chunks (validate / reconstruct).
+static int eval_rows(vaeb_ctx* c, const float* x, int64_t n, int mode, float* out_y, double* out_sum) {
+    if (!c || !x || n <= 0) return fail(VAEB_ERR_ARG, "bad arguments");
+    if (mode == MODE_EVAL && c->eps_mode == VAEB_EPS_HOST && c->eps_rows != n)
+        return fail(VAEB_ERR_STATE, "host eps mode: validate needs eps for %lld rows (pushed %lld)", (long long)n,
+                    (long long)c->eps_rows);
+    const vaeb_config& g = c->c;
+    const int chunk = c->c.max_eval_rows;
+    HIP_TRY(hipMemsetAsync(c->eval_acc, 0, 2 * sizeof(double), c->s));
+    for (int64_t r0 = 0; r0 < n; r0 += chunk) {
+        const int rows = (int)std::min<int64_t>(chunk, n - r0);
+        HIP_TRY(hipMemcpyAsync(c->xeval, x + r0 * g.D, sizeof(float) * (size_t)rows * g.D, hipMemcpyHostToDevice, c->s));
+        StepArgs a = make_args(c, rows, mode, c->xeval, false);
+        a.row_base_add = r0;
+        a.eps_in = c->eps_in ? c->eps_in + r0 * g.Z : nullptr;
+        a.eps_in_ld = c->eps_rows;
+        Prof pr{c, false};
+        if (int rc = enqueue_forward(c, a, pr)) return rc;
+        if (mode == MODE_RECON) {
+            HIP_TRY(hipMemcpyAsync(out_y + r0 * g.D, c->y, sizeof(float) * (size_t)rows * g.D, hipMemcpyDeviceToHost, c->s));
+        } else {
+            ElboArgs e = base_elbo(c, a);
+            e.eval_acc = c->eval_acc;
+            hipLaunchKernelGGL(elbo_kernel, dim3(1), dim3(256), 0, c->s, e);
+            CHECK_LAUNCH();
+        }
+        HIP_TRY(hipStreamSynchronize(c->s));
+    }
+    if (mode == MODE_EVAL) {
+        double tp = 0.0;
+        if (g.estimator == VAEB_EST_FV) {
+            hipLaunchKernelGGL(fv_kernel, dim3(kFvParts), dim3(256), 0, c->s, c->fvmu, c->fvsg, c->fvam, c->fvas, c->P,
+                               g.lr, g.adagrad_eps, 0, c->fv_part);
+            CHECK_LAUNCH();
+            std::vector<float> parts(kFvParts);
+            HIP_TRY(hipMemcpyAsync(parts.data(), c->fv_part, sizeof(float) * kFvParts, hipMemcpyDeviceToHost, c->s));
+            HIP_TRY(hipStreamSynchronize(c->s));
+            for (float p : parts) tp += p;
+        }
+        HIP_TRY(hipMemcpy(c->h_d2, c->eval_acc, 2 * sizeof(double), hipMemcpyDeviceToHost));
+        const double data = c->h_d2[0];
+        // FV validate: x.shape[0] * (sum logp + sum KL) + thetaPrior (VAEB.py:364)
+        *out_sum = (g.estimator == VAEB_EST_FV) ? (double)n * data + tp : data;
+    }
+    return 0;
+}
+
+int vaeb_validate(vaeb_ctx* c, const float* x, int64_t n, double* out_sum) {
+    if (!out_sum) return fail(VAEB_ERR_ARG, "null out_sum");
+    return eval_rows(c, x, n, MODE_EVAL, nullptr, out_sum);
+}
+
+int vaeb_reconstruct(vaeb_ctx* c, const float* x, int64_t n, float* out_y) {
+    if (!out_y) return fail(VAEB_ERR_ARG, "null out_y");
+    return eval_rows(c, x, n, MODE_RECON, out_y, nullptr);
+}
+
+int vaeb_comm_unique_id(uint8_t out_id[128]) {
+    ncclUniqueId id;
+    ncclResult_t r = ncclGetUniqueId(&id);
+    if (r != ncclSuccess) return fail(VAEB_ERR_COMM, "ncclGetUniqueId: %s", ncclGetErrorString(r));
+    static_assert(sizeof(id) == 128, "ncclUniqueId is 128 bytes");
+    memcpy(out_id, &id, 128);
+    return 0;
+}
+
+int vaeb_comm_init(vaeb_ctx* c, const uint8_t id_bytes[128], int32_t rank, int32_t world) {
+    if (!c || !id_bytes || world <= 0 || rank < 0 || rank >= world) return fail(VAEB_ERR_ARG, "bad comm arguments");
+    if (c->c.estimator == VAEB_EST_FV && world > 1)
+        return fail(VAEB_ERR_ARG, "the literal full-variational path is single-rank");
+    HIP_TRY(hipSetDevice(c->c.device));
+    ncclUniqueId id;
+    memcpy(&id, id_bytes, 128);
+    ncclResult_t r = ncclCommInitRank(&c->comm, world, id, rank);
+    if (r != ncclSuccess) return fail(VAEB_ERR_COMM, "ncclCommInitRank: %s", ncclGetErrorString(r));
+    c->rank = rank;
+    c->world = world;
+    free_graphs(c);
+    c->graph_failed = false;
+    return 0;
+}
+
+static const struct { const char* name; int which; } kActs[] = {
+    {"h", 0}, {"mu", 1}, {"lv", 2}, {"eps", 3}, {"z", 4}, {"hd", 5}, {"dA2", 6}, {"dA6", 7},
+    {"dA1", 8}, {"dZ", 9}, {"dMuLv", 10}, {"dA3", 11}, {"y", 12}, {"kl_part", 13}, {"lp_part", 14}};
+
+int vaeb_get_activation(vaeb_ctx* c, const char* name, float* out, int64_t n) {
+    if (!c || !name || !out) return fail(VAEB_ERR_ARG, "null argument");
+    float* ptrs[] = {c->h, c->mu, c->lv, c->eps, c->z, c->hd, c->dA2, c->dA6, c->dA1, c->dZ, c->dMuLv, c->dA3, c->y,
+                     c->kl_part, c->lp_part};
+    for (auto& a : kActs)
+        if (strcmp(a.name, name) == 0) {
+            if (!ptrs[a.which]) return fail(VAEB_ERR_STATE, "activation %s not allocated", name);
+            HIP_TRY(hipStreamSynchronize(c->s));
+            HIP_TRY(hipMemcpy(out, ptrs[a.which], sizeof(float) * n, hipMemcpyDeviceToHost));
+            return 0;
+        }
+    return fail(VAEB_ERR_ARG, "unknown activation '%s'", name);
+}
+
+int vaeb_profile_steps(vaeb_ctx* c, int32_t n_steps, float* out_ms, int32_t* out_ids, int32_t max_k,
+                       int32_t* out_nk) {
+    if (!c || !out_ms || n_steps <= 0) return fail(VAEB_ERR_ARG, "bad arguments");
+    if (!c->data) return fail(VAEB_ERR_STATE, "no data");
+    std::vector<int32_t> order(n_steps);
+    const int64_t nb = c->nrows / c->c.B_global;
+    for (int i = 0; i < n_steps; ++i) order[i] = (int32_t)(i % nb);
+    if (int rc = upload_order(c, order.data(), n_steps)) return rc;
+    std::vector<double> tot(kMaxProfKernels, 0.0);
+    for (int it = 0; it < n_steps; ++it) {
+        if (int rc = enqueue_train_step(c, true)) return rc;
+        HIP_TRY(hipStreamSynchronize(c->s));
+        for (int k = 0; k + 1 < c->prof_n; ++k) {
+            float ms = 0.f;
+            HIP_TRY(hipEventElapsedTime(&ms, c->pev[k], c->pev[k + 1]));
+            tot[k] += ms;
+        }
+    }
+    const int nk = std::max(0, c->prof_n - 1);
+    for (int k = 0; k < nk && k < max_k; ++k) {
+        out_ms[k] = (float)(tot[k] / n_steps);
+        if (out_ids) out_ids[k] = c->prof_ids[k];
+    }
+    if (out_nk) *out_nk = nk;
+    return 0;
+}
+
+int vaeb_kernel_name(int32_t id, char* out, int32_t cap) {
+    if (!out || cap <= 0) return fail(VAEB_ERR_ARG, "bad buffer");
+    const int n = (int)(sizeof(kKernelNames) / sizeof(kKernelNames[0]));
+    if (id < 0 || id >= n) return fail(VAEB_ERR_ARG, "unknown kernel id %d", id);
+    snprintf(out, (size_t)cap, "%s", kKernelNames[id]);
+    return 0;
+}
+
+}  // extern "C"
