@@ -40,6 +40,8 @@ def phase_flops(D, H, Z, B, L=1, gaussian=False):
         "p6_dz": 2 * L * B * H * Z,
         "p7_dh": 2 * B * 2 * Z * H,
         "p8_wgrad": 2 * B * (D * H + H * 2 * Z) + 2 * L * B * (Z * H + H * D * g),
+        "p23_heads_dechid": 2 * B * H * 2 * Z + 2 * L * B * Z * H,
+        "p67_dz_dh": 2 * L * B * H * Z + 2 * B * 2 * Z * H,
     }
 
 

@@ -120,6 +120,10 @@ int vaeb_get_activation(vaeb_ctx* ctx, const char* name, float* out, int64_t n);
 int vaeb_profile_steps(vaeb_ctx* ctx, int32_t n_steps, float* out_ms_per_kernel,
                        int32_t* out_kernel_ids, int32_t max_kernels, int32_t* out_n_kernels);
 int vaeb_kernel_name(int32_t kernel_id, char* out, int32_t cap);
+/* Diagnostics: one eager step with a 100 MHz s_memrealtime stamp per workgroup at the
+ * stage boundaries of every launch; out = [launch][1024 workgroups][8 slots]. */
+int vaeb_debug_timeline(vaeb_ctx* ctx, int32_t batch_index, uint64_t* out, int64_t cap,
+                        int32_t* out_launches);
 
 #ifdef __cplusplus
 }

@@ -27,7 +27,7 @@ EXPORTS = [
     "vaeb_push_eps", "vaeb_set_step", "vaeb_update", "vaeb_update_async", "vaeb_update_many",
     "vaeb_epoch_elbo", "vaeb_synchronize", "vaeb_validate", "vaeb_reconstruct",
     "vaeb_comm_unique_id", "vaeb_comm_init", "vaeb_get_grads", "vaeb_get_activation",
-    "vaeb_profile_steps", "vaeb_kernel_name",
+    "vaeb_profile_steps", "vaeb_kernel_name", "vaeb_debug_timeline",
 ]
 
 
@@ -91,6 +91,8 @@ def load():
         "vaeb_profile_steps": ([_P, ctypes.c_int32, _F, ctypes.POINTER(ctypes.c_int32), ctypes.c_int32,
                                 ctypes.POINTER(ctypes.c_int32)], ctypes.c_int),
         "vaeb_kernel_name": ([ctypes.c_int32, ctypes.c_char_p, ctypes.c_int32], ctypes.c_int),
+        "vaeb_debug_timeline": ([_P, ctypes.c_int32, ctypes.POINTER(ctypes.c_uint64), _I64,
+                                 ctypes.POINTER(ctypes.c_int32)], ctypes.c_int),
     }
     for name, (args, res) in sig.items():
         fn = getattr(lib, name)
@@ -242,6 +244,14 @@ class Context:
         check(self.lib.vaeb_comm_init(self.h, buf, rank, world))
 
     # ---- measurement
+    def debug_timeline(self, batch_index=0):
+        """[launch][workgroup][slot] 100 MHz stamps of one eager step (diagnostics)."""
+        out = np.zeros(16 * 1024 * 8, np.uint64)
+        nl = ctypes.c_int32()
+        check(self.lib.vaeb_debug_timeline(self.h, int(batch_index), out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)),
+                                           out.size, ctypes.byref(nl)))
+        return out.reshape(16, 1024, 8)[:nl.value]
+
     def profile_steps(self, n_steps):
         ms = np.zeros(16, np.float32)
         ids = np.zeros(16, np.int32)

@@ -1,7 +1,7 @@
 // kernels_aux.hpp -- the weight-gradient / optimizer end of the SGVB step and the
 // reductions (/root/reference/VAEB.py:385-444).
 #pragma once
-#include "phases.hpp"
+#include "fused.hpp"
 
 namespace vaeb {
 
@@ -103,50 +103,74 @@ struct WGradArgs {
     OptArgs opt;
     ElboArgs elbo;
     const float* xbase; const int* cur_batch; int64_t batch_stride;
+    int64_t P;
+    uint64_t* dbg;
 };
 
 struct WGProb {
     const WGroup* g;
-    const float* at;
+    rsrc_t bat, bb0, bb1;
     DEV f32x4 a4(int i, int k) const {
-        if (i < g->rowsW) return ld4_mc(at, g->ld_at, i, k, g->rowsW, g->klim_at);
-        f32x4 v = zero4();
-        if (i == g->rowsW) {
-            v.x = (k + 0 < g->K) ? 1.f : 0.f;
-            v.y = (k + 1 < g->K) ? 1.f : 0.f;
-            v.z = (k + 2 < g->K) ? 1.f : 0.f;
-            v.w = (k + 3 < g->K) ? 1.f : 0.f;
-        }
+        f32x4 v = mc4(bat, g->ld_at, i, k, g->rowsW, g->klim_at);
+        const bool one = i == g->rowsW;  // the all-ones row (bias gradient), branch-free
+        v.x = one ? ((k + 0 < g->K) ? 1.f : 0.f) : v.x;
+        v.y = one ? ((k + 1 < g->K) ? 1.f : 0.f) : v.y;
+        v.z = one ? ((k + 2 < g->K) ? 1.f : 0.f) : v.z;
+        v.w = one ? ((k + 3 < g->K) ? 1.f : 0.f) : v.w;
         return v;
     }
-    DEV f32x4 b4(int j, int k, int w) const { return ld4_mc(w ? g->bm1 : g->bm0, g->ld_b, j, k, g->N, g->K); }
+    DEV f32x4 b4(int j, int k, int w) const { return mc4(w ? bb1 : bb0, g->ld_b, j, k, g->N, g->K); }
 };
 
 template <int NB>
-DEV void wgrad_tile(const WGradArgs& p, const WGroup& g, const float* at, int m0, int n0) {
+DEV void wgrad_tile(const WGradArgs& p, const WGroup& g, const float* at, int m0, int n0, int64_t P) {
     f32x4 acc[NB];
 #pragma unroll
     for (int w = 0; w < NB; ++w) acc[w] = zero4();
     const int lane = threadIdx.x & 63;
-    WGProb prob{&g, at};
-    if (m0 <= g.rowsW && n0 < g.N) wave_mainloop<NB, 1>(prob, m0 + (lane & 15), n0 + (lane & 15), g.K, 0, acc);
     const int j = n0 + (lane & 15);
-    if (j >= g.N) return;
+    const rsrc_t bth = mkbuf(p.opt.theta, P * 4), bac = mkbuf(p.opt.acc, P * 4), bgr = mkbuf(p.opt.grad, P * 4);
+    // prefetch theta / acc of this lane's outputs so the optimizer epilogue does not pay
+    // a second memory round trip after the MFMA chain (byte offsets; kOOB = masked)
+    uint32_t off[4][NB];
+    float th[4][NB], ac[4][NB];
+    const bool upd = p.opt.update != 0;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
         const int i = m0 + 4 * (lane >> 4) + r;
-        if (i > g.rowsW) continue;
+        const bool ok = j < g.N && i <= g.rowsW;
 #pragma unroll
         for (int w = 0; w < NB; ++w) {
-            const int64_t idx = (i < g.rowsW) ? (w ? g.offW1 : g.offW0) + (int64_t)i * g.N + j
-                                              : (w ? g.offb1 : g.offb0) + j;
-            opt_apply(p.opt, idx, acc[w][r]);
+            const int64_t idx = (i < g.rowsW) ? (w ? g.offW1 : g.offW0) + (int64_t)i * g.N + j : (w ? g.offb1 : g.offb0) + j;
+            off[r][w] = ok ? (uint32_t)idx * 4u : kOOB;
+            th[r][w] = upd ? bld(bth, off[r][w]) : 0.f;
+            ac[r][w] = upd ? bld(bac, off[r][w]) : 0.f;
         }
     }
+    WGProb prob{&g, mkbuf(at, (int64_t)g.klim_at * g.ld_at * 4), mkbuf(g.bm0, (int64_t)g.K * g.ld_b * 4),
+                mkbuf(g.bm1 ? g.bm1 : g.bm0, (int64_t)g.K * g.ld_b * 4)};
+    if (m0 <= g.rowsW && n0 < g.N) wave_mainloop<NB, 1, 8>(prob, m0 + (lane & 15), n0 + (lane & 15), g.K, 0, acc);
+    if (p.dbg && threadIdx.x == 0) p.dbg[blockIdx.x * 8 + 1] = __builtin_amdgcn_s_memrealtime();
+    // out-of-range byte offsets make the masked buffer stores no-ops
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int w = 0; w < NB; ++w) {
+            const float dsg = acc[w][r];
+            if (p.opt.store_grad) bst(bgr, off[r][w], dsg);
+            if (upd) {
+                const float t0 = th[r][w];
+                const float g2 = dsg - p.opt.prior * t0;
+                const float a2 = ac[r][w] + g2 * g2;
+                bst(bac, off[r][w], a2);
+                bst(bth, off[r][w], t0 + p.opt.lr * g2 / (sqrtf(a2) + p.opt.eps) - p.opt.decay * t0 * t0);
+            }
+        }
 }
 
 __global__ __launch_bounds__(256) void wgrad_kernel(WGradArgs p) {
     const int bid = blockIdx.x;
+    if (p.dbg && threadIdx.x == 0) p.dbg[bid * 8 + 0] = __builtin_amdgcn_s_memrealtime();
     if (bid >= p.total_wgs) {  // the extra workgroup: ELBO of this step
         elbo_reduce(p.elbo);
         return;
@@ -161,8 +185,9 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WGradArgs p) {
     const int wave = threadIdx.x >> 6;
     const int m0 = ((lt / g.tiles_n) * 2 + (wave >> 1)) * 16;
     const int n0 = ((lt % g.tiles_n) * 2 + (wave & 1)) * 16;
-    if (g.nb == 2) wgrad_tile<2>(p, g, at, m0, n0);
-    else wgrad_tile<1>(p, g, at, m0, n0);
+    if (g.nb == 2) wgrad_tile<2>(p, g, at, m0, n0, p.P);
+    else wgrad_tile<1>(p, g, at, m0, n0, p.P);
+    if (p.dbg && threadIdx.x == 0) p.dbg[bid * 8 + 3] = __builtin_amdgcn_s_memrealtime();
 }
 
 // ----------------------------------------------------------------- DP optimizer

@@ -54,7 +54,10 @@ struct StepArgs {
     // ELBO partials: [rows][col tiles]
     float *kl_part, *la_part, *lp_part;
     int nctZ, nctD;
+    uint64_t* dbg;         // diagnostics: per-workgroup s_memrealtime stamps (null = off)
 };
+
+
 
 // P1 resolves the minibatch index from the device-side batch order; every later phase
 // of the step reads the resolved copy (the cursor advances inside P8 / the optimizer).
@@ -68,21 +71,35 @@ DEV int64_t global_row0(const StepArgs& a) {
     return (a.order ? (int64_t)(*a.cur_batch) * a.row_base_mul : 0) + a.row_base_add;
 }
 
+struct NoPre {};
+
 // ----------------------------------------------------------------------------- P1
 struct PEnc {
     StepArgs a;
     const float* x;
     int M, N, K;
-    DEV void prepare() { x = x_rows_p1(a); }
-    DEV f32x4 a4(int m, int k) const { return ld4_kc(x, a.D, m, k, a.Mb, a.D, (a.D & 3) == 0); }
-    DEV f32x4 b4(int n, int k, int) const { return ld4_mc(a.W3, a.H, n, k, a.H, a.D); }
+    rsrc_t bx, bw;
+    bool vx;
+    DEV void prepare() {
+        x = x_rows_p1(a);
+        bx = mkbuf(x, (int64_t)a.Mb * a.D * 4);
+        bw = mkbuf(a.W3, (int64_t)a.D * a.H * 4);
+        vx = (a.D & 3) == 0 && aligned16(x);
+    }
+    DEV f32x4 a4(int m, int k) const { return kc4(bx, a.D, m, k, a.Mb, a.D, vx); }
+    DEV f32x4 b4(int n, int k, int) const { return mc4(bw, a.H, n, k, a.H, a.D); }
+    struct Pre { float b; };
+    DEV Pre prefetch(int, int n0) const {
+        const int n = n0 + (threadIdx.x & 15);
+        return Pre{bld(mkbuf(a.b3, (int64_t)a.H * 4), n < a.H ? (uint32_t)n * 4u : kOOB)};
+    }
     template <int NB>
-    DEV void epilogue(int m0, int n0, const f32x4 (&acc)[NB]) const {
+    DEV void epilogue(int m0, int n0, const f32x4 (&acc)[NB], const Pre& pre) const {
         const int lane = threadIdx.x & 63;
         if (a.order && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) *a.cur_batch = a.order[*a.cursor];
         const int n = n0 + (lane & 15);
         if (n >= a.H) return;
-        const float b = a.b3[n];
+        const float b = pre.b;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const int m = m0 + 4 * (lane >> 4) + r;
@@ -92,14 +109,22 @@ struct PEnc {
 };
 
 // ----------------------------------------------------------------------------- P2
+// (generic path for Z > 32; Z <= 32 uses heads_dechid_kernel in fused.hpp)
 struct PHeads {
     StepArgs a;
     int M, N, K;
-    DEV void prepare() {}
-    DEV f32x4 a4(int m, int k) const { return ld4_kc(a.h, a.H, m, k, a.Mbp, a.H, (a.H & 3) == 0); }
-    DEV f32x4 b4(int n, int k, int w) const { return ld4_mc(w ? a.W5 : a.W4, a.Z, n, k, a.Z, a.H); }
+    rsrc_t bh, bw4, bw5;
+    DEV void prepare() {
+        bh = mkbuf(a.h, (int64_t)a.Mbp * a.H * 4);
+        bw4 = mkbuf(a.W4, (int64_t)a.H * a.Z * 4);
+        bw5 = mkbuf(a.W5, (int64_t)a.H * a.Z * 4);
+    }
+    DEV f32x4 a4(int m, int k) const { return kc4(bh, a.H, m, k, a.Mbp, a.H, (a.H & 3) == 0); }
+    DEV f32x4 b4(int n, int k, int w) const { return mc4(w ? bw5 : bw4, a.Z, n, k, a.Z, a.H); }
+    using Pre = NoPre;
+    DEV Pre prefetch(int, int) const { return Pre{}; }
     template <int NB>
-    DEV void epilogue(int m0, int n0, const f32x4 (&acc)[NB]) const {
+    DEV void epilogue(int m0, int n0, const f32x4 (&acc)[NB], const Pre&) const {
         const int lane = threadIdx.x & 63;
         const int n = n0 + (lane & 15);
         const bool ncol = n < a.Z;
@@ -153,11 +178,17 @@ struct PHeads {
 struct PDecHid {
     StepArgs a;
     int M, N, K;
-    DEV void prepare() {}
-    DEV f32x4 a4(int m, int k) const { return ld4_kc(a.z, a.Z, m, k, a.Me, a.Z, (a.Z & 3) == 0); }
-    DEV f32x4 b4(int n, int k, int) const { return ld4_mc(a.W1, a.H, n, k, a.H, a.Z); }
+    rsrc_t bz, bw1;
+    DEV void prepare() {
+        bz = mkbuf(a.z, (int64_t)a.Me * a.Z * 4);
+        bw1 = mkbuf(a.W1, (int64_t)a.Z * a.H * 4);
+    }
+    DEV f32x4 a4(int m, int k) const { return kc4(bz, a.Z, m, k, a.Me, a.Z, (a.Z & 3) == 0); }
+    DEV f32x4 b4(int n, int k, int) const { return mc4(bw1, a.H, n, k, a.H, a.Z); }
+    using Pre = NoPre;
+    DEV Pre prefetch(int, int) const { return Pre{}; }
     template <int NB>
-    DEV void epilogue(int m0, int n0, const f32x4 (&acc)[NB]) const {
+    DEV void epilogue(int m0, int n0, const f32x4 (&acc)[NB], const Pre&) const {
         const int lane = threadIdx.x & 63;
         const int n = n0 + (lane & 15);
         if (n >= a.H) return;
@@ -176,18 +207,40 @@ struct PDecOut {
     StepArgs a;
     const float* x;
     int M, N, K;
-    DEV void prepare() { x = x_rows(a); }
-    DEV f32x4 a4(int m, int k) const { return ld4_kc(a.hd, a.H, m, k, a.Me, a.H, (a.H & 3) == 0); }
-    DEV f32x4 b4(int n, int k, int w) const { return ld4_mc(w ? a.W6 : a.W2, a.D, n, k, a.D, a.H); }
+    rsrc_t bhd, bw2, bw6;
+    DEV void prepare() {
+        x = x_rows(a);
+        bhd = mkbuf(a.hd, (int64_t)a.Me * a.H * 4);
+        bw2 = mkbuf(a.W2, (int64_t)a.H * a.D * 4);
+        bw6 = mkbuf(a.W6 ? a.W6 : a.W2, (int64_t)a.H * a.D * 4);
+    }
+    DEV f32x4 a4(int m, int k) const { return kc4(bhd, a.H, m, k, a.Me, a.H, (a.H & 3) == 0); }
+    DEV f32x4 b4(int n, int k, int w) const { return mc4(w ? bw6 : bw2, a.D, n, k, a.D, a.H); }
+    struct Pre { float b2, b6; f32x4 xv; };
+    DEV Pre prefetch(int m0, int n0) const {
+        const int lane = threadIdx.x & 63;
+        const int n = n0 + (lane & 15);
+        const bool ncol = n < a.D;
+        Pre pr;
+        pr.b2 = bld(mkbuf(a.b2, (int64_t)a.D * 4), ncol ? (uint32_t)n * 4u : kOOB);
+        pr.b6 = (a.dec == DEC_GAUSSIAN) ? bld(mkbuf(a.b6, (int64_t)a.D * 4), ncol ? (uint32_t)n * 4u : kOOB) : 0.f;
+        const rsrc_t bxr = mkbuf(x, (int64_t)a.Mb * a.D * 4);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int i = (m0 + 4 * (lane >> 4) + r) % a.Mbp;
+            pr.xv[r] = bld(bxr, (ncol && i < a.Mb) ? (uint32_t)(i * a.D + n) * 4u : kOOB);
+        }
+        return pr;
+    }
     template <int NB>
-    DEV void epilogue(int m0, int n0, const f32x4 (&acc)[NB]) const {
+    DEV void epilogue(int m0, int n0, const f32x4 (&acc)[NB], const Pre& pre) const {
         const int lane = threadIdx.x & 63;
         const int n = n0 + (lane & 15);
         const bool ncol = n < a.D;
         const int ct = n0 >> 4;
         const float sl = a.sc / (float)a.L;
-        const float b2 = ncol ? a.b2[n] : 0.f;
-        const float b6 = (ncol && a.dec == DEC_GAUSSIAN) ? a.b6[n] : 0.f;
+        const float b2 = pre.b2;
+        const float b6 = pre.b6;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const int m = m0 + 4 * (lane >> 4) + r;
@@ -195,7 +248,7 @@ struct PDecOut {
             const bool valid = ncol && i < a.Mb;
             float lp = 0.f, d2 = 0.f, d6 = 0.f, yv = 0.f;
             if (valid) {
-                const float xv = x[(int64_t)i * a.D + n];
+                const float xv = pre.xv[r];
                 const float a2 = acc[0][r] + b2;
                 yv = sigmoidf(a2);
                 if (a.dec == DEC_GAUSSIAN) {
@@ -228,21 +281,42 @@ struct PDecOut {
 // ----------------------------------------------------------------------------- P5
 struct PDhd {
     StepArgs a;
-    int M, N, K;  // K = D (Bernoulli) or 2D (Gaussian: [dA2|dA6] . [W2|W6]^T)
-    DEV void prepare() {}
-    // k in [D, 2D) addresses the Gaussian half; chunks past K read zeros.
+    int M, N, K;  // K = D (Bernoulli) or Dp + D (Gaussian: [dA2|dA6] . [W2|W6]^T, Dp = D rounded to 4)
+    int Dp;
+    bool vw;
+    rsrc_t bd2, bd6, bw2, bw6;
+    DEV void prepare() {
+        Dp = (a.D + 3) & ~3;
+        vw = (a.D & 3) == 0 && aligned16(a.W2) && (a.W6 == nullptr || aligned16(a.W6));
+        bd2 = mkbuf(a.dA2, (int64_t)a.Me * a.D * 4);
+        bd6 = mkbuf(a.dA6 ? a.dA6 : a.dA2, (int64_t)a.Me * a.D * 4);
+        bw2 = mkbuf(a.W2, (int64_t)a.H * a.D * 4);
+        bw6 = mkbuf(a.W6 ? a.W6 : a.W2, (int64_t)a.H * a.D * 4);
+    }
+    // k in [Dp, Dp + D) addresses the Gaussian half; chunks past K read zeros.
     DEV f32x4 a4(int m, int k) const {
-        if (k < a.D) return ld4_kc(a.dA2, a.D, m, k, a.Me, a.D, (a.D & 3) == 0);
-        if (k >= K) return zero4();
-        return ld4_kc(a.dA6, a.D, m, k - a.D, a.Me, a.D, (a.D & 3) == 0);
+        if (k < Dp) return kc4(bd2, a.D, m, k, a.Me, a.D, (a.D & 3) == 0);
+        return kc4(bd6, a.D, m, k - Dp, k < K ? a.Me : 0, a.D, (a.D & 3) == 0);
     }
     DEV f32x4 b4(int n, int k, int) const {
-        if (k < a.D) return ld4_kc(a.W2, a.D, n, k, a.H, a.D, (a.D & 3) == 0);
-        if (k >= K) return zero4();
-        return ld4_kc(a.W6, a.D, n, k - a.D, a.H, a.D, (a.D & 3) == 0);
+        if (k < Dp) return kc4(bw2, a.D, n, k, a.H, a.D, vw);
+        return kc4(bw6, a.D, n, k - Dp, k < K ? a.H : 0, a.D, vw);
+    }
+    struct Pre { f32x4 hd; };
+    DEV Pre prefetch(int m0, int n0) const {
+        const int lane = threadIdx.x & 63;
+        const int n = n0 + (lane & 15);
+        const rsrc_t b = mkbuf(a.hd, (int64_t)a.Me * a.H * 4);
+        Pre pr;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int m = m0 + 4 * (lane >> 4) + r;
+            pr.hd[r] = bld(b, (n < a.H && m < a.Me) ? (uint32_t)(m * a.H + n) * 4u : kOOB);
+        }
+        return pr;
     }
     template <int NB>
-    DEV void epilogue(int m0, int n0, const f32x4 (&acc)[NB]) const {
+    DEV void epilogue(int m0, int n0, const f32x4 (&acc)[NB], const Pre& pre) const {
         const int lane = threadIdx.x & 63;
         const int n = n0 + (lane & 15);
         if (n >= a.H) return;
@@ -250,21 +324,28 @@ struct PDhd {
         for (int r = 0; r < 4; ++r) {
             const int m = m0 + 4 * (lane >> 4) + r;
             const int64_t o = (int64_t)m * a.H + n;
-            const float hd = a.hd[o];
+            const float hd = pre.hd[r];
             a.dA1[o] = ((m % a.Mbp) < a.Mb) ? acc[0][r] * (1.f - hd * hd) : 0.f;
         }
     }
 };
 
 // ----------------------------------------------------------------------------- P6
+// (generic path for Z > 32; Z <= 32 uses dz_dh_kernel in fused.hpp)
 struct PDz {
     StepArgs a;
     int M, N, K;
-    DEV void prepare() {}
-    DEV f32x4 a4(int m, int k) const { return ld4_kc(a.dA1, a.H, m, k, a.Me, a.H, (a.H & 3) == 0); }
-    DEV f32x4 b4(int n, int k, int) const { return ld4_kc(a.W1, a.H, n, k, a.Z, a.H, (a.H & 3) == 0); }
+    rsrc_t bd1, bw1;
+    DEV void prepare() {
+        bd1 = mkbuf(a.dA1, (int64_t)a.Me * a.H * 4);
+        bw1 = mkbuf(a.W1, (int64_t)a.Z * a.H * 4);
+    }
+    DEV f32x4 a4(int m, int k) const { return kc4(bd1, a.H, m, k, a.Me, a.H, (a.H & 3) == 0); }
+    DEV f32x4 b4(int n, int k, int) const { return kc4(bw1, a.H, n, k, a.Z, a.H, (a.H & 3) == 0 && aligned16(a.W1)); }
+    using Pre = NoPre;
+    DEV Pre prefetch(int, int) const { return Pre{}; }
     template <int NB>
-    DEV void epilogue(int m0, int n0, const f32x4 (&acc)[NB]) const {
+    DEV void epilogue(int m0, int n0, const f32x4 (&acc)[NB], const Pre&) const {
         const int lane = threadIdx.x & 63;
         const int n = n0 + (lane & 15);
         if (n >= a.Z) return;
@@ -280,7 +361,11 @@ struct PDz {
 struct PDh {
     StepArgs a;
     int M, N, K;  // K = 2Z
-    DEV void prepare() {}
+    rsrc_t bw4, bw5;
+    DEV void prepare() {
+        bw4 = mkbuf(a.W4, (int64_t)a.H * a.Z * 4);
+        bw5 = mkbuf(a.W5, (int64_t)a.H * a.Z * 4);
+    }
     // [dMu | dLv](i, k) from dZ, mu, lv, eps, z (LA variant).
     DEV float dmulv(int i, int k) const {
         const int Z = a.Z;
@@ -326,21 +411,24 @@ struct PDh {
         }
         return v;
     }
+    // B(k, n) = [W4 | W5]^T: both halves loaded with out-of-range offsets for the other.
     DEV f32x4 b4(int n, int k, int) const {
-        f32x4 v = zero4();
-        if (n >= a.H) return v;
         const int Z = a.Z;
-        float t[4];
+        f32x4 v;
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
             const int kk = k + s;
-            t[s] = kk < Z ? a.W4[(int64_t)n * Z + kk] : (kk < 2 * Z ? a.W5[(int64_t)n * Z + kk - Z] : 0.f);
+            const bool ok = n < a.H;
+            const float w4 = bld(bw4, (ok && kk < Z) ? (uint32_t)(n * Z + kk) * 4u : kOOB);
+            const float w5 = bld(bw5, (ok && kk >= Z && kk < 2 * Z) ? (uint32_t)(n * Z + kk - Z) * 4u : kOOB);
+            v[s] = w4 + w5;
         }
-        v.x = t[0]; v.y = t[1]; v.z = t[2]; v.w = t[3];
         return v;
     }
+    using Pre = NoPre;
+    DEV Pre prefetch(int, int) const { return Pre{}; }
     template <int NB>
-    DEV void epilogue(int m0, int n0, const f32x4 (&acc)[NB]) const {
+    DEV void epilogue(int m0, int n0, const f32x4 (&acc)[NB], const Pre&) const {
         const int lane = threadIdx.x & 63;
         const int n = n0 + (lane & 15);
         if (n >= a.H) return;

@@ -2,15 +2,22 @@
 //
 // Every contraction of the SGVB step (VAEB.py:245-265 forward, the T.grad backward of
 // VAEB.py:397) is C[M x N] = A[M x K] * B[K x N] with small, awkward shapes (M = batch
-// rows = 100, K as small as Z = 20, N as small as Z).  One wave owns a 16x16 output tile
-// and runs v_mfma_f32_16x16x4_f32 (exact f32, 64 FLOP/clk/SIMD = the f32 peak of the
-// chip) over its share of K; a 256-thread workgroup holds WM x WN tiles x KS K-slices
-// (WM*WN*KS == 4 waves), and K-slices are summed through LDS before the fused epilogue.
+// rows = 100, K as small as Z = 20, N as small as Z).  At these sizes every phase is
+// latency-bound, so the engine is built to put a wave's whole K share in flight at once:
 //
-// Operand feeding (per lane l, i = l & 15, q = l >> 4, chunk c of 16 k-values):
-//   the MFMA's k-group q is fed k = 16c + 4q + s at step s = 0..3, so each lane needs
-//   FOUR CONSECUTIVE k at its fixed row (A) / column (B): one 16-byte load when the
-//   operand is K-contiguous, four coalesced scalar loads when it is M/N-contiguous.
+//  * one wave owns a 16x16 output tile and runs v_mfma_f32_16x16x4_f32 (exact f32,
+//    64 FLOP/clk/SIMD = the f32 peak of the chip) over its K-slice;
+//  * a workgroup holds WM x WN tiles x KS K-slices (4 or 8 waves); K-slices are summed
+//    through LDS before the fused epilogue;
+//  * a wave loads GCH chunks (16 k each) into registers before its first MFMA -- one
+//    memory round trip per group instead of one per chunk;
+//  * loads are raw buffer loads (32-bit offsets, out-of-range reads return 0), so a
+//    masked element costs one offset select and the load streams stay branch-free.
+//
+// Operand feeding (per lane l, i = l & 15, q = l >> 4, chunk c of 16 k-values): the
+// MFMA's k-group q is fed k = 16c + 4q + s at step s = 0..3, so each lane needs FOUR
+// CONSECUTIVE k at its fixed row (A) / column (B): one 16-byte load when the operand is
+// K-contiguous, four coalesced scalar loads when it is M/N-contiguous.
 // C/D mapping of 16x16x4 f32: col = l & 15, row = 4*(l >> 4) + r  (r = 0..3).
 #pragma once
 #include <hip/hip_runtime.h>
@@ -20,37 +27,69 @@
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
+// Diagnostics: wave 0 of each workgroup records a 100 MHz timestamp in slot `slot`.
+#define VAEB_STAMP(A, slot)                                                               \
+    do {                                                                                  \
+        if ((A).dbg && threadIdx.x == 0)                                                  \
+            (A).dbg[(blockIdx.x + (uint64_t)blockIdx.y * gridDim.x) * 8 + (slot)] =       \
+                __builtin_amdgcn_s_memrealtime();                                         \
+    } while (0)
+
 namespace vaeb {
 
 DEV f32x4 zero4() { f32x4 z = {0.f, 0.f, 0.f, 0.f}; return z; }
 
-// K-contiguous operand: element (r, k) = p[r * ld + k]; rows >= rlim or k >= klim read 0.
-DEV f32x4 ld4_kc(const float* __restrict__ p, int ld, int r, int k, int rlim, int klim, bool vec) {
-    f32x4 v = zero4();
-    if (r < rlim) {
-        const float* q = p + (int64_t)r * ld + k;
-        if (vec && k + 3 < klim && ((reinterpret_cast<uintptr_t>(q) & 15) == 0)) {
-            v = *reinterpret_cast<const f32x4*>(q);
-        } else {
-            if (k + 0 < klim) v.x = q[0];
-            if (k + 1 < klim) v.y = q[1];
-            if (k + 2 < klim) v.z = q[2];
-            if (k + 3 < klim) v.w = q[3];
-        }
-    }
+// ------------------------------------------------------------------ buffer operands
+// Every operand fetch is a raw buffer load through a 128-bit descriptor built from
+// wave-uniform kernel arguments: a 32-bit per-lane byte offset, and the hardware range
+// check returns 0 for an offset >= num_records.  Masking an element is therefore one
+// select of its offset to kOOB -- no 64-bit address arithmetic and no select on the
+// loaded value, which keeps the load streams short and lets them all issue before the
+// first wait (the flat-pointer form of this code serialised behind vmcnt(0)).
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+constexpr uint32_t kOOB = 0x80000000u;  // every buffer here is < 2 GiB
+
+// The descriptor inputs go through readfirstlane so the compiler can PROVE them
+// wave-uniform (otherwise it wraps every buffer op in a waterfall loop; guide T20).
+DEV rsrc_t mkbuf(const void* p, int64_t nbytes) {
+    const uint64_t a = reinterpret_cast<uint64_t>(p);
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+    const int n = __builtin_amdgcn_readfirstlane((int)(nbytes < 0x7FFFFFF0ll ? nbytes : 0x7FFFFFF0ll));
+    void* base = reinterpret_cast<void*>(((uint64_t)hi << 32) | lo);
+    return __builtin_amdgcn_make_buffer_rsrc(base, (short)0, n, 0x00020000);
+}
+DEV float bld(rsrc_t b, uint32_t off) { return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(b, off, 0, 0)); }
+DEV f32x4 bld4(rsrc_t b, uint32_t off) { return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(b, off, 0, 0)); }
+DEV void bst(rsrc_t b, uint32_t off, float v) { __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), b, off, 0, 0); }
+
+DEV bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
+// K-contiguous operand: element (r, k) at [r * ld + k]; r >= rlim or k >= klim read 0.
+// vec: ld % 4 == 0, klim % 4 == 0 and a 16-byte aligned base (a float4 at k % 4 == 0 is
+// then wholly in or wholly out of range).
+DEV f32x4 kc4(rsrc_t b, int ld, int r, int k, int rlim, int klim, bool vec) {
+    const bool rok = r < rlim;
+    const uint32_t base = (uint32_t)(r * ld + k) * 4u;
+    if (vec) return bld4(b, (rok && k < klim) ? base : kOOB);
+    f32x4 v;
+    v.x = bld(b, (rok && k + 0 < klim) ? base + 0 : kOOB);
+    v.y = bld(b, (rok && k + 1 < klim) ? base + 4 : kOOB);
+    v.z = bld(b, (rok && k + 2 < klim) ? base + 8 : kOOB);
+    v.w = bld(b, (rok && k + 3 < klim) ? base + 12 : kOOB);
     return v;
 }
 
-// M/N-contiguous operand: element (r, k) = p[k * ld + r].
-DEV f32x4 ld4_mc(const float* __restrict__ p, int ld, int r, int k, int rlim, int klim) {
-    f32x4 v = zero4();
-    if (r < rlim) {
-        const float* q = p + (int64_t)k * ld + r;
-        if (k + 0 < klim) v.x = q[0];
-        if (k + 1 < klim) v.y = q[(int64_t)ld];
-        if (k + 2 < klim) v.z = q[(int64_t)2 * ld];
-        if (k + 3 < klim) v.w = q[(int64_t)3 * ld];
-    }
+// M/N-contiguous operand: element (r, k) at [k * ld + r].
+DEV f32x4 mc4(rsrc_t b, int ld, int r, int k, int rlim, int klim) {
+    const bool rok = r < rlim;
+    const uint32_t base = (uint32_t)(k * ld + r) * 4u;
+    const uint32_t st = (uint32_t)ld * 4u;
+    f32x4 v;
+    v.x = bld(b, (rok && k + 0 < klim) ? base : kOOB);
+    v.y = bld(b, (rok && k + 1 < klim) ? base + st : kOOB);
+    v.z = bld(b, (rok && k + 2 < klim) ? base + 2 * st : kOOB);
+    v.w = bld(b, (rok && k + 3 < klim) ? base + 3 * st : kOOB);
     return v;
 }
 
@@ -71,43 +110,60 @@ DEV float sum16(float v) {
     return v;
 }
 
-// The wave-level main loop: accumulate NB tiles that share the A operand.
+// The wave-level main loop: accumulate NB tiles that share the A operand, over the
+// chunks c = kslice, kslice + KS, ... < ceil(K/16), GCH chunks per memory round trip.
 // P must provide:  f32x4 a4(int m, int k) const;  f32x4 b4(int n, int k, int which) const;
-template <int NB, int KS, class P>
+template <int NB, int KS, int GCH, class P>
 DEV void wave_mainloop(const P& p, int m, int n, int K, int kslice, f32x4 (&acc)[NB]) {
     const int lane = threadIdx.x & 63;
     const int kq = 4 * (lane >> 4);
     const int nch = (K + 15) >> 4;
-    int c = kslice;
-    // 4 chunks in flight per iteration (16 VGPR of A + 16*NB of B) to hide L2 latency.
-    for (; c + 3 * KS < nch; c += 4 * KS) {
-        f32x4 a[4], b[4][NB];
+    for (int c0 = kslice; c0 < nch; c0 += GCH * KS) {
+        f32x4 a[GCH], b[GCH][NB];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const int k = (c + u * KS) * 16 + kq;
+        for (int u = 0; u < GCH; ++u) {
+            const int k = (c0 + u * KS) * 16 + kq;  // k >= K: the loaders return zeros
             a[u] = p.a4(m, k);
 #pragma unroll
             for (int w = 0; w < NB; ++w) b[u][w] = p.b4(n, k, w);
         }
 #pragma unroll
-        for (int u = 0; u < 4; ++u)
+        for (int u = 0; u < GCH; ++u)
 #pragma unroll
             for (int w = 0; w < NB; ++w) acc[w] = mfma4(a[u], b[u][w], acc[w]);
     }
-    for (; c < nch; c += KS) {
-        const int k = c * 16 + kq;
-        f32x4 a = p.a4(m, k);
-#pragma unroll
-        for (int w = 0; w < NB; ++w) acc[w] = mfma4(a, p.b4(n, k, w), acc[w]);
-    }
 }
 
-// Generic tile kernel.  Grid: x = M tiles / WM, y = N tiles / WN.  P also provides
-//   int M, N, K;  void prepare();  void epilogue(int m0, int n0, const f32x4 (&acc)[NB]) const;
-template <int WM, int WN, int KS, int NB, class P>
-__global__ __launch_bounds__(256) void tile_kernel(P p0) {
-    static_assert(WM * WN * KS == 4, "4 waves per workgroup");
+// Sum the KS K-slice partials of each tile through LDS; afterwards the ks == 0 wave of
+// each tile holds the total.  Returns false for the other waves.
+template <int NW, int KS, int NB>
+DEV bool ks_reduce(f32x4 (&acc)[NB], int wave, int ks) {
+    if constexpr (KS > 1) {
+        __shared__ f32x4 red[NW][NB][64];
+        const int lane = threadIdx.x & 63;
+#pragma unroll
+        for (int w = 0; w < NB; ++w) red[wave][w][lane] = acc[w];
+        __syncthreads();
+        if (ks != 0) return false;
+#pragma unroll
+        for (int s = 1; s < KS; ++s)
+#pragma unroll
+            for (int w = 0; w < NB; ++w) acc[w] += red[wave + s][w][lane];
+    }
+    return true;
+}
+
+// Generic tile kernel.  Grid: x = M tiles / WM, y = N tiles / WN; WM*WN*KS waves.
+// P also provides  int M, N, K;  void prepare();
+//                  Pre prefetch(int m0, int n0) const;   (epilogue operands, issued
+//                      before the main loop so they ride the same memory round trip)
+//                  void epilogue(int m0, int n0, const f32x4 (&acc)[NB], const Pre&) const;
+template <int WM, int WN, int KS, int NB, int GCH, class P>
+__global__ __launch_bounds__(64 * WM * WN * KS) void tile_kernel(P p0) {
+    constexpr int NW = WM * WN * KS;
     P p = p0;
+    VAEB_STAMP(p.a, 0);
+    if (p.a.dbg && threadIdx.x == 0) p.a.dbg[(blockIdx.x + (uint64_t)blockIdx.y * gridDim.x) * 8 + 6] = __builtin_amdgcn_s_memtime();
     p.prepare();
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
@@ -118,20 +174,16 @@ __global__ __launch_bounds__(256) void tile_kernel(P p0) {
     f32x4 acc[NB];
 #pragma unroll
     for (int w = 0; w < NB; ++w) acc[w] = zero4();
-    if (m0 < p.M && n0 < p.N) wave_mainloop<NB, KS>(p, m0 + (lane & 15), n0 + (lane & 15), p.K, ks, acc);
-    if constexpr (KS > 1) {
-        __shared__ f32x4 red[4][NB][64];
-#pragma unroll
-        for (int w = 0; w < NB; ++w) red[wave][w][lane] = acc[w];
-        __syncthreads();
-        if (ks != 0) return;
-#pragma unroll
-        for (int s = 1; s < KS; ++s)
-#pragma unroll
-            for (int w = 0; w < NB; ++w) acc[w] += red[wave + s][w][lane];
-    }
+    typename P::Pre pre{};
+    if (ks == 0) pre = p.prefetch(m0, n0);
+    if (m0 < p.M && n0 < p.N) wave_mainloop<NB, KS, GCH>(p, m0 + (lane & 15), n0 + (lane & 15), p.K, ks, acc);
+    VAEB_STAMP(p.a, 1);
+    if (!ks_reduce<NW, KS, NB>(acc, wave, ks)) return;
+    VAEB_STAMP(p.a, 2);
     if (m0 >= p.M || n0 >= p.N) return;
-    p.epilogue(m0, n0, acc);
+    p.epilogue(m0, n0, acc, pre);
+    VAEB_STAMP(p.a, 3);
+    if (p.a.dbg && threadIdx.x == 0) p.a.dbg[(blockIdx.x + (uint64_t)blockIdx.y * gridDim.x) * 8 + 7] = __builtin_amdgcn_s_memtime();
 }
 
 // ------------------------------------------------------------------ Philox4x32-10

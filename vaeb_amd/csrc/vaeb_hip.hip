@@ -59,9 +59,11 @@ constexpr int kOrderCap = 1 << 20;
 constexpr int kFvParts = 512;
 constexpr int kGraphSteps = 32;
 constexpr int kMaxProfKernels = 16;
+constexpr int kDbgWG = 1024;      // diagnostics: stamp slots per launch (workgroups)
 
 const char* kKernelNames[] = {"p1_enc", "p2_heads", "p3_dechid", "p4_decout", "p5_dhd", "p6_dz",
-                              "p7_dh", "p8_wgrad", "allreduce", "adagrad", "fv_update", "elbo"};
+                              "p7_dh", "p8_wgrad", "allreduce", "adagrad", "fv_update", "elbo",
+                              "p23_heads_dechid", "p67_dz_dh"};
 
 }  // namespace
 
@@ -109,11 +111,16 @@ struct vaeb_ctx {
     hipEvent_t pev[kMaxProfKernels + 1] = {};
     int prof_n = 0;
     std::vector<int> prof_ids;
+    // diagnostics timeline (vaeb_debug_timeline)
+    uint64_t* dbg = nullptr;
+    int dbg_slot = 0;
 };
 
 namespace {
 
 bool gaussian(const vaeb_ctx* c) { return c->c.decoder == VAEB_DEC_GAUSSIAN; }
+
+uint64_t* next_dbg(vaeb_ctx* c) { return c->dbg ? c->dbg + (size_t)(c->dbg_slot++) * kDbgWG * 8 : nullptr; }
 
 StepArgs make_args(vaeb_ctx* c, int Mb, int mode, const float* xbase, bool train) {
     StepArgs a{};
@@ -159,11 +166,21 @@ StepArgs make_args(vaeb_ctx* c, int Mb, int mode, const float* xbase, bool train
     return a;
 }
 
-template <int WM, int WN, int KS, int NB, class P>
+template <int WM, int WN, int KS, int NB, int GCH, class P>
 void launch_tile(hipStream_t s, const P& p) {
     dim3 grid(cdiv(p.M, 16 * WM), cdiv(p.N, 16 * WN));
-    hipLaunchKernelGGL((tile_kernel<WM, WN, KS, NB, P>), grid, dim3(256), 0, s, p);
+    hipLaunchKernelGGL((tile_kernel<WM, WN, KS, NB, GCH, P>), grid, dim3(64 * WM * WN * KS), 0, s, p);
 }
+
+// Big-K phases: 8 waves split K; a wave's chunks go in flight together (GCH per trip).
+template <int NB, class P>
+void launch_bigk(hipStream_t s, const P& p) {
+    const int per_wave = cdiv(cdiv(p.K, 16), 8);
+    if (per_wave <= 4) launch_tile<1, 1, 8, NB, 4>(s, p);
+    else launch_tile<1, 1, 8, NB, 8>(s, p);
+}
+
+bool fused_latent(const vaeb_ctx* c) { return c->c.Z <= 32; }
 
 struct Prof {
     vaeb_ctx* c;
@@ -189,20 +206,31 @@ ElboArgs base_elbo(vaeb_ctx* c, const StepArgs& a) {
 }
 
 // Forward phases P1..P4 for any mode.
-int enqueue_forward(vaeb_ctx* c, const StepArgs& a, Prof& pr) {
+int enqueue_forward(vaeb_ctx* c, const StepArgs& a0, Prof& pr) {
     hipStream_t s = c->s;
+    StepArgs a = a0;
+    a.dbg = next_dbg(c);
     pr.mark(0);
-    launch_tile<1, 1, 4, 1>(s, PEnc{a, nullptr, a.Mbp, a.H, a.D});
+    launch_bigk<1>(s, PEnc{a, nullptr, a.Mbp, a.H, a.D});
     CHECK_LAUNCH();
-    pr.mark(1);
-    launch_tile<1, 1, 4, 2>(s, PHeads{a, a.Mbp, a.Z, a.H});
-    CHECK_LAUNCH();
-    pr.mark(2);
-    launch_tile<1, 4, 1, 1>(s, PDecHid{a, a.Me, a.H, a.Z});
-    CHECK_LAUNCH();
+    a.dbg = next_dbg(c);
+    if (fused_latent(c)) {
+        pr.mark(12);
+        if (a.Z <= 16) hipLaunchKernelGGL(heads_dechid_kernel<1>, dim3(a.Mbp / 16), dim3(512), 0, s, a);
+        else hipLaunchKernelGGL(heads_dechid_kernel<2>, dim3(a.Mbp / 16), dim3(512), 0, s, a);
+        CHECK_LAUNCH();
+    } else {
+        pr.mark(1);
+        launch_tile<1, 1, 4, 2, 8>(s, PHeads{a, a.Mbp, a.Z, a.H});
+        CHECK_LAUNCH();
+        pr.mark(2);
+        launch_tile<1, 4, 1, 1, 8>(s, PDecHid{a, a.Me, a.H, a.Z});
+        CHECK_LAUNCH();
+    }
+    a.dbg = next_dbg(c);
     pr.mark(3);
-    if (gaussian(c)) launch_tile<1, 1, 4, 2>(s, PDecOut{a, nullptr, a.Me, a.D, a.H});
-    else launch_tile<1, 1, 4, 1>(s, PDecOut{a, nullptr, a.Me, a.D, a.H});
+    if (gaussian(c)) launch_bigk<2>(s, PDecOut{a, nullptr, a.Me, a.D, a.H});
+    else launch_bigk<1>(s, PDecOut{a, nullptr, a.Me, a.D, a.H});
     CHECK_LAUNCH();
     return 0;
 }
@@ -242,15 +270,24 @@ int enqueue_train_step(vaeb_ctx* c, bool prof) {
         c->prof_n = pr.k;
         return 0;
     }
+    a.dbg = next_dbg(c);
     pr.mark(4);
-    launch_tile<1, 1, 4, 1>(s, PDhd{a, a.Me, a.H, gaussian(c) ? 2 * a.D : a.D});
+    launch_bigk<1>(s, PDhd{a, a.Me, a.H, gaussian(c) ? ((a.D + 3) & ~3) + a.D : a.D});
     CHECK_LAUNCH();
-    pr.mark(5);
-    launch_tile<1, 1, 4, 1>(s, PDz{a, a.Me, a.Z, a.H});
-    CHECK_LAUNCH();
-    pr.mark(6);
-    launch_tile<1, 4, 1, 1>(s, PDh{a, a.Mbp, a.H, 2 * a.Z});
-    CHECK_LAUNCH();
+    a.dbg = next_dbg(c);
+    if (fused_latent(c)) {
+        pr.mark(13);
+        if (a.Z <= 16) hipLaunchKernelGGL(dz_dh_kernel<1>, dim3(a.Mbp / 16), dim3(512), 0, s, a);
+        else hipLaunchKernelGGL(dz_dh_kernel<2>, dim3(a.Mbp / 16), dim3(512), 0, s, a);
+        CHECK_LAUNCH();
+    } else {
+        pr.mark(5);
+        launch_tile<1, 1, 4, 1, 8>(s, PDz{a, a.Me, a.Z, a.H});
+        CHECK_LAUNCH();
+        pr.mark(6);
+        launch_tile<1, 4, 1, 1, 8>(s, PDh{a, a.Mbp, a.H, 2 * a.Z});
+        CHECK_LAUNCH();
+    }
 
     // P8: grouped weight gradients (+ fused prior/Adagrad when single rank)
     const bool dp = c->comm != nullptr && c->world > 1;
@@ -282,7 +319,8 @@ int enqueue_train_step(vaeb_ctx* c, bool prof) {
     w.opt = make_opt(c, !dp, dp || g.keep_grads != 0);
     w.elbo = e;
     if (dp) { w.elbo.dp_slot = c->grad + c->P; w.elbo.elbo_out = nullptr; w.elbo.cursor = nullptr; w.elbo.step = nullptr; }
-    w.xbase = c->data; w.cur_batch = c->ictl + 1; w.batch_stride = a.batch_stride;
+    w.xbase = c->data; w.cur_batch = c->ictl + 1; w.batch_stride = a.batch_stride; w.P = c->P;
+    w.dbg = next_dbg(c);
     pr.mark(7);
     hipLaunchKernelGGL(wgrad_kernel, dim3(w.total_wgs + 1), dim3(256), 0, s, w);
     CHECK_LAUNCH();
@@ -743,6 +781,29 @@ int vaeb_profile_steps(vaeb_ctx* c, int32_t n_steps, float* out_ms, int32_t* out
         if (out_ids) out_ids[k] = c->prof_ids[k];
     }
     if (out_nk) *out_nk = nk;
+    return 0;
+}
+
+int vaeb_debug_timeline(vaeb_ctx* c, int32_t batch_index, uint64_t* out, int64_t cap, int32_t* out_launches) {
+    if (!c || !out) return fail(VAEB_ERR_ARG, "bad arguments");
+    if (int rc = check_batches(c, &batch_index, 1)) return rc;
+    const size_t n = (size_t)kMaxProfKernels * kDbgWG * 8;
+    if (!c->dbg)
+        if (int rc = dalloc(&c->dbg, n)) return rc;
+    HIP_TRY(hipMemsetAsync(c->dbg, 0, n * sizeof(uint64_t), c->s));
+    if (int rc = upload_order(c, &batch_index, 1)) return rc;
+    c->dbg_slot = 0;
+    int rc = enqueue_train_step(c, false);
+    const int launches = c->dbg_slot;
+    c->dbg_slot = 0;
+    uint64_t* d = c->dbg;
+    c->dbg = nullptr;  // later steps (and captured graphs) run without stamps
+    if (rc) { hipFree(d); return rc; }
+    HIP_TRY(hipStreamSynchronize(c->s));
+    const size_t m = std::min<size_t>(n, (size_t)cap);
+    HIP_TRY(hipMemcpy(out, d, m * sizeof(uint64_t), hipMemcpyDeviceToHost));
+    hipFree(d);
+    if (out_launches) *out_launches = launches;
     return 0;
 }
 
