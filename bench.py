@@ -45,6 +45,25 @@ def phase_flops(D, H, Z, B, L=1, gaussian=False):
     }
 
 
+KERNEL_SYMBOLS = {"p1_enc": "PEnc", "p23_heads_dechid": "heads_dechid_kernel", "p4_decout": "PDecOut",
+                  "p5_dhd": "PDhd", "p67_dz_dh": "dz_dh_kernel", "p8_wgrad": "wgrad_kernel"}
+
+
+def committed_traffic(kernel):
+    """HBM bytes per launch (FETCH_SIZE + WRITE_SIZE, KB units) of `kernel` from the
+    rocprofv3 PMC passes committed under profiles/ (separate --pmc passes)."""
+    path = os.path.join(ROOT, "profiles", "r1", "pmc_per_launch.json")
+    try:
+        data = json.load(open(path))
+    except Exception:
+        return None
+    sym = KERNEL_SYMBOLS.get(kernel)
+    for name, v in data.items():
+        if sym and sym in name and "FETCH_SIZE" in v and "WRITE_SIZE" in v:
+            return (v["FETCH_SIZE"] + v["WRITE_SIZE"]) * 1024.0
+    return None
+
+
 def cpu_baseline(D, H, Z, B, x, budget_s=10.0):
     """The oracle's float32 NumPy restatement of the same step, on the host cores."""
     from oracle import vaeb_oracle as O
@@ -155,6 +174,7 @@ def main():
     fl = phase_flops(D, H, Z, B)
     dom = max((k for k in prof if k[0] in fl), key=lambda k: k[1])
     achieved = fl[dom[0]] / (dom[1] * 1e-3) / 1e12
+    traffic = committed_traffic(dom[0])
 
     res = {
         "metric": "SGVB training images/sec + ELBO at MNIST 784-500-20, batch 100",
@@ -174,7 +194,7 @@ def main():
         "elbo": elbo_sum / max(nsteps, 1),
         "kernels_ms": {k: round(v, 5) for k, v in prof},
         "roofline": {"bound": "mfma", "kernel": dom[0], "achieved": achieved, "peak": PEAK_F32_TFLOPS,
-                     "unit": "TFLOP/s", "frac": achieved / PEAK_F32_TFLOPS, "traffic": None,
+                     "unit": "TFLOP/s", "frac": achieved / PEAK_F32_TFLOPS, "traffic": traffic,
                      "flops_per_launch": fl[dom[0]], "avg_launch_ms": dom[1]},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

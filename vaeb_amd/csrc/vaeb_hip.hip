@@ -290,7 +290,7 @@ int enqueue_train_step(vaeb_ctx* c, bool prof) {
     }
 
     // P8: grouped weight gradients (+ fused prior/Adagrad when single rank)
-    const bool dp = c->comm != nullptr && c->world > 1;
+    const bool dp = c->comm != nullptr;  // any communicator (also world 1) takes the all-reduce path
     WGradArgs w{};
     const int bo = gaussian(c) ? 6 : 5;
     auto add = [&](int gi, const float* at, int ld_at, int klim, int at_is_x, int rowsW, const float* b0,

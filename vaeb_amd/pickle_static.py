@@ -209,17 +209,29 @@ def _dtype_of(obj):
     return None
 
 
+_RECONSTRUCT = {("numpy.core.multiarray", "_reconstruct"), ("numpy._core.multiarray", "_reconstruct")}
+
+
+def _as_bytes(raw):
+    # protocol-2 pickles written by Python 3 carry bytes as _codecs.encode(text, 'latin1');
+    # that one pattern is decoded here as data (nothing is called).
+    if isinstance(raw, Reduce) and raw.func == ("_codecs", "encode") and len(raw.args) == 2 \
+            and raw.args[1] == "latin1" and isinstance(raw.args[0], str):
+        return raw.args[0].encode("latin1")
+    if isinstance(raw, str):
+        return raw.encode("latin1")
+    return raw
+
+
 def to_array(obj):
     """Turn the inert ndarray-reconstruct record into a numpy array (None if not one)."""
     if not isinstance(obj, Reduce):
         return None
-    if obj.func == ("numpy.core.multiarray", "_reconstruct") and obj.state is not None:
+    if obj.func in _RECONSTRUCT and obj.state is not None:
         st = obj.state
-        shape, dt, fortran, raw = st[1], _dtype_of(st[2]), st[3], st[4]
-        if dt is None:
+        shape, dt, fortran, raw = st[1], _dtype_of(st[2]), st[3], _as_bytes(st[4])
+        if dt is None or not isinstance(raw, (bytes, bytearray)):
             return None
-        if isinstance(raw, str):
-            raw = raw.encode("latin1")
         arr = np.frombuffer(bytes(raw), dtype=dt).copy()
         return arr.reshape(shape, order="F" if fortran else "C")
     return None
@@ -246,7 +258,8 @@ def find_arrays(obj, depth=0):
 
 
 def _is_randomstate(fr):
-    return isinstance(fr, Reduce) and fr.func == ("numpy.random", "__RandomState_ctor")
+    return isinstance(fr, Reduce) and fr.func in (("numpy.random", "__RandomState_ctor"),
+                                                  ("numpy.random._pickle", "__randomstate_ctor"))
 
 
 def read_mdl(path):
