@@ -39,14 +39,19 @@ def phase_flops(D, H, Z, B, L=1, gaussian=False):
         "p5_dhd": 2 * L * B * D * H * g,
         "p6_dz": 2 * L * B * H * Z,
         "p7_dh": 2 * B * 2 * Z * H,
-        "p8_wgrad": 2 * B * (D * H + H * 2 * Z) + 2 * L * B * (Z * H + H * D * g),
+        "p8_wgrad_w2": 2 * L * B * H * D * g,
+        "p8_wgrad_w1": 2 * L * B * Z * H,
+        "p8_wgrad_w3w45": 2 * B * (D * H + H * 2 * Z),
         "p23_heads_dechid": 2 * B * H * 2 * Z + 2 * L * B * Z * H,
-        "p67_dz_dh": 2 * L * B * H * Z + 2 * B * 2 * Z * H,
+        # horizontally fused launches (hfuse.hpp): phase + weight-gradient tiles in one grid
+        "p5_dhd_w2": 2 * L * B * D * H * g + 2 * L * B * H * D * g,
+        "p67_dz_dh_w1": 2 * L * B * H * Z + 2 * B * 2 * Z * H + 2 * L * B * Z * H,
     }
 
 
 KERNEL_SYMBOLS = {"p1_enc": "PEnc", "p23_heads_dechid": "heads_dechid_kernel", "p4_decout": "PDecOut",
-                  "p5_dhd": "PDhd", "p67_dz_dh": "dz_dh_kernel", "p8_wgrad": "wgrad_kernel"}
+                  "p5_dhd_w2": "vaeb::tile_wgrad_kernel", "p67_dz_dh_w1": "vaeb::dz_dh_wgrad_kernel",
+                  "p8_wgrad_w3w45": "vaeb::wgrad_kernel"}
 
 
 def committed_traffic(kernel):

@@ -196,14 +196,12 @@ __global__ __launch_bounds__(512) void heads_dechid_kernel(StepArgs a) {
 
 // ---------------------------------------------------------------------------- P67
 template <int NCT>
-__global__ __launch_bounds__(512) void dz_dh_kernel(StepArgs a) {
+DEV void dz_dh_body(const StepArgs& a, int i0) {
     __shared__ f32x4 red[8][NCT][64];
     __shared__ float dml[16][kKP];     // [dMu | dLv] tile (A operand of the dA3 GEMM)
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int li = lane & 15, q = lane >> 4;
-    const int i0 = blockIdx.x * 16;
     const int Z = a.Z, H = a.H;
-    VAEB_STAMP(a, 0);
     for (int e = threadIdx.x; e < 16 * kKP; e += 512) dml[e / kKP][e % kKP] = 0.f;
 
     // ---- prefetch: element-wise operands of this thread's (row, latent) element
@@ -367,6 +365,12 @@ __global__ __launch_bounds__(512) void dz_dh_kernel(StepArgs a) {
         tile3(t, bw, ldh(t * 16 + li));
     }
     VAEB_STAMP(a, 4);
+}
+
+template <int NCT>
+__global__ __launch_bounds__(512) void dz_dh_kernel(StepArgs a) {
+    VAEB_STAMP(a, 0);
+    dz_dh_body<NCT>(a, blockIdx.x * 16);
 }
 
 }  // namespace vaeb

@@ -1,0 +1,47 @@
+// Horizontally fused launches: a critical-path phase and an off-path weight-gradient
+// group share one grid, so the weight-gradient tiles run on the CUs the narrow phase
+// leaves idle, with no extra kernel boundary and no cross-stream dependency (a forked
+// side stream inside a hipGraph measured ~12 us/step slower than one stream).
+//
+//   P5  (dhd, 224 tiles at MNIST-20) + dW2|dW6 (104 tiles)   -- both need only P4's output
+//   P67 (dz/dh, 7 row blocks)         + dW1 (8 tiles)         -- both need only P5's output
+//
+// Phase blocks come first in the grid (they gate the next launch); all blocks are 512
+// threads, so the weight-gradient tiles use the 8-wave K-split form.
+#pragma once
+#include "fused.hpp"
+#include "kernels_aux.hpp"
+
+namespace vaeb {
+
+template <int WM, int WN, int KS, int NB, int GCH, class P, bool VEC>
+__global__ __launch_bounds__(512) void tile_wgrad_kernel(P p0, WGradArgs w, int ntile, int gx) {
+    static_assert(WM * WN * KS == 8, "fused launches are 512 threads");
+    __shared__ float sa[kWKB][kWP];
+    __shared__ float sb[kWKB][kWP];
+    const int bid = blockIdx.x;
+    if (bid < ntile) {
+        P p = p0;
+        VAEB_STAMP(p.a, 0);
+        tile_body<WM, WN, KS, NB, GCH, P>(p, bid % gx, bid / gx);
+        return;
+    }
+    if (w.dbg && threadIdx.x == 0) w.dbg[bid * 8 + 0] = __builtin_amdgcn_s_memrealtime();
+    wgrad_body<VEC, 8>(w, w.g[0], bid, sa, sb);
+}
+
+template <int NCT, bool VEC>
+__global__ __launch_bounds__(512) void dz_dh_wgrad_kernel(StepArgs a, WGradArgs w, int nrow) {
+    __shared__ float sa[kWKB][kWP];
+    __shared__ float sb[kWKB][kWP];
+    const int bid = blockIdx.x;
+    if (bid < nrow) {
+        VAEB_STAMP(a, 0);
+        dz_dh_body<NCT>(a, bid * 16);
+        return;
+    }
+    if (w.dbg && threadIdx.x == 0) w.dbg[bid * 8 + 0] = __builtin_amdgcn_s_memrealtime();
+    wgrad_body<VEC, 8>(w, w.g[0], bid, sa, sb);
+}
+
+}  // namespace vaeb

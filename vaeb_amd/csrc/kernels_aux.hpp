@@ -37,8 +37,7 @@ DEV double block_sum256(double v, double* sh) {
 }
 
 // Deterministic (fixed-order) reduction by one 256-thread workgroup.
-DEV void elbo_reduce(const ElboArgs& e) {
-    __shared__ double sh[256];
+DEV void elbo_reduce(const ElboArgs& e, double* sh) {
     double lp = 0, kl = 0, fv = 0;
     for (int64_t i = threadIdx.x; i < e.n_lp; i += 256) lp += e.lp_part[i];
     for (int64_t i = threadIdx.x; i < e.n_kl; i += 256) kl += e.kl_part[i];
@@ -64,130 +63,223 @@ DEV void elbo_reduce(const ElboArgs& e) {
     if (e.step) *e.step += 1;
 }
 
-__global__ __launch_bounds__(256) void elbo_kernel(ElboArgs e) { elbo_reduce(e); }
+__global__ __launch_bounds__(256) void elbo_kernel(ElboArgs e) {
+    __shared__ double sh[256];
+    elbo_reduce(e, sh);
+}
 
 // ----------------------------------------------------------------- optimizer rule
+// Parameters ping-pong between two arenas: a step reads theta_in (every phase of the
+// step sees the pre-update values, as Theano's simultaneous updates do, VAEB.py:438-442)
+// and writes theta_out, so the optimizer of one weight group can run while later phases
+// of the same step still read the old weights.  Accumulators are updated in place (only
+// the owning element reads them).
 struct OptArgs {
-    float* theta; float* acc; float* grad;
+    const float* theta_in; float* theta_out; float* acc; float* grad;
     float lr, eps, prior, decay;  // decay = lr*eps for the mean_map variant, else 0
     int update, store_grad;
 };
 
 // VAEB.getUpdates (VAEB.py:438-442) on one element, prior folded in (VAEB.py:389-390):
 //   g = dSGVB/dtheta - prior*theta;  acc += g^2;  theta += lr*g/(sqrt(acc)+eps) [- decay*theta^2]
-DEV void opt_apply(const OptArgs& o, int64_t idx, float dsg) {
-    if (o.store_grad) o.grad[idx] = dsg;
-    if (!o.update) return;
-    const float th = o.theta[idx];
+DEV float opt_rule(const OptArgs& o, float th, float& acc, float dsg) {
     const float g = dsg - o.prior * th;
-    const float a = o.acc[idx] + g * g;
-    o.acc[idx] = a;
-    o.theta[idx] = th + o.lr * g / (sqrtf(a) + o.eps) - o.decay * th * th;
+    acc += g * g;
+    return th + o.lr * g / (sqrtf(acc) + o.eps) - o.decay * th * th;
 }
 
-// ----------------------------------------------------------------- P8 weight gradients
-// C[i][j] = sum_k At[k][i] * Bm[k][j] over the minibatch rows k, with row i == rowsW the
-// all-ones row, so the bias gradient (the column sum of the delta) is the last row.
+// ----------------------------------------------------------------- weight gradients
+// C[i][j] = sum_k At[k][i] * B[k][j] over the minibatch rows k (K padded to 16; pad rows
+// of every delta are zero), i = weight row, with row i == rowsW the all-ones row so the
+// bias gradient (the column sum of the delta) is computed by the same MFMAs.  B is the
+// column concatenation of up to two delta arrays (dA2 | dA6 -> W2 | W6, dMu | dLv ->
+// W4 | W5).  A 256-thread workgroup owns a 64 x 64 tile: both operand panels are staged
+// through LDS with 16-byte loads (K rows x 64 floats, pitch 68 to spread the column
+// reads over the banks), then wave w computes rows 16w..16w+15 x 64 columns
+// (4 accumulators sharing one A fragment).  The epilogue applies prior + Adagrad
+// (theta / acc prefetched before the panels) or stores the gradient (DP / introspection).
+constexpr int kWT = 64;
+constexpr int kWKB = 128;
+constexpr int kWP = 68;
+
 struct WGroup {
     const float* at; int ld_at; int klim_at; int at_is_x;
     int rowsW;
-    const float* bm0; const float* bm1; int ld_b; int nb;
-    int N, K;
+    const float* b0; int ld0; int N0;
+    const float* b1; int ld1; int N1;
+    int K;
     int64_t offW0, offb0, offW1, offb1;
-    int tiles_n, wg_begin, wg_end;
+    int tiles_j, wg_begin, wg_end;
 };
 
 struct WGradArgs {
-    WGroup g[4];
+    WGroup g[2];
     int ngroups, total_wgs;
     OptArgs opt;
     ElboArgs elbo;
+    int with_elbo;
     const float* xbase; const int* cur_batch; int64_t batch_stride;
     int64_t P;
     uint64_t* dbg;
 };
 
-struct WGProb {
-    const WGroup* g;
-    rsrc_t bat, bb0, bb1;
-    DEV f32x4 a4(int i, int k) const {
-        f32x4 v = mc4(bat, g->ld_at, i, k, g->rowsW, g->klim_at);
-        const bool one = i == g->rowsW;  // the all-ones row (bias gradient), branch-free
-        v.x = one ? ((k + 0 < g->K) ? 1.f : 0.f) : v.x;
-        v.y = one ? ((k + 1 < g->K) ? 1.f : 0.f) : v.y;
-        v.z = one ? ((k + 2 < g->K) ? 1.f : 0.f) : v.z;
-        v.w = one ? ((k + 3 < g->K) ? 1.f : 0.f) : v.w;
-        return v;
-    }
-    DEV f32x4 b4(int j, int k, int w) const { return mc4(w ? bb1 : bb0, g->ld_b, j, k, g->N, g->K); }
-};
+// One 64 x 64 tile of group g (passed with a compile-time index, so its fields are
+// scalar kernel-argument loads; a dynamic index made hipcc fetch them with serialized
+// per-lane vector loads).  NWV = 4 waves (standalone launch) or 8 (a 512-thread fused
+// launch): waves w and w + 4 then take alternate K chunks and are summed through LDS.
+template <bool VEC, int NWV>
+DEV void wgrad_body(const WGradArgs& p, const WGroup& g, int bid, float (*sa)[kWP], float (*sb)[kWP]) {
+    static_assert(NWV == 4 || NWV == 8, "wgrad: 4 or 8 waves");
+    constexpr int NTH = 64 * NWV;
+    // resolve the batch pointer first: its load must not queue behind the prefetches below
+    const float* at = g.at_is_x ? p.xbase + (int64_t)__builtin_amdgcn_readfirstlane(*p.cur_batch) * p.batch_stride : g.at;
+    const rsrc_t ba = mkbuf(at, (int64_t)g.klim_at * g.ld_at * 4);
+    const int lt = bid - g.wg_begin;
+    const int i0 = (lt / g.tiles_j) * kWT, j0 = (lt % g.tiles_j) * kWT;
+    const int lane = threadIdx.x & 63, wave = (threadIdx.x >> 6) & 3, kh = threadIdx.x >> 8;
+    const int li = lane & 15, q = lane >> 4;
+    const int NT = g.N0 + g.N1;
 
-template <int NB>
-DEV void wgrad_tile(const WGradArgs& p, const WGroup& g, const float* at, int m0, int n0, int64_t P) {
-    f32x4 acc[NB];
-#pragma unroll
-    for (int w = 0; w < NB; ++w) acc[w] = zero4();
-    const int lane = threadIdx.x & 63;
-    const int j = n0 + (lane & 15);
-    const rsrc_t bth = mkbuf(p.opt.theta, P * 4), bac = mkbuf(p.opt.acc, P * 4), bgr = mkbuf(p.opt.grad, P * 4);
-    // prefetch theta / acc of this lane's outputs so the optimizer epilogue does not pay
-    // a second memory round trip after the MFMA chain (byte offsets; kOOB = masked)
-    uint32_t off[4][NB];
-    float th[4][NB], ac[4][NB];
+    // ---- prefetch theta / acc of this lane's 16 outputs (rows i0+16w+4q+r, cols j0+16t+li)
     const bool upd = p.opt.update != 0;
+    const rsrc_t bth = mkbuf(p.opt.theta_in, p.P * 4), bac = mkbuf(p.opt.acc, p.P * 4);
+    uint32_t off[4][4];
+    float th[4][4], ac[4][4];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-        const int i = m0 + 4 * (lane >> 4) + r;
-        const bool ok = j < g.N && i <= g.rowsW;
+    for (int t = 0; t < 4; ++t) {
+        const int j = j0 + 16 * t + li;
+        const bool s1 = j >= g.N0;
+        const int jj = s1 ? j - g.N0 : j;
+        const int nrow = s1 ? g.N1 : g.N0;
 #pragma unroll
-        for (int w = 0; w < NB; ++w) {
-            const int64_t idx = (i < g.rowsW) ? (w ? g.offW1 : g.offW0) + (int64_t)i * g.N + j : (w ? g.offb1 : g.offb0) + j;
-            off[r][w] = ok ? (uint32_t)idx * 4u : kOOB;
-            th[r][w] = upd ? bld(bth, off[r][w]) : 0.f;
-            ac[r][w] = upd ? bld(bac, off[r][w]) : 0.f;
+        for (int r = 0; r < 4; ++r) {
+            const int i = i0 + 16 * wave + 4 * q + r;
+            const bool ok = j < NT && i <= g.rowsW;
+            const int64_t idx = (i < g.rowsW) ? (s1 ? g.offW1 : g.offW0) + (int64_t)i * nrow + jj
+                                              : (s1 ? g.offb1 : g.offb0) + jj;
+            off[t][r] = ok ? (uint32_t)idx * 4u : kOOB;
+            // unconditional loads (no branch): the waitcnt pass then sees them retired
+            // by the first panel wait instead of re-waiting after every epilogue store
+            const uint32_t lo = (upd && kh == 0) ? off[t][r] : kOOB;
+            th[t][r] = bld(bth, lo);
+            ac[t][r] = bld(bac, lo);
         }
     }
-    WGProb prob{&g, mkbuf(at, (int64_t)g.klim_at * g.ld_at * 4), mkbuf(g.bm0, (int64_t)g.K * g.ld_b * 4),
-                mkbuf(g.bm1 ? g.bm1 : g.bm0, (int64_t)g.K * g.ld_b * 4)};
-    if (m0 <= g.rowsW && n0 < g.N) wave_mainloop<NB, 1, 8>(prob, m0 + (lane & 15), n0 + (lane & 15), g.K, 0, acc);
-    if (p.dbg && threadIdx.x == 0) p.dbg[blockIdx.x * 8 + 1] = __builtin_amdgcn_s_memrealtime();
-    // out-of-range byte offsets make the masked buffer stores no-ops
+
+    // ---- K loop over LDS stages of kWKB rows
+    const rsrc_t bb0 = mkbuf(g.b0, (int64_t)g.K * g.ld0 * 4);
+    const rsrc_t bb1 = mkbuf(g.b1 ? g.b1 : g.b0, (int64_t)g.K * (g.b1 ? g.ld1 : g.ld0) * 4);
+    // VEC (chosen on the host): every panel row is 16-byte aligned with widths % 4 == 0
+    constexpr bool va = VEC, vb = VEC;
+    f32x4 acc[4];
 #pragma unroll
-    for (int r = 0; r < 4; ++r)
+    for (int t = 0; t < 4; ++t) acc[t] = zero4();
+    int kb = 0;
+    do {  // K >= 1 always; a do-loop keeps the pre-loop loads off the exit path
+        // stage the panels: element e = (row kr, float4 column c4).  All 16 loads of a
+        // thread are issued before the first LDS store (one memory round trip).
+        constexpr int NU = (kWKB * 16) / NTH;
+        f32x4 ra[NU], rb[NU];
 #pragma unroll
-        for (int w = 0; w < NB; ++w) {
-            const float dsg = acc[w][r];
-            if (p.opt.store_grad) bst(bgr, off[r][w], dsg);
-            if (upd) {
-                const float t0 = th[r][w];
-                const float g2 = dsg - p.opt.prior * t0;
-                const float a2 = ac[r][w] + g2 * g2;
-                bst(bac, off[r][w], a2);
-                bst(bth, off[r][w], t0 + p.opt.lr * g2 / (sqrtf(a2) + p.opt.eps) - p.opt.decay * t0 * t0);
+        for (int u = 0; u < NU; ++u) {
+            const int e = threadIdx.x + NTH * u;
+            const int kr = e >> 4, c4 = e & 15;
+            const int k = kb + kr;
+            const int i = i0 + 4 * c4, j = j0 + 4 * c4;
+            if (va) {
+                ra[u] = bld4(ba, (k < g.klim_at && i < g.rowsW) ? (uint32_t)(k * g.ld_at + i) * 4u : kOOB);
+            } else {
+#pragma unroll
+                for (int s = 0; s < 4; ++s)
+                    ra[u][s] = bld(ba, (k < g.klim_at && i + s < g.rowsW) ? (uint32_t)(k * g.ld_at + i + s) * 4u : kOOB);
+            }
+            if (vb) {
+                const bool in0 = j < g.N0;
+                const uint32_t o0 = (k < g.K && in0) ? (uint32_t)(k * g.ld0 + j) * 4u : kOOB;
+                const uint32_t o1 = (k < g.K && !in0 && j - g.N0 < g.N1) ? (uint32_t)(k * g.ld1 + j - g.N0) * 4u : kOOB;
+                rb[u] = in0 ? bld4(bb0, o0) : bld4(bb1, o1);
+            } else {
+#pragma unroll
+                for (int s = 0; s < 4; ++s) {
+                    const int jj = j + s;
+                    const bool in0 = jj < g.N0;
+                    rb[u][s] = in0 ? bld(bb0, (k < g.K) ? (uint32_t)(k * g.ld0 + jj) * 4u : kOOB)
+                                   : bld(bb1, (k < g.K && jj - g.N0 < g.N1) ? (uint32_t)(k * g.ld1 + jj - g.N0) * 4u : kOOB);
+                }
             }
         }
+#pragma unroll
+        for (int u = 0; u < NU; ++u) {
+            const int e = threadIdx.x + NTH * u;
+            const int kr = e >> 4, c4 = e & 15;
+            const int i = i0 + 4 * c4;
+            // the all-ones row (bias gradient) for every batch row of the padded K
+            f32x4 v = ra[u];
+#pragma unroll
+            for (int s = 0; s < 4; ++s) v[s] = (i + s == g.rowsW) ? ((kb + kr < g.K) ? 1.f : 0.f) : v[s];
+            *reinterpret_cast<f32x4*>(&sa[kr][4 * c4]) = v;
+            *reinterpret_cast<f32x4*>(&sb[kr][4 * c4]) = rb[u];
+        }
+        __syncthreads();
+        const int nch = min(kWKB, g.K - kb) >> 4;
+        for (int c = kh; c < nch; c += NWV / 4) {
+            const int kk = 16 * c + 4 * q;
+            f32x4 a4;
+#pragma unroll
+            for (int s = 0; s < 4; ++s) a4[s] = sa[kk + s][16 * wave + li];
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                f32x4 b4;
+#pragma unroll
+                for (int s = 0; s < 4; ++s) b4[s] = sb[kk + s][16 * t + li];
+                acc[t] = mfma4(a4, b4, acc[t]);
+            }
+        }
+        __syncthreads();
+        kb += kWKB;
+    } while (kb < g.K);
+    if constexpr (NWV == 8) {  // fold the odd-chunk half into waves 0..3 (sa is free again)
+        f32x4* red = reinterpret_cast<f32x4*>(&sa[0][0]);
+        if (kh == 1)
+#pragma unroll
+            for (int t = 0; t < 4; ++t) red[(wave * 4 + t) * 64 + lane] = acc[t];
+        __syncthreads();
+        if (kh == 1) return;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) acc[t] += red[(wave * 4 + t) * 64 + lane];
+    }
+    if (p.dbg && threadIdx.x == 0) p.dbg[bid * 8 + 1] = __builtin_amdgcn_s_memrealtime();
+
+    // ---- epilogue: out-of-range byte offsets make masked buffer stores no-ops
+    const rsrc_t bto = mkbuf(p.opt.theta_out, p.P * 4), bgr = mkbuf(p.opt.grad, p.P * 4);
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const float dsg = acc[t][r];
+            if (p.opt.store_grad) bst(bgr, off[t][r], dsg);
+            if (upd) {
+                float a2 = ac[t][r];
+                const float nt = opt_rule(p.opt, th[t][r], a2, dsg);
+                bst(bac, off[t][r], a2);
+                bst(bto, off[t][r], nt);
+            }
+        }
+    if (p.dbg && threadIdx.x == 0) p.dbg[bid * 8 + 3] = __builtin_amdgcn_s_memrealtime();
 }
 
+template <bool VEC>
 __global__ __launch_bounds__(256) void wgrad_kernel(WGradArgs p) {
+    __shared__ float sa[kWKB][kWP];
+    __shared__ float sb[kWKB][kWP];
     const int bid = blockIdx.x;
     if (p.dbg && threadIdx.x == 0) p.dbg[bid * 8 + 0] = __builtin_amdgcn_s_memrealtime();
     if (bid >= p.total_wgs) {  // the extra workgroup: ELBO of this step
-        elbo_reduce(p.elbo);
+        elbo_reduce(p.elbo, reinterpret_cast<double*>(&sa[0][0]));
         return;
     }
-    int gi = 0;
-#pragma unroll
-    for (int t = 1; t < 4; ++t)
-        if (t < p.ngroups && bid >= p.g[t].wg_begin) gi = t;
-    const WGroup& g = p.g[gi];
-    const float* at = g.at_is_x ? p.xbase + (int64_t)(*p.cur_batch) * p.batch_stride : g.at;
-    const int lt = bid - g.wg_begin;
-    const int wave = threadIdx.x >> 6;
-    const int m0 = ((lt / g.tiles_n) * 2 + (wave >> 1)) * 16;
-    const int n0 = ((lt % g.tiles_n) * 2 + (wave & 1)) * 16;
-    if (g.nb == 2) wgrad_tile<2>(p, g, at, m0, n0, p.P);
-    else wgrad_tile<1>(p, g, at, m0, n0, p.P);
-    if (p.dbg && threadIdx.x == 0) p.dbg[bid * 8 + 3] = __builtin_amdgcn_s_memrealtime();
+    if (p.ngroups > 1 && bid >= p.g[1].wg_begin) wgrad_body<VEC, 4>(p, p.g[1], bid, sa, sb);
+    else wgrad_body<VEC, 4>(p, p.g[0], bid, sa, sb);
 }
 
 // ----------------------------------------------------------------- DP optimizer
@@ -195,9 +287,11 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WGradArgs p) {
 // added once (so every rank applies the identical update).
 __global__ __launch_bounds__(256) void adagrad_kernel(OptArgs o, int64_t P, ElboArgs e) {
     const int64_t stride = (int64_t)gridDim.x * 256;
-    OptArgs u = o;
-    u.store_grad = 0;
-    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < P; i += stride) opt_apply(u, i, o.grad[i]);
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < P; i += stride) {
+        float a = o.acc[i];
+        o.theta_out[i] = opt_rule(o, o.theta_in[i], a, o.grad[i]);
+        o.acc[i] = a;
+    }
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         const double v = (double)o.grad[P] * e.inv_bglob;
         *e.elbo_out = (float)v;

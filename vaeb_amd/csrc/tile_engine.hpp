@@ -158,19 +158,20 @@ DEV bool ks_reduce(f32x4 (&acc)[NB], int wave, int ks) {
 //                  Pre prefetch(int m0, int n0) const;   (epilogue operands, issued
 //                      before the main loop so they ride the same memory round trip)
 //                  void epilogue(int m0, int n0, const f32x4 (&acc)[NB], const Pre&) const;
+// One output tile (bx, by) of phase P; the standalone kernel and the horizontally fused
+// launches (phase tiles + weight-gradient tiles in one grid) share this body.
 template <int WM, int WN, int KS, int NB, int GCH, class P>
-__global__ __launch_bounds__(64 * WM * WN * KS) void tile_kernel(P p0) {
+DEV void tile_body(P& p, int bx, int by) {
     constexpr int NW = WM * WN * KS;
-    P p = p0;
-    VAEB_STAMP(p.a, 0);
-    if (p.a.dbg && threadIdx.x == 0) p.a.dbg[(blockIdx.x + (uint64_t)blockIdx.y * gridDim.x) * 8 + 6] = __builtin_amdgcn_s_memtime();
+    const int lin = bx + by * (int)gridDim.x;  // 1-D fused grids have gridDim.y == 1 and by == 0
+    if (p.a.dbg && threadIdx.x == 0) p.a.dbg[(uint64_t)lin * 8 + 6] = __builtin_amdgcn_s_memtime();
     p.prepare();
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
     const int ks = wave % KS;
     const int t = wave / KS;
-    const int m0 = (blockIdx.x * WM + t / WN) * 16;
-    const int n0 = (blockIdx.y * WN + t % WN) * 16;
+    const int m0 = (bx * WM + t / WN) * 16;
+    const int n0 = (by * WN + t % WN) * 16;
     f32x4 acc[NB];
 #pragma unroll
     for (int w = 0; w < NB; ++w) acc[w] = zero4();
@@ -183,7 +184,14 @@ __global__ __launch_bounds__(64 * WM * WN * KS) void tile_kernel(P p0) {
     if (m0 >= p.M || n0 >= p.N) return;
     p.epilogue(m0, n0, acc, pre);
     VAEB_STAMP(p.a, 3);
-    if (p.a.dbg && threadIdx.x == 0) p.a.dbg[(blockIdx.x + (uint64_t)blockIdx.y * gridDim.x) * 8 + 7] = __builtin_amdgcn_s_memtime();
+    if (p.a.dbg && threadIdx.x == 0) p.a.dbg[(uint64_t)lin * 8 + 7] = __builtin_amdgcn_s_memtime();
+}
+
+template <int WM, int WN, int KS, int NB, int GCH, class P>
+__global__ __launch_bounds__(64 * WM * WN * KS) void tile_kernel(P p0) {
+    P p = p0;
+    VAEB_STAMP(p.a, 0);
+    tile_body<WM, WN, KS, NB, GCH, P>(p, blockIdx.x, blockIdx.y);
 }
 
 // ------------------------------------------------------------------ Philox4x32-10

@@ -17,7 +17,7 @@
 #include <vector>
 
 #include "../../include/vaeb_hip.h"
-#include "kernels_aux.hpp"
+#include "hfuse.hpp"
 
 using namespace vaeb;
 
@@ -61,20 +61,22 @@ constexpr int kGraphSteps = 32;
 constexpr int kMaxProfKernels = 16;
 constexpr int kDbgWG = 1024;      // diagnostics: stamp slots per launch (workgroups)
 
-const char* kKernelNames[] = {"p1_enc", "p2_heads", "p3_dechid", "p4_decout", "p5_dhd", "p6_dz",
-                              "p7_dh", "p8_wgrad", "allreduce", "adagrad", "fv_update", "elbo",
-                              "p23_heads_dechid", "p67_dz_dh"};
+const char* kKernelNames[] = {"p1_enc", "p2_heads", "p3_dechid", "p4_decout", "p5_dhd_w2", "p6_dz",
+                              "p7_dh", "p8_wgrad_w3w45", "allreduce", "adagrad", "fv_update", "elbo",
+                              "p23_heads_dechid", "p67_dz_dh_w1", "p8_wgrad_w2", "p8_wgrad_w1"};
 
 }  // namespace
 
 struct vaeb_ctx {
     vaeb_config c{};
-    hipStream_t s = nullptr;
+    hipStream_t s = nullptr;   // every step launch goes to this one stream
     int64_t P = 0;
     int nparams = 0;
     int64_t off[12] = {};   // arena offsets, reference order
     // arenas
-    float *theta = nullptr, *acc = nullptr, *grad = nullptr;
+    float* theta2[2] = {nullptr, nullptr};   // ping-pong parameter arenas
+    int par = 0;                              // arena holding the current parameters
+    float *acc = nullptr, *grad = nullptr;
     float *fvmu = nullptr, *fvsg = nullptr, *fvam = nullptr, *fvas = nullptr, *fv_part = nullptr;
     // data
     float* data = nullptr;
@@ -102,7 +104,7 @@ struct vaeb_ctx {
     double* h_d2 = nullptr;
     hipEvent_t ctl_ev = nullptr;
     // graphs
-    hipGraphExec_t g1 = nullptr, gS = nullptr;
+    hipGraphExec_t g1[2] = {nullptr, nullptr}, gS = nullptr;
     bool graph_failed = false;
     // comm
     ncclComm_t comm = nullptr;
@@ -122,14 +124,14 @@ bool gaussian(const vaeb_ctx* c) { return c->c.decoder == VAEB_DEC_GAUSSIAN; }
 
 uint64_t* next_dbg(vaeb_ctx* c) { return c->dbg ? c->dbg + (size_t)(c->dbg_slot++) * kDbgWG * 8 : nullptr; }
 
-StepArgs make_args(vaeb_ctx* c, int Mb, int mode, const float* xbase, bool train) {
+StepArgs make_args(vaeb_ctx* c, int par, int Mb, int mode, const float* xbase, bool train) {
     StepArgs a{};
     const vaeb_config& g = c->c;
     a.D = g.D; a.H = g.H; a.Z = g.Z; a.L = g.L;
     a.Mb = Mb; a.Mbp = r16(Mb); a.Me = g.L * a.Mbp;
     a.dec = g.decoder; a.est = g.estimator; a.mode = mode;
     a.sc = (g.objective == VAEB_OBJ_MEAN_MAP) ? 1.0f / (float)g.B_global : 1.0f;
-    const float* t = c->theta;
+    const float* t = c->theta2[par];
     const bool gs = gaussian(c);
     // reference order: W3,W4,W5,W1,W2,(W6),b3,b4,b5,b1,b2,(b6)
     a.W3 = t + c->off[0]; a.W4 = t + c->off[1]; a.W5 = t + c->off[2]; a.W1 = t + c->off[3];
@@ -235,9 +237,11 @@ int enqueue_forward(vaeb_ctx* c, const StepArgs& a0, Prof& pr) {
     return 0;
 }
 
-OptArgs make_opt(vaeb_ctx* c, bool update, bool store) {
+OptArgs make_opt(vaeb_ctx* c, int par, bool update, bool store) {
     OptArgs o{};
-    o.theta = c->theta; o.acc = c->acc; o.grad = c->grad;
+    o.theta_in = c->theta2[par];
+    o.theta_out = c->theta2[par ^ 1];
+    o.acc = c->acc; o.grad = c->grad;
     o.lr = c->c.lr; o.eps = c->c.adagrad_eps;
     const bool mean = c->c.objective == VAEB_OBJ_MEAN_MAP;
     o.prior = mean ? 0.f : 1.f;
@@ -247,11 +251,72 @@ OptArgs make_opt(vaeb_ctx* c, bool update, bool store) {
     return o;
 }
 
-int enqueue_train_step(vaeb_ctx* c, bool prof) {
+// Weight-gradient arguments over `n` groups whose tiles start at block `base` of the
+// launch (+ the ELBO workgroup when e != nullptr).  *vec: 16-byte panel loads are legal.
+int prep_wgrad(vaeb_ctx* c, const WGroup* groups, int n, const OptArgs& opt, const ElboArgs* e, const StepArgs& a,
+               int base, WGradArgs& w, bool& vec) {
+    w = WGradArgs{};
+    int begin = base;
+    if (n < 1 || n > 2) return fail(VAEB_ERR_ARG, "internal: 1 or 2 weight-gradient groups per launch");
+    for (int gi = 0; gi < n; ++gi) {
+        w.g[gi] = groups[gi];
+        WGroup& G = w.g[gi];
+        G.tiles_j = cdiv(G.N0 + G.N1, kWT);
+        G.wg_begin = begin;
+        G.wg_end = begin + cdiv(G.rowsW + 1, kWT) * G.tiles_j;
+        begin = G.wg_end;
+    }
+    w.ngroups = n;
+    w.total_wgs = begin;
+    w.opt = opt;
+    w.with_elbo = e != nullptr;
+    if (e) w.elbo = *e;
+    w.xbase = c->data; w.cur_batch = c->ictl + 1; w.batch_stride = a.batch_stride; w.P = c->P;
+    w.dbg = a.dbg;
+    // 16-byte panel loads need every panel row aligned with widths % 4 == 0 (the
+    // activation buffers are hipMalloc'd; X rows are D floats apart)
+    vec = true;
+    auto al = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+    for (int gi = 0; gi < n; ++gi) {
+        const WGroup& G = w.g[gi];
+        vec = vec && (G.ld_at % 4 == 0) && (G.rowsW % 4 == 0) && (G.at_is_x ? al(c->data) : al(G.at)) &&
+              (G.ld0 % 4 == 0) && (G.N0 % 4 == 0) && al(G.b0) &&
+              (G.N1 == 0 || ((G.ld1 % 4 == 0) && (G.N1 % 4 == 0) && al(G.b1)));
+    }
+    return 0;
+}
+
+// A standalone weight-gradient launch (256-thread blocks).
+int launch_wgrad(vaeb_ctx* c, hipStream_t s, const WGroup* groups, int n, const OptArgs& opt, const ElboArgs* e,
+                 const StepArgs& a) {
+    WGradArgs w;
+    bool vec;
+    if (int rc = prep_wgrad(c, groups, n, opt, e, a, 0, w, vec)) return rc;
+    if (vec) hipLaunchKernelGGL(wgrad_kernel<true>, dim3(w.total_wgs + (e ? 1 : 0)), dim3(256), 0, s, w);
+    else hipLaunchKernelGGL(wgrad_kernel<false>, dim3(w.total_wgs + (e ? 1 : 0)), dim3(256), 0, s, w);
+    CHECK_LAUNCH();
+    return 0;
+}
+
+WGroup make_group(vaeb_ctx* c, const float* at, int ld_at, int klim, int at_is_x, int rowsW, const float* b0, int ld0,
+                  int N0, const float* b1, int ld1, int N1, int K, int pW0, int pb0, int pW1, int pb1) {
+    WGroup G{};
+    G.at = at; G.ld_at = ld_at; G.klim_at = klim; G.at_is_x = at_is_x; G.rowsW = rowsW;
+    G.b0 = b0; G.ld0 = ld0; G.N0 = N0; G.b1 = b1; G.ld1 = ld1; G.N1 = N1; G.K = K;
+    G.offW0 = c->off[pW0]; G.offb0 = c->off[pb0];
+    G.offW1 = pW1 >= 0 ? c->off[pW1] : 0; G.offb1 = pb1 >= 0 ? c->off[pb1] : 0;
+    return G;
+}
+
+// One training step reading parameter arena `par` and writing arena par ^ 1.
+// One stream: P1 -> P23 -> P4 -> [P5 | dW2 (| dW6)] -> [P67 | dW1] -> [dW3 | dW45 + ELBO]
+// (bracketed groups share one grid, see hfuse.hpp); DP adds all-reduce -> Adagrad.
+// `prof` brackets every launch with timing events.
+int enqueue_train_step(vaeb_ctx* c, int par, bool prof) {
     Prof pr{c, prof};
     const vaeb_config& g = c->c;
     hipStream_t s = c->s;
-    StepArgs a = make_args(c, g.B, g.estimator == VAEB_EST_FV ? MODE_EVAL : MODE_TRAIN, c->data, true);
+    StepArgs a = make_args(c, par, g.B, g.estimator == VAEB_EST_FV ? MODE_EVAL : MODE_TRAIN, c->data, true);
     if (int rc = enqueue_forward(c, a, pr)) return rc;
     ElboArgs e = base_elbo(c, a);
     e.elbo_out = c->elbo_out; e.epoch = c->epoch; e.cursor = c->ictl; e.step = c->step;
@@ -270,68 +335,83 @@ int enqueue_train_step(vaeb_ctx* c, bool prof) {
         c->prof_n = pr.k;
         return 0;
     }
+    const bool dp = c->comm != nullptr;  // any communicator (also world 1) takes the all-reduce path
+    const OptArgs opt = make_opt(c, par, !dp, dp || g.keep_grads != 0);
+    const int bo = gaussian(c) ? 6 : 5;
+    const bool gs = gaussian(c);
+
+    // P5 + dW2 (| dW6) = [hd|1]^T [dA2 (| dA6)] in one grid: both need only P4's outputs
     a.dbg = next_dbg(c);
-    pr.mark(4);
-    launch_bigk<1>(s, PDhd{a, a.Me, a.H, gaussian(c) ? ((a.D + 3) & ~3) + a.D : a.D});
-    CHECK_LAUNCH();
-    a.dbg = next_dbg(c);
-    if (fused_latent(c)) {
-        pr.mark(13);
-        if (a.Z <= 16) hipLaunchKernelGGL(dz_dh_kernel<1>, dim3(a.Mbp / 16), dim3(512), 0, s, a);
-        else hipLaunchKernelGGL(dz_dh_kernel<2>, dim3(a.Mbp / 16), dim3(512), 0, s, a);
-        CHECK_LAUNCH();
-    } else {
-        pr.mark(5);
-        launch_tile<1, 1, 4, 1, 8>(s, PDz{a, a.Me, a.Z, a.H});
-        CHECK_LAUNCH();
-        pr.mark(6);
-        launch_tile<1, 4, 1, 1, 8>(s, PDh{a, a.Mbp, a.H, 2 * a.Z});
+    {
+        WGroup g4 = make_group(c, c->hd, a.H, a.Me, 0, a.H, c->dA2, a.D, a.D, gs ? c->dA6 : nullptr, a.D, gs ? a.D : 0,
+                               a.Me, 4, bo + 4, gs ? 5 : -1, gs ? bo + 5 : -1);
+        const PDhd p5{a, a.Me, a.H, gs ? ((a.D + 3) & ~3) + a.D : a.D};
+        const int gx = cdiv(p5.M, 16), ntile = gx * cdiv(p5.N, 16);
+        WGradArgs w;
+        bool vec;
+        if (int rc = prep_wgrad(c, &g4, 1, opt, nullptr, a, ntile, w, vec)) return rc;
+        const dim3 grid(w.total_wgs);
+        pr.mark(4);
+        if (cdiv(cdiv(p5.K, 16), 8) <= 4) {
+            if (vec) hipLaunchKernelGGL((tile_wgrad_kernel<1, 1, 8, 1, 4, PDhd, true>), grid, dim3(512), 0, s, p5, w, ntile, gx);
+            else hipLaunchKernelGGL((tile_wgrad_kernel<1, 1, 8, 1, 4, PDhd, false>), grid, dim3(512), 0, s, p5, w, ntile, gx);
+        } else {
+            if (vec) hipLaunchKernelGGL((tile_wgrad_kernel<1, 1, 8, 1, 8, PDhd, true>), grid, dim3(512), 0, s, p5, w, ntile, gx);
+            else hipLaunchKernelGGL((tile_wgrad_kernel<1, 1, 8, 1, 8, PDhd, false>), grid, dim3(512), 0, s, p5, w, ntile, gx);
+        }
         CHECK_LAUNCH();
     }
-
-    // P8: grouped weight gradients (+ fused prior/Adagrad when single rank)
-    const bool dp = c->comm != nullptr;  // any communicator (also world 1) takes the all-reduce path
-    WGradArgs w{};
-    const int bo = gaussian(c) ? 6 : 5;
-    auto add = [&](int gi, const float* at, int ld_at, int klim, int at_is_x, int rowsW, const float* b0,
-                   const float* b1, int ld_b, int nb, int N, int K, int pW0, int pb0, int pW1, int pb1) {
-        WGroup& G = w.g[gi];
-        G.at = at; G.ld_at = ld_at; G.klim_at = klim; G.at_is_x = at_is_x; G.rowsW = rowsW;
-        G.bm0 = b0; G.bm1 = b1; G.ld_b = ld_b; G.nb = nb; G.N = N; G.K = K;
-        G.offW0 = c->off[pW0]; G.offb0 = c->off[pb0];
-        G.offW1 = pW1 >= 0 ? c->off[pW1] : 0; G.offb1 = pb1 >= 0 ? c->off[pb1] : 0;
-        G.tiles_n = cdiv(N, 32);
-        const int tiles_m = cdiv(rowsW + 1, 32);
-        G.wg_begin = gi == 0 ? 0 : w.g[gi - 1].wg_end;
-        G.wg_end = G.wg_begin + tiles_m * G.tiles_n;
-    };
-    // G4 first: the largest group ([hd|1]^T [dA2 (|dA6)]) -> W2,b2 (W6,b6)
-    add(0, c->hd, a.H, a.Me, 0, a.H, c->dA2, gaussian(c) ? c->dA6 : nullptr, a.D, gaussian(c) ? 2 : 1,
-        a.D, a.Me, 4, bo + 4, gaussian(c) ? 5 : -1, gaussian(c) ? bo + 5 : -1);
-    // G1: [X|1]^T dA3 -> W3,b3
-    add(1, nullptr, a.D, a.Mb, 1, a.D, c->dA3, nullptr, a.H, 1, a.H, a.Mbp, 0, bo + 0, -1, -1);
-    // G3: [z|1]^T dA1 -> W1,b1
-    add(2, c->z, a.Z, a.Me, 0, a.Z, c->dA1, nullptr, a.H, 1, a.H, a.Me, 3, bo + 3, -1, -1);
-    // G2: [h|1]^T [dMu|dLv] -> (W4,b4), (W5,b5)
-    add(3, c->h, a.H, a.Mbp, 0, a.H, c->dMuLv, c->dMuLv + a.Z, 2 * a.Z, 2, a.Z, a.Mbp, 1, bo + 1, 2, bo + 2);
-    w.ngroups = 4;
-    w.total_wgs = w.g[3].wg_end;
-    w.opt = make_opt(c, !dp, dp || g.keep_grads != 0);
-    w.elbo = e;
-    if (dp) { w.elbo.dp_slot = c->grad + c->P; w.elbo.elbo_out = nullptr; w.elbo.cursor = nullptr; w.elbo.step = nullptr; }
-    w.xbase = c->data; w.cur_batch = c->ictl + 1; w.batch_stride = a.batch_stride; w.P = c->P;
-    w.dbg = next_dbg(c);
-    pr.mark(7);
-    hipLaunchKernelGGL(wgrad_kernel, dim3(w.total_wgs + 1), dim3(256), 0, s, w);
-    CHECK_LAUNCH();
+    // P67 (+ dW1 = [z|1]^T dA1 on the fused path): both need only P5's output
+    a.dbg = next_dbg(c);
+    {
+        WGroup g3 = make_group(c, c->z, a.Z, a.Me, 0, a.Z, c->dA1, a.H, a.H, nullptr, 0, 0, a.Me, 3, bo + 3, -1, -1);
+        if (fused_latent(c)) {
+            const int nrow = a.Mbp / 16;
+            WGradArgs w;
+            bool vec;
+            if (int rc = prep_wgrad(c, &g3, 1, opt, nullptr, a, nrow, w, vec)) return rc;
+            const dim3 grid(w.total_wgs);
+            pr.mark(13);
+            if (a.Z <= 16) {
+                if (vec) hipLaunchKernelGGL((dz_dh_wgrad_kernel<1, true>), grid, dim3(512), 0, s, a, w, nrow);
+                else hipLaunchKernelGGL((dz_dh_wgrad_kernel<1, false>), grid, dim3(512), 0, s, a, w, nrow);
+            } else {
+                if (vec) hipLaunchKernelGGL((dz_dh_wgrad_kernel<2, true>), grid, dim3(512), 0, s, a, w, nrow);
+                else hipLaunchKernelGGL((dz_dh_wgrad_kernel<2, false>), grid, dim3(512), 0, s, a, w, nrow);
+            }
+            CHECK_LAUNCH();
+        } else {
+            pr.mark(15);
+            if (int rc = launch_wgrad(c, s, &g3, 1, opt, nullptr, a)) return rc;
+            a.dbg = next_dbg(c);
+            pr.mark(5);
+            launch_tile<1, 1, 4, 1, 8>(s, PDz{a, a.Me, a.Z, a.H});
+            CHECK_LAUNCH();
+            a.dbg = next_dbg(c);
+            pr.mark(6);
+            launch_tile<1, 4, 1, 1, 8>(s, PDh{a, a.Mbp, a.H, 2 * a.Z});
+            CHECK_LAUNCH();
+        }
+    }
+    // dW3 = [X|1]^T dA3 and dW4|dW5 = [h|1]^T [dMu|dLv], plus the ELBO workgroup
+    {
+        WGroup g12[2] = {
+            make_group(c, nullptr, a.D, a.Mb, 1, a.D, c->dA3, a.H, a.H, nullptr, 0, 0, a.Mbp, 0, bo + 0, -1, -1),
+            make_group(c, c->h, a.H, a.Mbp, 0, a.H, c->dMuLv, 2 * a.Z, a.Z, c->dMuLv + a.Z, 2 * a.Z, a.Z, a.Mbp, 1,
+                       bo + 1, 2, bo + 2)};
+        ElboArgs e1 = e;
+        if (dp) { e1.dp_slot = c->grad + c->P; e1.elbo_out = nullptr; e1.cursor = nullptr; e1.step = nullptr; }
+        a.dbg = next_dbg(c);
+        pr.mark(7);
+        if (int rc = launch_wgrad(c, s, g12, 2, opt, &e1, a)) return rc;
+    }
     if (dp) {
         pr.mark(8);
         ncclResult_t r = ncclAllReduce(c->grad, c->grad, (size_t)c->P + 1, ncclFloat, ncclSum, c->comm, s);
         if (r != ncclSuccess) return fail(VAEB_ERR_COMM, "ncclAllReduce: %s", ncclGetErrorString(r));
         pr.mark(9);
-        OptArgs o = make_opt(c, true, false);
-        ElboArgs e2 = e;
-        hipLaunchKernelGGL(adagrad_kernel, dim3(512), dim3(256), 0, s, o, c->P, e2);
+        const OptArgs o = make_opt(c, par, true, false);
+        hipLaunchKernelGGL(adagrad_kernel, dim3(512), dim3(256), 0, s, o, c->P, e);
         CHECK_LAUNCH();
     }
     pr.mark(-1);
@@ -339,17 +419,23 @@ int enqueue_train_step(vaeb_ctx* c, bool prof) {
     return 0;
 }
 
+bool flips(const vaeb_ctx* c) { return c->c.estimator != VAEB_EST_FV; }
+
 void free_graphs(vaeb_ctx* c) {
-    if (c->g1) hipGraphExecDestroy(c->g1);
+    for (auto& g1 : c->g1) if (g1) hipGraphExecDestroy(g1);
     if (c->gS) hipGraphExecDestroy(c->gS);
-    c->g1 = c->gS = nullptr;
+    c->g1[0] = c->g1[1] = c->gS = nullptr;
 }
 
-int capture(vaeb_ctx* c, int nsteps, hipGraphExec_t* out) {
+// Capture nsteps consecutive steps starting from parameter arena `par`.
+int capture(vaeb_ctx* c, int nsteps, int par, hipGraphExec_t* out) {
     hipGraph_t gr = nullptr;
     HIP_TRY(hipStreamBeginCapture(c->s, hipStreamCaptureModeThreadLocal));
     int rc = 0;
-    for (int i = 0; i < nsteps && rc == 0; ++i) rc = enqueue_train_step(c, false);
+    for (int i = 0; i < nsteps && rc == 0; ++i) {
+        rc = enqueue_train_step(c, par, false);
+        if (flips(c)) par ^= 1;
+    }
     hipError_t e = hipStreamEndCapture(c->s, &gr);
     if (rc) { if (gr) hipGraphDestroy(gr); return rc; }
     if (e != hipSuccess) return fail(VAEB_ERR_HIP, "hipStreamEndCapture: %s", hipGetErrorString(e));
@@ -359,23 +445,37 @@ int capture(vaeb_ctx* c, int nsteps, hipGraphExec_t* out) {
     return 0;
 }
 
-// Enqueue n steps (graph replay when enabled, else eager launches).
+int step_eager(vaeb_ctx* c) {
+    if (int rc = enqueue_train_step(c, c->par, false)) return rc;
+    if (flips(c)) c->par ^= 1;
+    return 0;
+}
+
+// Enqueue n steps (graph replay when enabled, else eager launches).  Graphs: g1[par]
+// is one step from arena par; gS is kGraphSteps (even) steps from arena 0.
 int run_steps(vaeb_ctx* c, int n) {
     if (c->c.use_graph && !c->graph_failed) {
-        if (!c->g1) {
-            int rc = capture(c, 1, &c->g1);
-            if (rc == 0 && !c->gS) rc = capture(c, kGraphSteps, &c->gS);
-            if (rc) { c->graph_failed = true; free_graphs(c); hipGetLastError(); }
+        if (!c->gS) {
+            int rc = capture(c, 1, 0, &c->g1[0]);
+            if (rc == 0) rc = capture(c, 1, 1, &c->g1[1]);
+            if (rc == 0) rc = capture(c, kGraphSteps, 0, &c->gS);
+            if (rc) { c->graph_failed = true; free_graphs(c); (void)hipGetLastError(); }
         }
         if (!c->graph_failed) {
             int i = 0;
+            auto one = [&]() -> int {
+                HIP_TRY(hipGraphLaunch(c->g1[c->par], c->s));
+                if (flips(c)) c->par ^= 1;
+                return 0;
+            };
+            if (c->par != 0 && n > 0) { if (int rc = one()) return rc; ++i; }
             for (; i + kGraphSteps <= n; i += kGraphSteps) HIP_TRY(hipGraphLaunch(c->gS, c->s));
-            for (; i < n; ++i) HIP_TRY(hipGraphLaunch(c->g1, c->s));
+            for (; i < n; ++i) if (int rc = one()) return rc;
             return 0;
         }
     }
     for (int i = 0; i < n; ++i)
-        if (int rc = enqueue_train_step(c, false)) return rc;
+        if (int rc = step_eager(c)) return rc;
     return 0;
 }
 
@@ -438,7 +538,7 @@ int vaeb_create(const vaeb_config* cfg, vaeb_ctx** out) {
     hipError_t e = hipSetDevice(g.device);
     if (e != hipSuccess) { delete c; return fail(VAEB_ERR_HIP, "hipSetDevice(%d): %s", g.device, hipGetErrorString(e)); }
     e = hipStreamCreateWithFlags(&c->s, hipStreamNonBlocking);
-    if (e != hipSuccess) { delete c; return fail(VAEB_ERR_HIP, "hipStreamCreate: %s", hipGetErrorString(e)); }
+    if (e != hipSuccess) { delete c; return fail(VAEB_ERR_HIP, "stream/event create: %s", hipGetErrorString(e)); }
     const int64_t D = g.D, H = g.H, Z = g.Z;
     std::vector<int64_t> sz = {D * H, H * Z, H * Z, Z * H, H * D};
     if (gaussian(c)) sz.push_back(H * D);
@@ -451,7 +551,8 @@ int vaeb_create(const vaeb_config* cfg, vaeb_ctx** out) {
     c->cap = std::max(r16(g.B), r16(c->c.max_eval_rows));
     const int64_t R = c->cap, RL = (int64_t)c->cap * g.L;
     int rc = 0;
-    rc = rc ? rc : dalloc(&c->theta, c->P);
+    rc = rc ? rc : dalloc(&c->theta2[0], c->P);
+    rc = rc ? rc : dalloc(&c->theta2[1], c->P);
     rc = rc ? rc : dalloc(&c->acc, c->P);
     rc = rc ? rc : dalloc(&c->grad, c->P + 1);
     if (g.estimator == VAEB_EST_FV) {
@@ -502,7 +603,7 @@ int vaeb_destroy(vaeb_ctx* c) {
     if (c->s) hipStreamSynchronize(c->s);
     free_graphs(c);
     if (c->comm) ncclCommDestroy(c->comm);
-    float* fp[] = {c->theta, c->acc, c->grad, c->fvmu, c->fvsg, c->fvam, c->fvas, c->fv_part, c->data, c->xeval,
+    float* fp[] = {c->theta2[0], c->theta2[1], c->acc, c->grad, c->fvmu, c->fvsg, c->fvam, c->fvas, c->fv_part, c->data, c->xeval,
                    c->elbo_out, c->eps_in, c->h, c->mu, c->lv, c->eps, c->z, c->hd, c->y, c->dA2, c->dA6, c->dA1,
                    c->dZ, c->dMuLv, c->dA3, c->kl_part, c->lp_part};
     for (float* p : fp) if (p) hipFree(p);
@@ -548,8 +649,8 @@ static int xfer(vaeb_ctx* c, float* dev, const float* hin, float* hout, int64_t 
     return 0;
 }
 
-int vaeb_set_params(vaeb_ctx* c, const float* f, int64_t n) { return xfer(c, c ? c->theta : nullptr, f, nullptr, n, c ? c->P : 0); }
-int vaeb_get_params(vaeb_ctx* c, float* f, int64_t n) { return xfer(c, c ? c->theta : nullptr, nullptr, f, n, c ? c->P : 0); }
+int vaeb_set_params(vaeb_ctx* c, const float* f, int64_t n) { return xfer(c, c ? c->theta2[c->par] : nullptr, f, nullptr, n, c ? c->P : 0); }
+int vaeb_get_params(vaeb_ctx* c, float* f, int64_t n) { return xfer(c, c ? c->theta2[c->par] : nullptr, nullptr, f, n, c ? c->P : 0); }
 int vaeb_set_adagrad_state(vaeb_ctx* c, const float* f, int64_t n) { return xfer(c, c ? c->acc : nullptr, f, nullptr, n, c ? c->P : 0); }
 int vaeb_get_adagrad_state(vaeb_ctx* c, float* f, int64_t n) { return xfer(c, c ? c->acc : nullptr, nullptr, f, n, c ? c->P : 0); }
 int vaeb_get_grads(vaeb_ctx* c, float* f, int64_t n) { return xfer(c, c ? c->grad : nullptr, nullptr, f, n, c ? c->P : 0); }
@@ -669,7 +770,7 @@ static int eval_rows(vaeb_ctx* c, const float* x, int64_t n, int mode, float* ou
     for (int64_t r0 = 0; r0 < n; r0 += chunk) {
         const int rows = (int)std::min<int64_t>(chunk, n - r0);
         HIP_TRY(hipMemcpyAsync(c->xeval, x + r0 * g.D, sizeof(float) * (size_t)rows * g.D, hipMemcpyHostToDevice, c->s));
-        StepArgs a = make_args(c, rows, mode, c->xeval, false);
+        StepArgs a = make_args(c, c->par, rows, mode, c->xeval, false);
         a.row_base_add = r0;
         a.eps_in = c->eps_in ? c->eps_in + r0 * g.Z : nullptr;
         a.eps_in_ld = c->eps_rows;
@@ -767,7 +868,8 @@ int vaeb_profile_steps(vaeb_ctx* c, int32_t n_steps, float* out_ms, int32_t* out
     if (int rc = upload_order(c, order.data(), n_steps)) return rc;
     std::vector<double> tot(kMaxProfKernels, 0.0);
     for (int it = 0; it < n_steps; ++it) {
-        if (int rc = enqueue_train_step(c, true)) return rc;
+        if (int rc = enqueue_train_step(c, c->par, true)) return rc;
+        if (flips(c)) c->par ^= 1;
         HIP_TRY(hipStreamSynchronize(c->s));
         for (int k = 0; k + 1 < c->prof_n; ++k) {
             float ms = 0.f;
@@ -793,7 +895,8 @@ int vaeb_debug_timeline(vaeb_ctx* c, int32_t batch_index, uint64_t* out, int64_t
     HIP_TRY(hipMemsetAsync(c->dbg, 0, n * sizeof(uint64_t), c->s));
     if (int rc = upload_order(c, &batch_index, 1)) return rc;
     c->dbg_slot = 0;
-    int rc = enqueue_train_step(c, false);
+    int rc = enqueue_train_step(c, c->par, false);
+    if (flips(c)) c->par ^= 1;
     const int launches = c->dbg_slot;
     c->dbg_slot = 0;
     uint64_t* d = c->dbg;
