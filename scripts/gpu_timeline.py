@@ -17,7 +17,10 @@ for i in range(20):
     ctx.update(i % 20)
 for rep in range(3):
     tl = ctx.debug_timeline(rep).astype(np.int64)
-    t0 = tl[tl > 0].min()
+    # s_memtime (shader clock) stamps live in slots 6/7 of tile_body launches; realtime
+    # stamps (100 MHz) everywhere else -- keep t0 on the realtime ones
+    rt = tl[:, :, :6]
+    t0 = rt[rt > 0].min()
     print(f"--- rep {rep} (units: 10 ns ticks from first stamp)")
     for k in range(tl.shape[0]):
         s = tl[k]
@@ -25,15 +28,22 @@ for rep in range(3):
         if not used.any():
             continue
         s = s[used]
+        memtime = (s[:, 6] > 0).any() and np.median(s[:, 6]) < t0 / 2
         cols = []
         for slot in range(8):
             v = s[:, slot]
             v = v[v > 0]
-            if len(v):
+            if len(v) and not (memtime and slot >= 6):
                 cols.append(f"s{slot}[{(v.min()-t0):5d}..{(v.max()-t0):5d}]")
         print(f"launch {k}: wgs={used.sum():4d} " + " ".join(cols))
-        med = [np.median(s[:, j] - s[:, j - 1]) for j in range(1, 6) if (s[:, j] > 0).all() and (s[:, j - 1] > 0).all()]
-        print("          median stage deltas (10ns):", med)
-        if (s[:, 6] > 0).all() and (s[:, 7] > 0).all() and (s[:, 3] > 0).all():
+        rel = []
+        for slot in range(1, 8):
+            if memtime and slot >= 6:
+                continue
+            ok = (s[:, slot] > 0)
+            if ok.sum() > 0:
+                rel.append(f"s{slot}:{np.median(s[ok, slot] - s[ok, 0]):.0f}")
+        print("          median ticks since s0:", " ".join(rel))
+        if memtime and (s[:, 7] > 0).all() and (s[:, 3] > 0).all():
             clk = np.median((s[:, 7] - s[:, 6]) / np.maximum(s[:, 3] - s[:, 0], 1)) * 100
             print(f"          shader clock ~ {clk:.0f} MHz")

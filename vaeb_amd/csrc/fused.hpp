@@ -120,8 +120,8 @@ __global__ __launch_bounds__(512) void heads_dechid_kernel(StepArgs a) {
         }
         mu = valid ? mu + b4n : 0.f;
         lv = valid ? lv + b5n : 0.f;
-        const float sd = expf(0.5f * lv);
-        const float elv = expf(lv);
+        const float sd = fexp(0.5f * lv);
+        const float elv = fexp(lv);
         const uint64_t c23 = (uint64_t)stp ^ ((uint64_t)a.domain << 63);
         for (int l = 0; l < a.L; ++l) {
             float e = 0.f;
@@ -174,7 +174,7 @@ __global__ __launch_bounds__(512) void heads_dechid_kernel(StepArgs a) {
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int mm = i0 + 4 * q + r;
-                a.hd[((int64_t)l * a.Mbp + mm) * H + nn] = (mm < a.Mb) ? tanhf(acc2[r] + b) : 0.f;
+                a.hd[((int64_t)l * a.Mbp + mm) * H + nn] = (mm < a.Mb) ? ftanh(acc2[r] + b) : 0.f;
             }
         }
     };
@@ -308,7 +308,7 @@ DEV void dz_dh_body(const StepArgs& a, int i0) {
     // ---- stage 2: [dMu | dLv] (LA: direct terms of VAEB.py:322-325)
     if (j < Z) {
         const float sl = a.sc / (float)a.L;
-        const float sd = expf(0.5f * lv);
+        const float sd = fexp(0.5f * lv);
         float dmu = 0.f, dlv = 0.f;
         if (valid) {
             if (a.est == EST_LA) {
@@ -324,7 +324,7 @@ DEV void dz_dh_body(const StepArgs& a, int i0) {
                 dlv = dzes * 0.5f * sd + sl * tv;
             } else {
                 dmu = dzsum - a.sc * mu;
-                dlv = dzes * 0.5f * sd + a.sc * 0.5f * (1.f - expf(lv));
+                dlv = dzes * 0.5f * sd + a.sc * 0.5f * (1.f - fexp(lv));
             }
         }
         dml[ml][j] = dmu;

@@ -1,0 +1,297 @@
+// latent.hpp -- the latent block folded into the wide GEMM phases (training step, Z <= 32).
+//
+// The latent-width GEMMs of the step are reductions over H (mu|lv = h [W4|W5]) followed
+// by per-element work on only B x Z values.  As its own launch (P23) that ran on 7
+// workgroups (one per 16 batch rows) for ~12 us.  Here:
+//
+//  enc_latent_kernel  (P1 + heads + sample): every 16x16 tile of h = tanh(X W3 + b3)
+//      also multiplies its h tile by the matching 16 rows of [W4|W5] and publishes that
+//      partial [mu|lv] slab; the LAST tile of each 16-row block to arrive sums the
+//      block's slabs in fixed order (bitwise reproducible) and runs the element-wise
+//      middle: eps, z = mu + exp(lv/2) eps, KL / LA terms (VAEB.py:41-47, 248-249,
+//      322-325, 343).
+//  decout_z_kernel    (dechid + decout): each K-slice wave recomputes its hd chunks
+//      hd = tanh(z W1 + b1) as (W1^T z^T) -- whose MFMA output layout IS the A-operand
+//      layout of the decoder GEMM -- so hd never makes a round trip through memory
+//      before it is used; column tile 0 stores hd for the backward phases (VAEB.py:254).
+//
+// Slab hand-off (MI355X_MICROARCH.md visibility rules): slabs are stored write-through
+// (sc1) with 16-byte stores, the storing wave drains (s_waitcnt vmcnt(0)) before one
+// relaxed agent-scope fetch_add on the row block's counter, and the reducer reads every
+// slab with sc1 loads: no fences, no spinning, correct for any XCD placement.  The
+// reducer resets its counter (zeroed at context creation).
+//
+// Measured alternative (not kept): summing the slabs in the prologue of every
+// decout workgroup instead -- each of the 49 column tiles of a row block then reads the
+// block's 80 KB of slabs, and at ~90 GB/s of L2->CU bandwidth per CU that cost more
+// (15.7 us decoder launch) than the arrival round trip here.
+#pragma once
+#include "fused.hpp"
+
+namespace vaeb {
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(1))) int gint;
+
+DEV void st4_sc1(rsrc_t b, uint32_t off, f32x4 v) {
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), b, off, 0, 16);
+}
+DEV f32x4 ld4_sc1(rsrc_t b, uint32_t off) {
+    return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(b, off, 0, 16));
+}
+
+// Wave 0's slab stores are drained, then one ticket per tile; returns (to every thread)
+// whether this workgroup is the last of its row block.
+DEV bool arrive_last(int* cnt, int target, int* sflag) {
+    if (threadIdx.x < 64) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (threadIdx.x == 0) {
+            const int old = __hip_atomic_fetch_add((gint*)cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            *sflag = (old == target - 1);
+        }
+    }
+    __syncthreads();
+    const bool last = *sflag != 0;
+    if (last && threadIdx.x == 0) __hip_atomic_store((gint*)cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // keep the slab loads below the ticket
+    return last;
+}
+
+// ----------------------------------------------------------------------------- P1'
+// Grid (Mbp/16, ceil(H/16)), 512 threads: 8 waves split K = D.  Tile (bx, by) stores its
+// partial [mu | lv] slab column-major: slab[((bx * nctH + by) * 2Z + c) * 16 + m]
+// (c < Z: mu column c, c >= Z: lv column c - Z).
+template <int NCT, int GCH>
+__global__ __launch_bounds__(512) void enc_latent_kernel(StepArgs a) {
+    __shared__ f32x4 red[512];
+    __shared__ float hs[16][20];
+    __shared__ int sflag;
+    VAEB_STAMP(a, 0);
+    PEnc p{a, nullptr, a.Mbp, a.H, a.D};
+    p.prepare();
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int li = lane & 15, q = lane >> 4;
+    const int bx = blockIdx.x, by = blockIdx.y, nctH = gridDim.y;
+    const int m0 = bx * 16, n0 = by * 16;
+    const int Z = a.Z, H = a.H;
+    const rsrc_t bs = mkbuf(a.slab_ml, (int64_t)gridDim.x * nctH * 2 * Z * 16 * 4);
+
+    PEnc::Pre pre{};
+    f32x4 bw[2 * NCT];
+    if (wave == 0) {
+        pre = p.prefetch(m0, n0);
+        const rsrc_t bw4 = mkbuf(a.W4, (int64_t)H * Z * 4), bw5 = mkbuf(a.W5, (int64_t)H * Z * 4);
+#pragma unroll
+        for (int ct = 0; ct < NCT; ++ct) {
+            bw[2 * ct] = mc4(bw4, Z, ct * 16 + li, n0 + 4 * q, Z, H);
+            bw[2 * ct + 1] = mc4(bw5, Z, ct * 16 + li, n0 + 4 * q, Z, H);
+        }
+    }
+    f32x4 acc[1] = {zero4()};
+    wave_mainloop<1, 8, GCH>(p, m0 + li, n0 + li, p.K, wave, acc);
+    VAEB_STAMP(a, 1);
+    red[wave * 64 + lane] = acc[0];
+    __syncthreads();
+    if (wave == 0) {
+#pragma unroll
+        for (int s = 1; s < 8; ++s) acc[0] += red[s * 64 + lane];
+        if (a.order && bx == 0 && by == 0 && lane == 0) *a.cur_batch = a.order[*a.cursor];
+        const int n = n0 + li;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int m = m0 + 4 * q + r;
+            const float hv = (m < a.Mb && n < H) ? ftanh(acc[0][r] + pre.b) : 0.f;
+            if (n < H) a.h[(int64_t)m * H + n] = hv;
+            hs[4 * q + r][li] = hv;
+        }
+        // partial [mu|lv] of this tile: (16 x 16 h) . (16 rows of [W4|W5])
+        f32x4 av;
+#pragma unroll
+        for (int s = 0; s < 4; ++s) av[s] = hs[li][4 * q + s];
+        const int64_t base = ((int64_t)bx * nctH + by) * 2 * Z;
+#pragma unroll
+        for (int w = 0; w < 2 * NCT; ++w) {
+            const f32x4 sv = mfma4(av, bw[w], zero4());
+            const int nz = (w >> 1) * 16 + li;  // latent column of this lane
+            st4_sc1(bs, nz < Z ? (uint32_t)(((base + (w & 1) * Z + nz) * 16 + 4 * q) * 4) : kOOB, sv);
+        }
+    }
+    VAEB_STAMP(a, 2);
+    if (!arrive_last(a.cnt_ml + bx, nctH, &sflag)) return;
+    VAEB_STAMP(a, 3);
+
+    // ---- reducer (the last tile of row block bx): the element-wise operands ride the
+    // same round trip as the slab loads
+    const int ml = threadIdx.x >> 5, n = threadIdx.x & 31;
+    const int m = m0 + ml;
+    const bool valid = n < Z && m < a.Mb;
+    const float b4n = bld(mkbuf(a.b4, (int64_t)Z * 4), n < Z ? (uint32_t)n * 4u : kOOB);
+    const float b5n = bld(mkbuf(a.b5, (int64_t)Z * 4), n < Z ? (uint32_t)n * 4u : kOOB);
+    float epre[kLP];
+    {
+        const rsrc_t be = mkbuf(a.eps_in, a.eps_mode == 1 ? (int64_t)a.L * a.eps_in_ld * Z * 4 : 0);
+#pragma unroll
+        for (int l = 0; l < kLP; ++l)
+            epre[l] = bld(be, (a.eps_mode == 1 && l < a.L && valid) ? (uint32_t)((l * a.eps_in_ld + m) * Z + n) * 4u : kOOB);
+    }
+    // the row base comes from the order itself: cur_batch is written by tile (0,0) of
+    // this same launch, which need not have run yet
+    const int64_t grow0 = (a.order ? (int64_t)a.order[*a.cursor] * a.row_base_mul : 0) + a.row_base_add;
+    const int64_t stp = a.step ? *a.step : 0;
+    const int NF4 = 8 * Z;                  // float4 per slab (2Z columns x 16 rows)
+    const int NP = 512 / NF4;               // slab partitions (threads >= NP * NF4 idle)
+    {
+        const int f = threadIdx.x % NF4, part = threadIdx.x / NF4;
+        const int64_t first = (int64_t)bx * nctH * NF4;
+        constexpr int SV = 12;
+        f32x4 sum = zero4();
+        for (int c0 = part; c0 < nctH; c0 += SV * NP) {
+            f32x4 v[SV];
+#pragma unroll
+            for (int u = 0; u < SV; ++u) {
+                const int ct = c0 + u * NP;
+                v[u] = ld4_sc1(bs, (part < NP && ct < nctH) ? (uint32_t)((first + (int64_t)ct * NF4 + f) * 16) : kOOB);
+            }
+#pragma unroll
+            for (int u = 0; u < SV; ++u) sum += v[u];
+        }
+        red[threadIdx.x] = sum;
+    }
+    __syncthreads();
+    VAEB_STAMP(a, 4);
+    auto at = [&](int c) {  // element (column c, row ml) of the summed slab
+        const int ff = (c * 16 + ml) >> 2, comp = ml & 3;
+        float v = 0.f;
+        for (int pp = 0; pp < NP; ++pp) v += red[pp * NF4 + ff][comp];
+        return v;
+    };
+    float mu = 0.f, lv = 0.f;
+    if (n < Z) { mu = at(n); lv = at(Z + n); }
+    mu = valid ? mu + b4n : 0.f;
+    lv = valid ? lv + b5n : 0.f;
+    const float sd = fexp(0.5f * lv);
+    const float elv = fexp(lv);
+    const uint64_t c23 = (uint64_t)stp ^ ((uint64_t)a.domain << 63);
+    for (int l = 0; l < a.L; ++l) {
+        float e = 0.f;
+        if (valid) {
+            if (a.eps_mode == 0) e = philox_normal(a.seed, (uint32_t)(grow0 + m), (uint32_t)(l * Z + n), c23);
+            else if (a.eps_mode == 1) e = (l < kLP) ? epre[l] : a.eps_in[((int64_t)l * a.eps_in_ld + m) * Z + n];
+        }
+        const float z = valid ? mu + sd * e : 0.f;
+        if (n < Z) {
+            const int64_t o = ((int64_t)l * a.Mbp + m) * Z + n;
+            a.eps[o] = e;
+            a.z[o] = z;
+        }
+        if (a.est == EST_LA) {
+            const float d = z - mu;
+            float f = valid ? (-0.5f * z * z) - (-0.5f * lv - 0.5f * d * d / elv) : 0.f;
+            f = sum32(f);
+            if (n < a.nctZ) a.la_part[((int64_t)l * a.Mbp + m) * a.nctZ + n] = (n == 0) ? f : 0.f;
+        }
+    }
+    if (n < Z) {
+        a.mu[(int64_t)m * Z + n] = mu;
+        a.lv[(int64_t)m * Z + n] = lv;
+    }
+    if (a.est != EST_LA) {
+        float kl = valid ? 0.5f * (1.f + lv - mu * mu - elv) : 0.f;
+        kl = sum32(kl);
+        if (n < a.nctZ) a.kl_part[(int64_t)m * a.nctZ + n] = (n == 0) ? kl : 0.f;
+    }
+    VAEB_STAMP(a, 5);
+}
+
+// ----------------------------------------------------------------------------- P4'
+// Grid (Me/16, ceil(D/16)), 512 threads.  Wave w owns the 64-wide K blocks
+// kb = 64 (w + 8 g); within a block, sub-chunk u (0..3) of the hd^T product puts hd
+// column kb + 4 i + u on output row i, so one float4 of W1 feeds all four sub-chunks
+// and lane (m, q) ends with hd[m][kb + 16 q + 4 r + u] -- the decoder GEMM's A operand
+// at MFMA step r, matched by W2 row kb + 16 q + 4 r + u on the B side.
+// ZS = ceil(Z / 4): the hd^T product runs ZS MFMA k-steps (latent 4t + q at step t).
+template <int NB, int ZS>
+__global__ __launch_bounds__(512, 4) void decout_z_kernel(StepArgs a) {
+    VAEB_STAMP(a, 0);
+    PDecOut p{a, nullptr, a.Me, a.D, a.H};
+    p.prepare();
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int li = lane & 15, q = lane >> 4;
+    const int m0 = blockIdx.x * 16, n0 = blockIdx.y * 16;
+    const int Z = a.Z, H = a.H;
+    const bool col0 = blockIdx.y == 0;
+    const bool rowok = ((m0 + li) % a.Mbp) < a.Mb;
+    const rsrc_t bw1 = mkbuf(a.W1, (int64_t)Z * H * 4);
+    const rsrc_t bb1 = mkbuf(a.b1, (int64_t)H * 4);
+    const bool v1 = (H & 3) == 0 && aligned16(a.W1) && aligned16(a.b1);
+    float zb[ZS];
+    {
+        const rsrc_t bz = mkbuf(a.z, (int64_t)a.Me * Z * 4);
+#pragma unroll
+        for (int t = 0; t < ZS; ++t) zb[t] = bld(bz, (4 * t + q < Z) ? (uint32_t)((m0 + li) * Z + 4 * t + q) * 4u : kOOB);
+    }
+    PDecOut::Pre pre{};
+    if (wave == 0) pre = p.prefetch(m0, n0);
+    f32x4 acc[NB];
+#pragma unroll
+    for (int w = 0; w < NB; ++w) acc[w] = zero4();
+    for (int kb = 64 * wave; kb < H; kb += 64 * 8) {
+        // W1^T rows kb + 4 li + (0..3) at latent 4t + q; b1 at kb + 16 q + 4 r + (0..3)
+        f32x4 w1v[ZS], b1v[4];
+        float w2b[4][4][NB];
+#pragma unroll
+        for (int t = 0; t < ZS; ++t) {
+            const int c = 4 * t + q, k = kb + 4 * li;
+            w1v[t] = kc4(bw1, H, c, k, Z, H, v1);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) b1v[r] = kc4(bb1, 0, 0, kb + 16 * q + 4 * r, 1, H, v1);
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+#pragma unroll
+                for (int w = 0; w < NB; ++w) {
+                    const int k = kb + 16 * q + 4 * r + u;
+                    w2b[u][r][w] = p.b1(n0 + li, k, w);
+                }
+        f32x4 hv[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            f32x4 t = zero4();
+#pragma unroll
+            for (int st = 0; st < ZS; ++st) t = __builtin_amdgcn_mfma_f32_16x16x4f32(w1v[st][u], zb[st], t, 0, 0, 0);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) hv[u][r] = rowok ? ftanh(t[r] + b1v[r][u]) : 0.f;
+        }
+        if (col0) {  // hd[m][kb + 16q + 4r + u] for u = 0..3: one float4 per r
+            float* dst = a.hd + (int64_t)(m0 + li) * H;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int k = kb + 16 * q + 4 * r;
+                const f32x4 o = {hv[0][r], hv[1][r], hv[2][r], hv[3][r]};
+                if (v1) {
+                    if (k < H) *reinterpret_cast<f32x4*>(dst + k) = o;
+                } else {
+#pragma unroll
+                    for (int u = 0; u < 4; ++u)
+                        if (k + u < H) dst[k + u] = o[u];
+                }
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+#pragma unroll
+                for (int w = 0; w < NB; ++w)
+                    acc[w] = __builtin_amdgcn_mfma_f32_16x16x4f32(hv[u][r], w2b[u][r][w], acc[w], 0, 0, 0);
+    }
+    VAEB_STAMP(a, 1);
+    if (!ks_reduce<8, 8, NB>(acc, wave, wave)) return;
+    VAEB_STAMP(a, 2);
+    p.epilogue(m0, n0, acc, pre);
+    VAEB_STAMP(a, 3);
+}
+
+}  // namespace vaeb

@@ -54,6 +54,9 @@ struct StepArgs {
     // ELBO partials: [rows][col tiles]
     float *kl_part, *la_part, *lp_part;
     int nctZ, nctD;
+    // latent slabs + per-row-block arrival counters of the folded latent phases (latent.hpp)
+    float *slab_ml, *slab_dz;
+    int *cnt_ml, *cnt_dz;
     uint64_t* dbg;         // diagnostics: per-workgroup s_memrealtime stamps (null = off)
 };
 
@@ -103,7 +106,7 @@ struct PEnc {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const int m = m0 + 4 * (lane >> 4) + r;
-            a.h[(int64_t)m * a.H + n] = (m < a.Mb) ? tanhf(acc[0][r] + b) : 0.f;
+            a.h[(int64_t)m * a.H + n] = (m < a.Mb) ? ftanh(acc[0][r] + b) : 0.f;
         }
     }
 };
@@ -142,8 +145,8 @@ struct PHeads {
                 a.mu[(int64_t)m * a.Z + n] = mu;
                 a.lv[(int64_t)m * a.Z + n] = lv;
             }
-            const float sd = expf(0.5f * lv);
-            float kl = valid ? 0.5f * (1.f + lv - mu * mu - expf(lv)) : 0.f;
+            const float sd = fexp(0.5f * lv);
+            float kl = valid ? 0.5f * (1.f + lv - mu * mu - fexp(lv)) : 0.f;
             for (int l = 0; l < a.L; ++l) {
                 float e = 0.f;
                 if (valid) {
@@ -161,7 +164,7 @@ struct PHeads {
                 if (a.est == EST_LA) {
                     // (-1/2 log2pi - z^2/2) - (-1/2 log2pi - lv/2 - (z-mu)^2/(2 exp lv))
                     const float d = z - mu;
-                    float f = valid ? (-0.5f * z * z) - (-0.5f * lv - 0.5f * d * d / expf(lv)) : 0.f;
+                    float f = valid ? (-0.5f * z * z) - (-0.5f * lv - 0.5f * d * d / fexp(lv)) : 0.f;
                     f = sum16(f);
                     if ((lane & 15) == 0) a.la_part[((int64_t)l * a.Mbp + m) * a.nctZ + ct] = f;
                 }
@@ -197,7 +200,7 @@ struct PDecHid {
         for (int r = 0; r < 4; ++r) {
             const int m = m0 + 4 * (lane >> 4) + r;
             const bool valid = (m % a.Mbp) < a.Mb;
-            a.hd[(int64_t)m * a.H + n] = valid ? tanhf(acc[0][r] + b) : 0.f;
+            a.hd[(int64_t)m * a.H + n] = valid ? ftanh(acc[0][r] + b) : 0.f;
         }
     }
 };
@@ -208,14 +211,18 @@ struct PDecOut {
     const float* x;
     int M, N, K;
     rsrc_t bhd, bw2, bw6;
-    DEV void prepare() {
-        x = x_rows(a);
+    DEV void prepare() { prepare_at(x_rows(a)); }
+    DEV void prepare_at(const float* xr) {
+        x = xr;
         bhd = mkbuf(a.hd, (int64_t)a.Me * a.H * 4);
         bw2 = mkbuf(a.W2, (int64_t)a.H * a.D * 4);
         bw6 = mkbuf(a.W6 ? a.W6 : a.W2, (int64_t)a.H * a.D * 4);
     }
     DEV f32x4 a4(int m, int k) const { return kc4(bhd, a.H, m, k, a.Me, a.H, (a.H & 3) == 0); }
     DEV f32x4 b4(int n, int k, int w) const { return mc4(w ? bw6 : bw2, a.D, n, k, a.D, a.H); }
+    DEV float b1(int n, int k, int w) const {  // one element W(k, n)
+        return bld(w ? bw6 : bw2, (n < a.D && k < a.H) ? (uint32_t)(k * a.D + n) * 4u : kOOB);
+    }
     struct Pre { float b2, b6; f32x4 xv; };
     DEV Pre prefetch(int m0, int n0) const {
         const int lane = threadIdx.x & 63;
@@ -254,7 +261,7 @@ struct PDecOut {
                 if (a.dec == DEC_GAUSSIAN) {
                     const float a6 = acc[NB - 1][r] + b6;
                     const float rr = xv - yv;
-                    const float e = expf(-a6);
+                    const float e = fexp(-a6);
                     lp = -kHalfLog2Pi - 0.5f * a6 - 0.5f * rr * rr * e;
                     d2 = rr * e * yv * (1.f - yv) * sl;
                     d6 = (-0.5f + 0.5f * rr * rr * e) * sl;
@@ -373,7 +380,7 @@ struct PDh {
         const int j = isv ? k - Z : k;
         const int64_t o = (int64_t)i * Z + j;
         const float mu = a.mu[o], lv = a.lv[o];
-        const float sd = expf(0.5f * lv);
+        const float sd = fexp(0.5f * lv);
         const float sl = a.sc / (float)a.L;
         float g = 0.f, t = 0.f;
         for (int l = 0; l < a.L; ++l) {
@@ -389,7 +396,7 @@ struct PDh {
             }
         }
         if (a.est == EST_LA) return g + sl * t;
-        return isv ? g + a.sc * 0.5f * (1.f - expf(lv)) : g - a.sc * mu;
+        return isv ? g + a.sc * 0.5f * (1.f - fexp(lv)) : g - a.sc * mu;
     }
     DEV f32x4 a4(int m, int k) const {
         f32x4 v = zero4();

@@ -35,6 +35,18 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
                 __builtin_amdgcn_s_memrealtime();                                         \
     } while (0)
 
+// Diagnostics variant that first drains this wave's outstanding vector-memory operations,
+// so the stamp marks when its loads have actually landed (debug launches only).
+#define VAEB_STAMP_SYNC(A, slot)                                                          \
+    do {                                                                                  \
+        if ((A).dbg) {                                                                    \
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");                              \
+            if (threadIdx.x == 0)                                                         \
+                (A).dbg[(blockIdx.x + (uint64_t)blockIdx.y * gridDim.x) * 8 + (slot)] =   \
+                    __builtin_amdgcn_s_memrealtime();                                     \
+        }                                                                                 \
+    } while (0)
+
 namespace vaeb {
 
 DEV f32x4 zero4() { f32x4 z = {0.f, 0.f, 0.f, 0.f}; return z; }
@@ -210,16 +222,36 @@ DEV void philox4x32(uint32_t (&ctr)[4], uint32_t k0, uint32_t k1) {
     }
 }
 
-// One standard normal for the 128-bit counter (Box-Muller on the first two words).
+// ------------------------------------------------------------ fast transcendentals
+// Every phase here is latency-bound with 8-16 waves per CU, so the libm (ocml) forms --
+// range reduction, special-case branches, IEEE division -- made the element-wise stages
+// VALU-bound (the latent middle took 3 us).  These use the hardware approximations
+// (v_exp_f32 / v_log_f32 / v_rcp_f32 / v_sqrt_f32 / v_cos_f32, ~1 ulp each); the
+// resulting differences (~1e-6 relative) sit far inside the parity tolerance (1e-4).
+constexpr float kLog2e = 1.4426950408889634f;
+constexpr float kLn2 = 0.6931471805599453f;
+DEV float fexp(float x) { return __builtin_amdgcn_exp2f(x * kLog2e); }
+DEV float flog(float x) { return __builtin_amdgcn_logf(x) * kLn2; }
+DEV float frcp(float x) { return __builtin_amdgcn_rcpf(x); }
+// tanh: odd; 1 - 2 / (e^{2|x|} + 1) away from 0, Taylor below 1/16 (no cancellation)
+DEV float ftanh(float x) {
+    const float ax = fabsf(x);
+    const float x2 = ax * ax;
+    const float small = ax * (1.f + x2 * (-1.f / 3.f + x2 * (2.f / 15.f)));
+    const float big = 1.f - 2.f * frcp(fexp(2.f * ax) + 1.f);
+    return copysignf(ax < 0.0625f ? small : big, x);
+}
+DEV float softplusf(float a) { return fmaxf(a, 0.f) + flog(1.f + fexp(-fabsf(a))); }
+DEV float sigmoidf(float a) { return frcp(1.f + fexp(-a)); }
+
+// One standard normal for the 128-bit counter (Box-Muller on the first two words;
+// v_cos_f32 takes its argument in revolutions).
 DEV float philox_normal(uint64_t seed, uint32_t c0, uint32_t c1, uint64_t c23) {
     uint32_t ctr[4] = {c0, c1, (uint32_t)c23, (uint32_t)(c23 >> 32)};
     philox4x32(ctr, (uint32_t)seed, (uint32_t)(seed >> 32));
     const float u1 = ((float)(ctr[0] >> 8) + 1.0f) * (1.0f / 16777216.0f);   // (0, 1]
     const float u2 = (float)(ctr[1] >> 8) * (1.0f / 16777216.0f);            // [0, 1)
-    return sqrtf(-2.0f * logf(u1)) * cospif(2.0f * u2);
+    return __builtin_amdgcn_sqrtf(-2.0f * flog(u1)) * __builtin_amdgcn_cosf(u2);
 }
-
-DEV float softplusf(float a) { return fmaxf(a, 0.f) + log1pf(expf(-fabsf(a))); }
-DEV float sigmoidf(float a) { return 1.0f / (1.0f + expf(-a)); }
 
 }  // namespace vaeb

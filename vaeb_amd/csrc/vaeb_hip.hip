@@ -18,6 +18,7 @@
 
 #include "../../include/vaeb_hip.h"
 #include "hfuse.hpp"
+#include "latent.hpp"
 
 using namespace vaeb;
 
@@ -63,7 +64,8 @@ constexpr int kDbgWG = 1024;      // diagnostics: stamp slots per launch (workgr
 
 const char* kKernelNames[] = {"p1_enc", "p2_heads", "p3_dechid", "p4_decout", "p5_dhd_w2", "p6_dz",
                               "p7_dh", "p8_wgrad_w3w45", "allreduce", "adagrad", "fv_update", "elbo",
-                              "p23_heads_dechid", "p67_dz_dh_w1", "p8_wgrad_w2", "p8_wgrad_w1"};
+                              "p23_heads_dechid", "p67_dz_dh_w1", "p8_wgrad_w2", "p8_wgrad_w1",
+                              "p1_enc_latent", "p4_decout_z"};
 
 }  // namespace
 
@@ -98,6 +100,8 @@ struct vaeb_ctx {
     float *h = nullptr, *mu = nullptr, *lv = nullptr, *eps = nullptr, *z = nullptr, *hd = nullptr,
           *y = nullptr, *dA2 = nullptr, *dA6 = nullptr, *dA1 = nullptr, *dZ = nullptr,
           *dMuLv = nullptr, *dA3 = nullptr, *kl_part = nullptr, *lp_part = nullptr;
+    float *slab_ml = nullptr, *slab_dz = nullptr;  // folded-latent partial slabs (latent.hpp)
+    int *cnt_ml = nullptr, *cnt_dz = nullptr;      // their per-row-block arrival counters
     // host staging (pinned)
     int* h_ctl = nullptr;
     float* h_elbo = nullptr;
@@ -165,6 +169,7 @@ StepArgs make_args(vaeb_ctx* c, int par, int Mb, int mode, const float* xbase, b
     a.kl_part = c->kl_part; a.la_part = c->kl_part; a.lp_part = c->lp_part;
     a.nctZ = cdiv(g.Z, 16);
     a.nctD = cdiv(g.D, 16);
+    a.slab_ml = c->slab_ml; a.slab_dz = c->slab_dz; a.cnt_ml = c->cnt_ml; a.cnt_dz = c->cnt_dz;
     return a;
 }
 
@@ -207,11 +212,48 @@ ElboArgs base_elbo(vaeb_ctx* c, const StepArgs& a) {
     return e;
 }
 
+template <int NB>
+void launch_decout_z(hipStream_t s, dim3 grid, const StepArgs& a) {
+    switch ((a.Z + 3) / 4) {
+        case 1: hipLaunchKernelGGL((decout_z_kernel<NB, 1>), grid, dim3(512), 0, s, a); break;
+        case 2: hipLaunchKernelGGL((decout_z_kernel<NB, 2>), grid, dim3(512), 0, s, a); break;
+        case 3: case 4: hipLaunchKernelGGL((decout_z_kernel<NB, 4>), grid, dim3(512), 0, s, a); break;
+        case 5: hipLaunchKernelGGL((decout_z_kernel<NB, 5>), grid, dim3(512), 0, s, a); break;
+        default: hipLaunchKernelGGL((decout_z_kernel<NB, 8>), grid, dim3(512), 0, s, a); break;
+    }
+}
+
+// Training minibatches with Z <= 32 fold the latent block into the wide phases
+// (latent.hpp); validation / reconstruction chunks keep the per-row-block kernels.
+bool folded_latent(const vaeb_ctx* c, const StepArgs& a) {
+    return fused_latent(c) && a.order != nullptr && a.Mbp <= r16(c->c.B);
+}
+
 // Forward phases P1..P4 for any mode.
 int enqueue_forward(vaeb_ctx* c, const StepArgs& a0, Prof& pr) {
     hipStream_t s = c->s;
     StepArgs a = a0;
     a.dbg = next_dbg(c);
+    if (folded_latent(c, a)) {
+        const dim3 g1(a.Mbp / 16, cdiv(a.H, 16));
+        const bool deep = cdiv(cdiv(a.D, 16), 8) > 4;
+        pr.mark(16);
+        if (a.Z <= 16) {
+            if (deep) hipLaunchKernelGGL((enc_latent_kernel<1, 8>), g1, dim3(512), 0, s, a);
+            else hipLaunchKernelGGL((enc_latent_kernel<1, 4>), g1, dim3(512), 0, s, a);
+        } else {
+            if (deep) hipLaunchKernelGGL((enc_latent_kernel<2, 8>), g1, dim3(512), 0, s, a);
+            else hipLaunchKernelGGL((enc_latent_kernel<2, 4>), g1, dim3(512), 0, s, a);
+        }
+        CHECK_LAUNCH();
+        a.dbg = next_dbg(c);
+        const dim3 g4(a.Me / 16, cdiv(a.D, 16));
+        pr.mark(17);
+        if (gaussian(c)) launch_decout_z<2>(s, g4, a);
+        else launch_decout_z<1>(s, g4, a);
+        CHECK_LAUNCH();
+        return 0;
+    }
     pr.mark(0);
     launch_bigk<1>(s, PEnc{a, nullptr, a.Mbp, a.H, a.D});
     CHECK_LAUNCH();
@@ -583,6 +625,13 @@ int vaeb_create(const vaeb_config* cfg, vaeb_ctx** out) {
     rc = rc ? rc : dalloc(&c->dA3, (size_t)R * H);
     rc = rc ? rc : dalloc(&c->kl_part, (size_t)RL * cdiv(Z, 16));
     rc = rc ? rc : dalloc(&c->lp_part, (size_t)RL * cdiv(D, 16));
+    {   // folded-latent slabs and arrival counters (training minibatch only)
+        const int64_t Bp = r16(g.B), nctH = cdiv(H, 16);
+        rc = rc ? rc : dalloc(&c->slab_ml, (size_t)(Bp * nctH * 64));
+        rc = rc ? rc : dalloc(&c->slab_dz, (size_t)(g.L * Bp * nctH * 32));
+        rc = rc ? rc : dalloc(&c->cnt_ml, (size_t)(Bp / 16));
+        rc = rc ? rc : dalloc(&c->cnt_dz, (size_t)(Bp / 16));
+    }
     if (rc) { vaeb_destroy(c); return rc; }
     if (hipHostMalloc((void**)&c->h_ctl, sizeof(int) * (kOrderCap + 2), 0) != hipSuccess ||
         hipHostMalloc((void**)&c->h_elbo, sizeof(float) * 4, 0) != hipSuccess ||
@@ -605,8 +654,10 @@ int vaeb_destroy(vaeb_ctx* c) {
     if (c->comm) ncclCommDestroy(c->comm);
     float* fp[] = {c->theta2[0], c->theta2[1], c->acc, c->grad, c->fvmu, c->fvsg, c->fvam, c->fvas, c->fv_part, c->data, c->xeval,
                    c->elbo_out, c->eps_in, c->h, c->mu, c->lv, c->eps, c->z, c->hd, c->y, c->dA2, c->dA6, c->dA1,
-                   c->dZ, c->dMuLv, c->dA3, c->kl_part, c->lp_part};
+                   c->dZ, c->dMuLv, c->dA3, c->kl_part, c->lp_part, c->slab_ml, c->slab_dz};
     for (float* p : fp) if (p) hipFree(p);
+    if (c->cnt_ml) hipFree(c->cnt_ml);
+    if (c->cnt_dz) hipFree(c->cnt_dz);
     if (c->ictl) hipFree(c->ictl);
     if (c->step) hipFree(c->step);
     if (c->epoch) hipFree(c->epoch);
