@@ -46,26 +46,31 @@ def phase_flops(D, H, Z, B, L=1, gaussian=False):
         # horizontally fused launches (hfuse.hpp): phase + weight-gradient tiles in one grid
         "p5_dhd_w2": 2 * L * B * D * H * g + 2 * L * B * H * D * g,
         "p67_dz_dh_w1": 2 * L * B * H * Z + 2 * B * 2 * Z * H + 2 * L * B * Z * H,
+        # folded latent block (latent.hpp): encoder GEMM + heads; hd recompute + decoder GEMM
+        "p1_enc_latent": 2 * B * D * H + 2 * B * H * 2 * Z,
+        "p4_decout_z": 2 * L * B * Z * H + 2 * L * B * H * D * g,
     }
 
 
 KERNEL_SYMBOLS = {"p1_enc": "PEnc", "p23_heads_dechid": "heads_dechid_kernel", "p4_decout": "PDecOut",
                   "p5_dhd_w2": "vaeb::tile_wgrad_kernel", "p67_dz_dh_w1": "vaeb::dz_dh_wgrad_kernel",
-                  "p8_wgrad_w3w45": "vaeb::wgrad_kernel"}
+                  "p8_wgrad_w3w45": "vaeb::wgrad_kernel", "p1_enc_latent": "vaeb::enc_latent_kernel",
+                  "p4_decout_z": "vaeb::decout_z_kernel"}
+PMC_FILE = os.path.join(ROOT, "profiles", "r1", "pmc_per_launch.json")
 
 
-def committed_traffic(kernel):
-    """HBM bytes per launch (FETCH_SIZE + WRITE_SIZE, KB units) of `kernel` from the
-    rocprofv3 PMC passes committed under profiles/ (separate --pmc passes)."""
-    path = os.path.join(ROOT, "profiles", "r1", "pmc_per_launch.json")
+def committed_traffic(kernel, path=PMC_FILE, symbols=KERNEL_SYMBOLS):
+    """HBM bytes per launch of `kernel` from the rocprofv3 PMC passes committed under
+    profiles/ (separate FETCH_SIZE / WRITE_SIZE passes folded by scripts/pmc_summary.py,
+    FETCH_SIZE doubled per MI355X_MICROARCH.md §HBM)."""
     try:
         data = json.load(open(path))
     except Exception:
         return None
-    sym = KERNEL_SYMBOLS.get(kernel)
+    sym = symbols.get(kernel)
     for name, v in data.items():
-        if sym and sym in name and "FETCH_SIZE" in v and "WRITE_SIZE" in v:
-            return (v["FETCH_SIZE"] + v["WRITE_SIZE"]) * 1024.0
+        if sym and sym in name and "hbm_bytes_per_launch" in v:
+            return v["hbm_bytes_per_launch"]
     return None
 
 

@@ -63,6 +63,14 @@ DEV void elbo_reduce(const ElboArgs& e, double* sh) {
     if (e.step) *e.step += 1;
 }
 
+// Measurement helper: holds the stream for ~`ticks` x 10 ns (s_memrealtime runs at
+// 100 MHz) so that the host can enqueue a whole eager step behind it; the events
+// between the step's launches then time back-to-back kernels, as in a graph replay.
+__global__ __launch_bounds__(64) void delay_kernel(uint64_t ticks) {
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(8);
+}
+
 __global__ __launch_bounds__(256) void elbo_kernel(ElboArgs e) {
     __shared__ double sh[256];
     elbo_reduce(e, sh);
