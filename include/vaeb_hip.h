@@ -30,6 +30,9 @@ enum vaeb_estimator { VAEB_EST_LB = 0, VAEB_EST_LA = 1, VAEB_EST_FV = 2 };/* VAE
 enum vaeb_objective { VAEB_OBJ_SUM_PRIOR = 0,                             /* VAEB.py:386-390 */
                       VAEB_OBJ_MEAN_MAP = 1 };                            /* VAEBfullbayes.py:142,183 */
 enum vaeb_eps_mode  { VAEB_EPS_PHILOX = 0, VAEB_EPS_HOST = 1 };
+enum vaeb_dtype     { VAEB_DTYPE_F32 = 0,      /* fp32 MFMA, the reference's floatX (run_on_gpu.sh:2) */
+                      VAEB_DTYPE_BF16 = 1 };   /* bf16 MFMA operands, fp32 accumulation and fp32
+                                                  master weights / Adagrad state (BASELINE config 5) */
 enum vaeb_status    { VAEB_OK = 0, VAEB_ERR_ARG = -1, VAEB_ERR_HIP = -2, VAEB_ERR_STATE = -3,
                       VAEB_ERR_COMM = -4, VAEB_ERR_NOMEM = -5 };
 
@@ -50,7 +53,8 @@ typedef struct vaeb_config {
     int32_t max_eval_rows;/* largest x passed to vaeb_validate in one device chunk       */
     int32_t use_graph;    /* 1: replay the step as a captured hipGraph                   */
     int32_t keep_grads;   /* 1: also store each step's data gradient (vaeb_get_grads)    */
-    int32_t reserved[6];
+    int32_t dtype;        /* enum vaeb_dtype; BF16 needs D, H, Z % 8 == 0 (Gaussian: D % 32)  */
+    int32_t reserved[5];
 } vaeb_config;
 
 typedef struct vaeb_ctx vaeb_ctx;
@@ -124,6 +128,13 @@ int vaeb_kernel_name(int32_t kernel_id, char* out, int32_t cap);
  * stage boundaries of every launch; out = [launch][1024 workgroups][8 slots]. */
 int vaeb_debug_timeline(vaeb_ctx* ctx, int32_t batch_index, uint64_t* out, int64_t cap,
                         int32_t* out_launches);
+
+/* Test hook for the bf16 GEMM engine: C[M x N] = sum_k A(m, k) B(k, n) with the operands
+ * rounded to bf16 on device.  a_kouter = 0: A is stored [M x K], 1: [K x M]; b_kouter = 0:
+ * B is stored [N x K], 1: [K x N].  ksplit K slices are summed in fixed order.  Uses the
+ * context's device and stream. */
+int vaeb_test_gemm_bf16(vaeb_ctx* ctx, int32_t a_kouter, int32_t b_kouter, int32_t M, int32_t N, int32_t K,
+                        const float* A, const float* B, float* C, int32_t ksplit);
 
 #ifdef __cplusplus
 }

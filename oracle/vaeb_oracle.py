@@ -110,7 +110,16 @@ def _unpack(params, cfg):
     return d
 
 
-def forward_backward(params, x, eps, cfg: Config, need_grad=True):
+def bf16_round(a):
+    """Round to the nearest bfloat16 (ties to even), returned in a's dtype: the storage
+    rounding of the bf16 engine (vaeb_amd/csrc/gemm_bf16.hpp f2bf)."""
+    a = np.asarray(a)
+    u = a.astype(np.float32).view(np.uint32).astype(np.uint64)
+    u = ((u + 0x7FFF + ((u >> 16) & 1)) >> 16) << 16
+    return u.astype(np.uint32).view(np.float32).astype(a.dtype)
+
+
+def forward_backward(params, x, eps, cfg: Config, need_grad=True, q=None):
     """One SGVB evaluation and its reverse-mode gradient, restating:
       encoder VAEB.py:245-251, reparam_trick :41-47, decoder :253-265,
       posterior_log_prob :302-313, getLB :332-346 / getLA :315-330,
@@ -122,7 +131,13 @@ def forward_backward(params, x, eps, cfg: Config, need_grad=True):
     x: [B, D];  eps: [L, B, Z] standard normals.
     Returns dict with 'sgvb' (sum over batch, the reference's SGVB), intermediates and
     'grads' = dJ/dtheta in reference order (ascent direction, prior included).
+
+    q: optional storage quantizer (bf16_round) applied exactly where the bf16 engine
+    rounds: every GEMM operand (x, weights, h, z, hd, dA2/dA6, dA1, dMu/dLv, dA3), while
+    bias gradients, log-likelihood, KL and the latent block stay in full precision.
+    q=None is the plain restatement.
     """
+    Q = q if q is not None else (lambda v: v)
     p = _unpack(params, cfg)
     dt = p["W3"].dtype
     x = np.asarray(x, dt)
@@ -133,21 +148,22 @@ def forward_backward(params, x, eps, cfg: Config, need_grad=True):
     s = dt.type(1.0 / B) if cfg.objective == "mean_map" else dt.type(1.0)
     half = dt.type(0.5)
 
-    a3 = x @ p["W3"] + p["b3"]
-    h = np.tanh(a3)
-    mu = h @ p["W4"] + p["b4"]
-    lv = h @ p["W5"] + p["b5"]
+    xq = Q(x)
+    a3 = xq @ Q(p["W3"]) + p["b3"]
+    h = Q(np.tanh(a3))
+    mu = h @ Q(p["W4"]) + p["b4"]
+    lv = h @ Q(p["W5"]) + p["b5"]
     std = np.exp(half * lv)
     z = mu[None] + std[None] * eps                    # [L, B, Z]
-    zf = z.reshape(L * B, Z)
-    a1 = zf @ p["W1"] + p["b1"]
-    hd = np.tanh(a1)
-    a2 = hd @ p["W2"] + p["b2"]
-    xr = np.tile(x, (L, 1))
+    zf = Q(z.reshape(L * B, Z))
+    a1 = zf @ Q(p["W1"]) + p["b1"]
+    hd = Q(np.tanh(a1))
+    a2 = hd @ Q(p["W2"]) + p["b2"]
+    xr = np.tile(xq, (L, 1))     # the bf16 engine stores the dataset itself in bf16
     y = sigmoid(a2)
     out = dict(a3=a3, h=h, mu=mu, lv=lv, z=z, hd=hd, a2=a2, y=y)
     if cfg.continuous:
-        a6 = hd @ p["W6"] + p["b6"]
+        a6 = hd @ Q(p["W6"]) + p["b6"]
         r = xr - y
         # VAEB.py:306-307
         logp_rows = (dt.type(-0.5 * LOG2PI) - half * a6 - half * r * r / np.exp(a6)).sum(1)
@@ -180,30 +196,30 @@ def forward_backward(params, x, eps, cfg: Config, need_grad=True):
     else:
         dA2 = (xr - y) * sl
     g = {}
-    g["W2"] = hd.T @ dA2
+    g["W2"] = hd.T @ Q(dA2)
     g["b2"] = dA2.sum(0)
-    dHd = dA2 @ p["W2"].T
+    dHd = Q(dA2) @ Q(p["W2"]).T
     if cfg.continuous:
-        g["W6"] = hd.T @ dA6
+        g["W6"] = hd.T @ Q(dA6)
         g["b6"] = dA6.sum(0)
-        dHd = dHd + dA6 @ p["W6"].T
+        dHd = dHd + Q(dA6) @ Q(p["W6"]).T
     dA1 = dHd * (1 - hd * hd)
-    g["W1"] = zf.T @ dA1
+    g["W1"] = zf.T @ Q(dA1)
     g["b1"] = dA1.sum(0)
-    dZ = (dA1 @ p["W1"].T).reshape(L, B, Z)
+    dZ = (Q(dA1) @ Q(p["W1"]).T).reshape(L, B, Z)
     if cfg.estimator == "LA":
         dMu = dZ.sum(0) + sl * (-z).sum(0)
         dLv = (dZ * half * std[None] * eps).sum(0) + sl * (half - half * z * std[None] * eps).sum(0)
     else:
         dMu = dZ.sum(0) - s * mu
         dLv = (dZ * half * std[None] * eps).sum(0) + s * half * (1 - np.exp(lv))
-    g["W4"] = h.T @ dMu
+    g["W4"] = h.T @ Q(dMu)
     g["b4"] = dMu.sum(0)
-    g["W5"] = h.T @ dLv
+    g["W5"] = h.T @ Q(dLv)
     g["b5"] = dLv.sum(0)
-    dH = dMu @ p["W4"].T + dLv @ p["W5"].T
+    dH = Q(dMu) @ Q(p["W4"]).T + Q(dLv) @ Q(p["W5"]).T
     dA3 = dH * (1 - h * h)
-    g["W3"] = x.T @ dA3
+    g["W3"] = xq.T @ Q(dA3)
     g["b3"] = dA3.sum(0)
     out.update(dA2=dA2, dA1=dA1, dZ=dZ, dMu=dMu, dLv=dLv, dA3=dA3)
     if cfg.continuous:
@@ -231,18 +247,18 @@ def adagrad_update(params, acc, grads, cfg: Config):
     return new_p, new_a
 
 
-def step(params, acc, x, eps, cfg: Config):
+def step(params, acc, x, eps, cfg: Config, q=None):
     """VAEB.update(index) (VAEB.py:408-415): returns (SGVB/B, theta', acc', aux)."""
-    out = forward_backward(params, x, eps, cfg)
+    out = forward_backward(params, x, eps, cfg, q=q)
     B = x.shape[0]
     new_p, new_a = adagrad_update(params, acc, out["grads"], cfg)
     return out["sgvb"] / B, new_p, new_a, out
 
 
-def validate(params, x, eps, cfg: Config):
+def validate(params, x, eps, cfg: Config, q=None):
     """VAEB.validate (VAEB.py:418-422): forward-only SGVB *sum* over all rows of x.
     (The mean_map variant returns the mean, VAEBfullbayes.py:161-165.)"""
-    out = forward_backward(params, x, eps, cfg, need_grad=False)
+    out = forward_backward(params, x, eps, cfg, need_grad=False, q=q)
     if cfg.objective == "mean_map":
         return out["sgvb"] / x.shape[0]
     return out["sgvb"]

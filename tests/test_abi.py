@@ -15,7 +15,7 @@ LIB = os.path.join(ROOT, "vaeb_amd", "libvaeb_hip.so")
 def header_functions():
     src = open(HEADER).read()
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
-    return sorted(set(re.findall(r"\b(vaeb_[a-z_]+)\s*\(", src)))
+    return sorted(set(re.findall(r"\b(vaeb_[a-z0-9_]+)\s*\(", src)))
 
 
 @pytest.fixture(scope="module")
@@ -66,5 +66,6 @@ def test_error_reporting_without_gpu(lib):
 
 def test_config_struct_layout_matches_header():
     from vaeb_amd import _lib
-    # 16 int32/float fields + 6 reserved = 22 * 4 bytes
+    # 17 int32/float fields (dtype included) + 5 reserved = 22 * 4 bytes
     assert ctypes.sizeof(_lib.VaebConfig) == 22 * 4
+    assert _lib.VaebConfig.dtype.offset == 16 * 4

@@ -1,0 +1,176 @@
+"""Parity of the bf16 large-batch engine (dtype=VAEB_DTYPE_BF16, vaeb_amd/csrc/gemm_bf16.hpp,
+step_bf16.hpp; BASELINE config 5) against the CPU oracle, through the C ABI.
+
+Two references:
+  * the oracle with `q=bf16_round` -- the same algorithm with bf16 storage rounding at
+    exactly the engine's rounding points, evaluated in float64.  Tolerances (fp32
+    accumulation order and the ~1-ulp hardware transcendentals remain; a value within
+    ~1e-7 of a bf16 rounding tie can round the other way):
+      ELBO relative <= 1e-4, data gradients norm-wise relative <= 2e-3 per tensor,
+      Adagrad accumulator relative <= 4e-3;
+  * the plain float64 oracle (no rounding) -- bounds the bf16 error itself:
+      ELBO relative <= 1e-2, gradients norm-wise relative <= 8e-2.
+The GEMM engine alone is checked against float64 products of bf16-rounded operands at
+|C - ref| <= 1e-5 * (|A| |B|) elementwise, for all four operand layouts, tails and
+split-K.
+"""
+import numpy as np
+import pytest
+
+from oracle import vaeb_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+EST = {"LB": 0, "LA": 1}
+OBJ = {"sum_prior": 0, "mean_map": 1}
+
+
+def rel(a, b):
+    return float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30))
+
+
+@pytest.fixture(scope="module")
+def gctx():
+    from vaeb_amd import _lib
+    c = _lib.Context(64, 32, 8, 16, dtype=_lib.DTYPE_BF16)
+    yield c
+    c.close()
+
+
+GEMM_SHAPES = [(256, 128, 512, 1), (200, 136, 328, 1), (200, 136, 328, 3), (64, 40, 72, 2), (8, 520, 4096, 4)]
+
+
+@pytest.mark.parametrize("ako,bko", [(0, 0), (0, 1), (1, 0), (1, 1)])
+@pytest.mark.parametrize("M,N,K,ks", GEMM_SHAPES)
+def test_gemm_layouts(gctx, ako, bko, M, N, K, ks):
+    rng = np.random.default_rng(M + 7 * N + K + ks + 10 * ako + 20 * bko)
+    A = rng.standard_normal((M, K)).astype(np.float32)   # logical [M, K]
+    B = rng.standard_normal((K, N)).astype(np.float32)   # logical [K, N]
+    As = A.T.copy() if ako else A                         # stored layout
+    Bs = B if bko else B.T.copy()
+    C = gctx.test_gemm_bf16(As, Bs, ako, bko, M, N, K, ks)
+    Aq = O.bf16_round(A).astype(np.float64)
+    Bq = O.bf16_round(B).astype(np.float64)
+    ref = Aq @ Bq
+    bound = 1e-5 * (np.abs(Aq) @ np.abs(Bq)) + 1e-30
+    assert np.all(np.abs(C - ref) <= bound), float(np.max(np.abs(C - ref) / bound))
+
+
+CASES = [
+    ("bern_LB", dict(D=256, H=128, Z=32), 256),
+    ("bern_LB_tails", dict(D=200, H=136, Z=24), 200),
+    ("gauss_LB", dict(D=256, H=96, Z=16, continuous=True), 192),
+    ("bern_LA_L2", dict(D=128, H=64, Z=16, estimator="LA", L=2), 136),
+    ("gauss_mean_map", dict(D=128, H=64, Z=8, continuous=True, objective="mean_map"), 128),
+    ("synth_shape_small_batch", dict(D=4096, H=2048, Z=128), 128),
+]
+
+
+def make_ctx(cfg, B, keep_grads=True):
+    from vaeb_amd import _lib
+    return _lib.Context(cfg.D, cfg.H, cfg.Z, B, L=cfg.L, decoder=int(cfg.continuous), estimator=EST[cfg.estimator],
+                        objective=OBJ[cfg.objective], lr=cfg.lr, keep_grads=keep_grads, max_eval_rows=512,
+                        dtype=_lib.DTYPE_BF16)
+
+
+def data_for(cfg, n, seed=0):
+    if cfg.continuous:
+        return O.synthetic_frey(n=n, D=cfg.D, seed=seed)
+    return O.synthetic_mnist(n=n, D=cfg.D, seed=seed)
+
+
+@pytest.mark.parametrize("name,kw,B", CASES, ids=[c[0] for c in CASES])
+def test_bf16_step_parity(name, kw, B):
+    cfg = O.Config(**kw)
+    x = data_for(cfg, 3 * B)
+    params = O.init_params(cfg)
+    rng = np.random.default_rng(5)
+    params = [p if p.ndim == 2 else (0.01 * rng.standard_normal(p.shape)).astype(np.float32) for p in params]
+    acc = [np.full_like(p, 1e-3) for p in params]
+    eps = rng.standard_normal((cfg.L, B, cfg.Z)).astype(np.float32)
+    idx = 1
+    xb = x[idx * B:(idx + 1) * B].astype(np.float64)
+
+    ctx = make_ctx(cfg, B)
+    ctx.set_data(x)
+    ctx.set_params(O.flatten(params))
+    ctx.set_adagrad_state(O.flatten(acc))
+    ctx.set_eps_mode(1)
+    ctx.push_eps(eps)
+    elbo = ctx.update(idx)
+    g = ctx.get_grads()
+    newa = ctx.get_adagrad_state()
+    newp = ctx.get_params()
+    ctx.close()
+
+    p64 = [p.astype(np.float64) for p in params]
+    a64 = [a.astype(np.float64) for a in acc]
+    e64 = eps.astype(np.float64)
+    q_elbo, q_p, q_a, q_aux = O.step(p64, a64, xb, e64, cfg, q=O.bf16_round)
+    f_elbo, _, _, f_aux = O.step(p64, a64, xb, e64, cfg)
+
+    assert abs(elbo - q_elbo) <= 1e-4 * abs(q_elbo), (elbo, q_elbo)
+    assert abs(elbo - f_elbo) <= 1e-2 * abs(f_elbo), (elbo, f_elbo)
+    for (n, s), gg, rq, rf in zip(O.param_shapes(cfg), O.unflatten(g, cfg), q_aux["data_grads"], f_aux["data_grads"]):
+        assert rel(gg.reshape(s), rq) <= 2e-3, (n, rel(gg.reshape(s), rq))
+        assert rel(gg.reshape(s), rf) <= 8e-2, (n, rel(gg.reshape(s), rf))
+    assert rel(newa, O.flatten(q_a)) <= 4e-3
+    # the optimizer applied to the engine's own gradient reproduces theta' (fp32 rule)
+    th = O.flatten(params).astype(np.float64)
+    gg = g.astype(np.float64)
+    prior = 1.0 if cfg.objective == "sum_prior" else 0.0
+    gt = gg - prior * th
+    a2 = O.flatten(acc).astype(np.float64) + gt * gt
+    want = th + cfg.lr * gt / (np.sqrt(a2) + cfg.eps)
+    if cfg.objective == "mean_map":
+        want = want - cfg.lr * cfg.eps * th * th
+    assert np.abs(newp - want).max() <= 1e-6 + 1e-5 * np.abs(want).max()
+
+
+def test_bf16_validate_and_reconstruct():
+    cfg = O.Config(D=256, H=128, Z=32)
+    B = 128
+    x = data_for(cfg, 4 * B)
+    params = O.init_params(cfg)
+    ctx = make_ctx(cfg, B, keep_grads=False)
+    ctx.set_data(x)
+    ctx.set_params(O.flatten(params))
+    ctx.set_eps_mode(1)
+    xv = x[:300]
+    eps = np.random.default_rng(1).standard_normal((1, 300, cfg.Z)).astype(np.float32)
+    ctx.push_eps(eps)
+    got = ctx.validate(xv)
+    p64 = [p.astype(np.float64) for p in params]
+    ref = O.validate(p64, xv.astype(np.float64), eps.astype(np.float64), cfg, q=O.bf16_round)
+    assert abs(got - ref) <= 1e-4 * abs(ref), (got, ref)
+    y = ctx.reconstruct(xv)
+    out = O.forward_backward(p64, xv.astype(np.float64), np.zeros((1, 300, cfg.Z)), cfg, need_grad=False,
+                             q=O.bf16_round)
+    assert np.abs(y - out["y"]).max() <= 2e-3
+    ctx.close()
+
+
+def test_bf16_graph_epoch_matches_eager_and_tracks_oracle():
+    """10 steps with device Philox noise: graph replay == eager launches bit for bit; the
+    epoch ELBO tracks the fp32 engine on the same noise within 1e-2."""
+    from vaeb_amd import _lib
+    cfg = O.Config(D=256, H=128, Z=32)
+    B = 256
+    x = data_for(cfg, 8 * B)
+    params = O.flatten(O.init_params(cfg))
+    order = np.array([3, 1, 4, 1, 5, 7, 2, 6, 0, 2], np.int32)
+    res = {}
+    for mode, kw in (("graph", dict(use_graph=True, dtype=_lib.DTYPE_BF16)),
+                     ("eager", dict(use_graph=False, dtype=_lib.DTYPE_BF16)),
+                     ("f32", dict(use_graph=True, dtype=_lib.DTYPE_F32))):
+        ctx = _lib.Context(cfg.D, cfg.H, cfg.Z, B, max_eval_rows=B, **kw)
+        ctx.set_data(x)
+        ctx.set_params(params)
+        ctx.set_eps_mode(0, seed=10)
+        ctx.update_many(order)
+        s, n = ctx.epoch_elbo()
+        res[mode] = (s / n, ctx.get_params())
+        ctx.close()
+    assert res["graph"][0] == res["eager"][0]
+    assert np.array_equal(res["graph"][1], res["eager"][1])
+    assert abs(res["graph"][0] - res["f32"][0]) <= 1e-2 * abs(res["f32"][0])

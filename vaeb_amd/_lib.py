@@ -18,6 +18,7 @@ DEC_BERNOULLI, DEC_GAUSSIAN = 0, 1
 EST_LB, EST_LA, EST_FV = 0, 1, 2
 OBJ_SUM_PRIOR, OBJ_MEAN_MAP = 0, 1
 EPS_PHILOX, EPS_HOST = 0, 1
+DTYPE_F32, DTYPE_BF16 = 0, 1
 
 # Every symbol declared in include/vaeb_hip.h (checked by tests/test_abi.py).
 EXPORTS = [
@@ -27,7 +28,7 @@ EXPORTS = [
     "vaeb_push_eps", "vaeb_set_step", "vaeb_update", "vaeb_update_async", "vaeb_update_many",
     "vaeb_epoch_elbo", "vaeb_synchronize", "vaeb_validate", "vaeb_reconstruct",
     "vaeb_comm_unique_id", "vaeb_comm_init", "vaeb_get_grads", "vaeb_get_activation",
-    "vaeb_profile_steps", "vaeb_kernel_name", "vaeb_debug_timeline",
+    "vaeb_profile_steps", "vaeb_kernel_name", "vaeb_debug_timeline", "vaeb_test_gemm_bf16",
 ]
 
 
@@ -38,7 +39,7 @@ class VaebConfig(ctypes.Structure):
         ("decoder", ctypes.c_int32), ("estimator", ctypes.c_int32), ("objective", ctypes.c_int32),
         ("lr", ctypes.c_float), ("adagrad_eps", ctypes.c_float), ("device", ctypes.c_int32),
         ("max_eval_rows", ctypes.c_int32), ("use_graph", ctypes.c_int32), ("keep_grads", ctypes.c_int32),
-        ("reserved", ctypes.c_int32 * 6),
+        ("dtype", ctypes.c_int32), ("reserved", ctypes.c_int32 * 5),
     ]
 
 
@@ -93,6 +94,7 @@ def load():
         "vaeb_kernel_name": ([ctypes.c_int32, ctypes.c_char_p, ctypes.c_int32], ctypes.c_int),
         "vaeb_debug_timeline": ([_P, ctypes.c_int32, ctypes.POINTER(ctypes.c_uint64), _I64,
                                  ctypes.POINTER(ctypes.c_int32)], ctypes.c_int),
+        "vaeb_test_gemm_bf16": ([_P] + [ctypes.c_int32] * 5 + [_F, _F, _F, ctypes.c_int32], ctypes.c_int),
     }
     for name, (args, res) in sig.items():
         fn = getattr(lib, name)
@@ -118,7 +120,7 @@ class Context:
 
     def __init__(self, D, H, Z, B, L=1, decoder=DEC_BERNOULLI, estimator=EST_LB, objective=OBJ_SUM_PRIOR,
                  lr=0.01, adagrad_eps=1e-6, device=0, B_global=None, row_offset=0, max_eval_rows=10000,
-                 use_graph=True, keep_grads=False):
+                 use_graph=True, keep_grads=False, dtype=DTYPE_F32):
         self.lib = load()
         cfg = VaebConfig()
         cfg.D, cfg.H, cfg.Z, cfg.B, cfg.L = D, H, Z, B, L
@@ -128,6 +130,7 @@ class Context:
         cfg.lr, cfg.adagrad_eps = lr, adagrad_eps
         cfg.device, cfg.max_eval_rows = device, max_eval_rows
         cfg.use_graph, cfg.keep_grads = int(bool(use_graph)), int(bool(keep_grads))
+        cfg.dtype = int(dtype)
         self.cfg = cfg
         self.h = _P()
         check(self.lib.vaeb_create(ctypes.byref(cfg), ctypes.byref(self.h)))
@@ -243,6 +246,16 @@ class Context:
         buf = (ctypes.c_uint8 * 128).from_buffer_copy(uid)
         check(self.lib.vaeb_comm_init(self.h, buf, rank, world))
 
+    def test_gemm_bf16(self, A, B, a_kouter, b_kouter, M, N, K, ksplit=1):
+        """bf16 GEMM engine test hook: C[M x N] = sum_k A(m,k) B(k,n); A stored [M,K] or
+        (a_kouter) [K,M], B stored [N,K] or (b_kouter) [K,N]."""
+        A = np.ascontiguousarray(A, np.float32)
+        B = np.ascontiguousarray(B, np.float32)
+        C = np.empty((M, N), np.float32)
+        check(self.lib.vaeb_test_gemm_bf16(self.h, int(a_kouter), int(b_kouter), M, N, K, fptr(A), fptr(B), fptr(C),
+                                           int(ksplit)))
+        return C
+
     # ---- measurement
     def debug_timeline(self, batch_index=0):
         """[launch][workgroup][slot] 100 MHz stamps of one eager step (diagnostics)."""
@@ -253,11 +266,11 @@ class Context:
         return out.reshape(16, 1024, 8)[:nl.value]
 
     def profile_steps(self, n_steps):
-        ms = np.zeros(16, np.float32)
-        ids = np.zeros(16, np.int32)
+        ms = np.zeros(32, np.float32)
+        ids = np.zeros(32, np.int32)
         nk = ctypes.c_int32()
         check(self.lib.vaeb_profile_steps(self.h, n_steps, fptr(ms), ids.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)),
-                                          16, ctypes.byref(nk)))
+                                          32, ctypes.byref(nk)))
         out = []
         for k in range(nk.value):
             buf = ctypes.create_string_buffer(64)

@@ -1,0 +1,450 @@
+// gemm_bf16.hpp -- bf16 MFMA GEMM engine for the large-batch SGVB step (gfx950).
+//
+// BASELINE config 5 (synthetic 4096 -> 2048 -> 128, batch 8192 per GPU) is a chain of
+// dense contractions big enough to fill the chip, so unlike the batch-100 fp32 path
+// (tile_engine.hpp, latency-bound) this engine is built for MFMA throughput:
+//
+//  * C[M x N] = sum_k A(m, k) B(k, n) with bf16 operands and fp32 accumulation on
+//    v_mfma_f32_16x16x32_bf16 (lane l holds A[l&15][8(l>>4)+j] and B[8(l>>4)+j][l&15],
+//    C/D: col = l&15, row = 4(l>>4)+r);
+//  * every operand is used IN ITS NATURAL LAYOUT: an operand is either K-contiguous
+//    (KC, stored [rows][K]) or K-outer (KO, stored [K][rows]).  KC tiles are read with
+//    ds_read_b128, KO tiles with the gfx950 transposing read ds_read_b64_tr_b16 -- so
+//    the forward (X W3), the data-gradient (dA2 W2^T) and the weight-gradient
+//    (X^T dA3) products all read the same single copy of each weight / activation and
+//    no transposed copies are ever written;
+//  * 128 x 128 x 64 block tile, 256 threads = 4 waves (2 x 2), 64 x 64 per wave
+//    (4 x 4 MFMA tiles, 64 accumulator VGPRs), register-staged double buffer
+//    (next tile's global loads issued before this tile's MFMAs, written to the other
+//    LDS buffer after them: one barrier per K tile), 64 KiB LDS, 2 blocks per CU;
+//  * LDS images are XOR-swizzled so the fragment reads are bank-conflict free:
+//    KC (128-B rows): 16-B chunk c of row r at c ^ ((r >> 1) & 7)  (ds_read_b128 lane
+//    groups of MI355X_MICROARCH.md §LDS);  KO (256-B k-rows): chunk c of k-row r at
+//    c ^ (((r & 3) << 1) | (((r >> 3) & 1) << 3))  (ds_read_b64_tr_b16 32-lane halves);
+//  * operand loads are 16-B raw buffer loads; a chunk outside [0, rows) x [0, K) is
+//    redirected out of range and reads 0 (tails need rows and K to be multiples of 8);
+//  * split-K over gridDim.y for the thin products (latent-width N or M): each slice
+//    stores an fp32 slab that a later kernel sums in fixed order (deterministic);
+//  * tile order: the linear block id is remapped so that the blocks sharing one XCD
+//    (blockIdx % 8, guide T1) take a contiguous run of tiles, grouped 8 row tiles at a
+//    time so concurrently running blocks share operand panels in that XCD's L2.
+// Epilogues are functors applied to the wave's 64 x 64 accumulator block in registers.
+#pragma once
+#include "tile_engine.hpp"
+
+namespace vaeb {
+namespace bf {
+
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+typedef uint16_t bf16_t;   // raw bf16 bits in memory
+
+enum : int { KC = 0, KO = 1 };
+constexpr int BM = 128, BN = 128, BK = 64, NTHR = 256;
+constexpr int kTileBytes = BM * BK * 2;          // one operand tile image (16 KiB)
+constexpr int kStageBytes = 2 * kTileBytes;      // A + B
+constexpr int kLdsBytes = 2 * kStageBytes;       // double buffer (64 KiB)
+
+// f32 -> bf16, round to nearest even (inputs here are finite)
+DEV uint32_t f2bf(float f) {
+    const uint32_t u = __builtin_bit_cast(uint32_t, f);
+    return (u + 0x7FFFu + ((u >> 16) & 1u)) >> 16;
+}
+DEV float bf2f(uint32_t b) { return __builtin_bit_cast(float, b << 16); }
+
+DEV int swz_kc(int r) { return (r >> 1) & 7; }
+DEV int swz_ko(int r) { return ((r & 3) << 1) | (((r >> 3) & 1) << 3); }
+
+// One 128-row x 64-k operand tile: 4 x 16 B per thread, global -> registers -> LDS.
+template <int LAY>
+struct TileLoader {
+    rsrc_t buf;
+    int ld;        // row stride (elements) of the stored matrix
+    int rlim;      // valid rows (M or N extent)
+    int klim;      // end of this block's K range
+    int r0;        // first row of the tile
+    DEV void load(v4u (&st)[4], int k0) const {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int id = threadIdx.x + NTHR * i;
+            uint32_t off;
+            if constexpr (LAY == KC) {
+                const int r = r0 + (id >> 3), k = k0 + (id & 7) * 8;
+                off = (r < rlim && k < klim) ? ((uint32_t)r * (uint32_t)ld + (uint32_t)k) * 2u : kOOB;
+            } else {
+                const int k = k0 + (id >> 4), r = r0 + (id & 15) * 8;
+                off = (k < klim && r < rlim) ? ((uint32_t)k * (uint32_t)ld + (uint32_t)r) * 2u : kOOB;
+            }
+            st[i] = __builtin_bit_cast(v4u, __builtin_amdgcn_raw_buffer_load_b128(buf, off, 0, 0));
+        }
+    }
+    DEV void store(const v4u (&st)[4], char* img) const {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int id = threadIdx.x + NTHR * i;
+            int o;
+            if constexpr (LAY == KC) {
+                const int r = id >> 3, c = id & 7;
+                o = r * 128 + ((c ^ swz_kc(r)) << 4);
+            } else {
+                const int r = id >> 4, c = id & 15;
+                o = r * 256 + ((c ^ swz_ko(r)) << 4);
+            }
+            *reinterpret_cast<v4u*>(img + o) = st[i];
+        }
+    }
+};
+
+// Fragment (8 consecutive k of one row / column) for MFMA k-step kk (k = 32 kk ...)
+// of the 16 rows starting at `row` of the tile image.
+template <int LAY>
+DEV bf16x8 frag(const char* img, int row, int kk, int lane) {
+    if constexpr (LAY == KC) {
+        const int r = row + (lane & 15);
+        const int c = 4 * kk + (lane >> 4);
+        return *reinterpret_cast<const bf16x8*>(img + r * 128 + ((c ^ swz_kc(r)) << 4));
+    } else {
+        // ds_read_b64_tr_b16: lane 4q+p of each 16-lane group supplies k-row q of its
+        // 4-row block, columns 4p..4p+3; lane i receives column i, k-row q in element q.
+        const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+        const int kr = 32 * kk + 8 * g + q;
+        const int c = (row >> 3) + (p >> 1);
+        const int o = ((c ^ swz_ko(kr)) << 4) + (p & 1) * 8;   // swz_ko(kr + 4) == swz_ko(kr)
+        const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + kr * 256 + o));
+        const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + (kr + 4) * 256 + o));
+        const s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        return __builtin_bit_cast(bf16x8, v);
+    }
+}
+
+// Device-side minibatch resolution: rows of batch order[*cursor] start `stride`
+// elements after the base (the cursor advances in the step's last kernel), so a whole
+// epoch replays as graphs with no host round trip.  order == nullptr: offset 0.
+struct BatchRef {
+    const int* order; const int* cursor; int64_t stride;
+    DEV int64_t offset() const { return order ? (int64_t)order[*cursor] * stride : 0; }
+};
+
+struct GemmArgs {
+    const bf16_t* A; int lda; int64_t a_bytes;   // a_bytes: readable extent from A
+    BatchRef ab;                                 // A += ab.offset() (the dataset operand)
+    const bf16_t* B; int ldb; int64_t b_bytes;
+    int M, N, K;
+    int tiles_m, tiles_n;
+    int kslice;    // K per split-K slice (multiple of BK); gridDim.y slices
+};
+
+// Bijective XCD-contiguous remap of the linear tile id (guide §5 template), then a
+// grouped order: runs of GM row tiles sweep all column tiles.
+DEV void tile_of(const GemmArgs& g, int& tm, int& tn) {
+    constexpr int GM = 8;
+    const int nwg = g.tiles_m * g.tiles_n;
+    const int b = blockIdx.x;
+    int t = b;
+    if (nwg >= 16) {
+        const int xcd = b & 7, q = nwg >> 3, r = nwg & 7;
+        t = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (b >> 3);
+    }
+    const int per_group = GM * g.tiles_n;
+    const int grp = t / per_group, in = t - grp * per_group;
+    const int gm = min(GM, g.tiles_m - grp * GM);
+    tm = grp * GM + in % gm;
+    tn = in / gm;
+}
+
+template <int LA, int LB, class Epi>
+__global__ __launch_bounds__(NTHR, 2) void gemm_kernel(GemmArgs g, Epi e) {
+    __shared__ __attribute__((aligned(16))) char smem[kLdsBytes];
+    int tm, tn;
+    tile_of(g, tm, tn);
+    const int m0 = tm * BM, n0 = tn * BN;
+    const int kz = blockIdx.y;
+    const int kbeg = kz * g.kslice;
+    const int kend = min(g.K, kbeg + g.kslice);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int wm = wave >> 1, wn = wave & 1;
+
+    TileLoader<LA> la{mkbuf(g.A + g.ab.offset(), g.a_bytes), g.lda, g.M, kend, m0};
+    TileLoader<LB> lb{mkbuf(g.B, g.b_bytes), g.ldb, g.N, kend, n0};
+
+    f32x4 acc[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = zero4();
+
+    const int nkt = (kend - kbeg + BK - 1) / BK;
+    v4u sa[4], sb[4];
+    if (nkt > 0) {
+        la.load(sa, kbeg);
+        lb.load(sb, kbeg);
+        la.store(sa, smem);
+        lb.store(sb, smem + kTileBytes);
+    }
+    __syncthreads();
+    for (int t = 0; t < nkt; ++t) {
+        char* As = smem + (t & 1) * kStageBytes;
+        char* Bs = As + kTileBytes;
+        const bool more = t + 1 < nkt;
+        if (more) {
+            la.load(sa, kbeg + (t + 1) * BK);
+            lb.load(sb, kbeg + (t + 1) * BK);
+        }
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {
+            bf16x8 af[4], bfr[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) af[i] = frag<LA>(As, wm * 64 + 16 * i, kk, lane);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) bfr[j] = frag<LB>(Bs, wn * 64 + 16 * j, kk, lane);
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+        }
+        if (more) {
+            char* nx = smem + ((t + 1) & 1) * kStageBytes;
+            la.store(sa, nx);
+            lb.store(sb, nx + kTileBytes);
+        }
+        __syncthreads();
+    }
+    e(m0 + wm * 64, n0 + wn * 64, acc, kz);
+}
+
+// ------------------------------------------------------------------ helpers
+// Lane l's element (i, j, r) of a wave block at (mw, nw): row mw + 16i + 4(l>>4) + r,
+// column nw + 16j + (l&15).
+DEV int erow(int mw, int i, int r, int lane) { return mw + 16 * i + 4 * (lane >> 4) + r; }
+DEV int ecol(int nw, int j, int lane) { return nw + 16 * j + (lane & 15); }
+
+// Column sums of the wave's 64 x 64 block (each lane: its column of tile j), reduced
+// over the 4 lane groups that share a column.  Lanes 0..15 hold the result for tile j.
+DEV float colsum_lanes(float s) {
+    s += __shfl_xor(s, 16, 64);
+    s += __shfl_xor(s, 32, 64);
+    return s;
+}
+
+// ------------------------------------------------------------------ epilogues
+// Plain fp32 store (split-K slabs: slice kz at out + kz * slab).
+struct EpiF32 {
+    float* out; int ldo; int M, N; int64_t slab;
+    DEV void operator()(int mw, int nw, f32x4 (&acc)[4][4], int kz) const {
+        const int lane = threadIdx.x & 63;
+        float* o = out + (int64_t)kz * slab;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int row = erow(mw, i, r, lane), col = ecol(nw, j, lane);
+                    if (row < M && col < N) o[(int64_t)row * ldo + col] = acc[i][j][r];
+                }
+    }
+};
+
+// v = act(acc + bias[col]) stored as bf16 (and optionally fp32).
+struct EpiBiasAct {
+    const float* bias; int tanh_act; int M, N;
+    bf16_t* out; int ldo;
+    DEV void operator()(int mw, int nw, f32x4 (&acc)[4][4], int) const {
+        const int lane = threadIdx.x & 63;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int col = ecol(nw, j, lane);
+            if (col >= N) continue;
+            const float b = bias[col];
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int row = erow(mw, i, r, lane);
+                    float v = acc[i][j][r] + b;
+                    if (tanh_act) v = ftanh(v);
+                    if (row < M) out[(int64_t)row * ldo + col] = (bf16_t)f2bf(v);
+                }
+        }
+    }
+};
+
+// Backward through tanh: out = acc * (1 - t^2) with t the stored bf16 activation at the
+// same (row, col); column sums of out (fp32, before rounding) -> colpart[mw/64][col]
+// (the bias gradient, reduced in fixed order by the optimizer).
+struct EpiDTanh {
+    const bf16_t* t; int ldt; int M, N;
+    bf16_t* out; int ldo;
+    float* colpart;
+    DEV void operator()(int mw, int nw, f32x4 (&acc)[4][4], int) const {
+        const int lane = threadIdx.x & 63;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int col = ecol(nw, j, lane);
+            const bool cok = col < N;
+            float cs = 0.f;
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int row = erow(mw, i, r, lane);
+                    if (cok && row < M) {
+                        const float tv = bf2f(t[(int64_t)row * ldt + col]);
+                        const float v = acc[i][j][r] * (1.f - tv * tv);
+                        out[(int64_t)row * ldo + col] = (bf16_t)f2bf(v);
+                        cs += v;
+                    }
+                }
+            cs = colsum_lanes(cs);
+            if (lane < 16 && cok) colpart[(int64_t)(mw >> 6) * N + col] = cs;
+        }
+    }
+};
+
+// Decoder output (VAEB.py:257-263, 302-313) on the [M_e x Dn] block of a2 (| a6):
+//  Bernoulli: a = acc + b2; log p += x a - softplus(a); dA2 = sl (x - sigmoid(a)).
+//  Gaussian : columns interleave in 32-wide groups ([W2 cols | W6 cols] per 64), so a
+//             wave's tiles j and j + 2 hold a2 and a6 of the same 32 data columns:
+//             y = sigmoid(a2), r = x - y, log p += -1/2 log 2pi - a6/2 - r^2 e^-a6 / 2,
+//             dA2 = sl r e^-a6 y (1 - y), dA6 = sl (-1/2 + r^2 e^-a6 / 2).
+// Per-row log p partials -> lp[row * nlp + nw/64]; bias-gradient column sums of dA ->
+// colpart[mw/64][col]; y (decoder mean, reconstruction) when yout != nullptr.
+template <bool GAUSS>
+struct EpiDecOut {
+    const float *b2, *b6;
+    const bf16_t* x; int ldx; int Mx;   // data row of output row m is m % Mx
+    int M, N, D;                        // N = Dn (D or 2D)
+    int train;
+    float sl;                           // sc / L
+    BatchRef xb;                        // device-resolved minibatch offset of x
+    bf16_t* dA; int ldd;
+    float* lp; int nlp;
+    float* colpart;
+    float* yout;
+    DEV void operator()(int mw, int nw, f32x4 (&acc)[4][4], int) const {
+        const int lane = threadIdx.x & 63;
+        if (nw >= N) return;
+        const bf16_t* xr = x + xb.offset();
+        float rs[4][4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) rs[i][r] = 0.f;
+        constexpr int JN = GAUSS ? 2 : 4;
+#pragma unroll
+        for (int j = 0; j < JN; ++j) {
+            const int col = ecol(nw, j, lane);                               // dA column
+            const int d = GAUSS ? (nw >> 1) + 16 * j + (lane & 15) : col;   // data column
+            const bool cok = d < D;
+            const float bb2 = cok ? b2[d] : 0.f;
+            const float bb6 = (GAUSS && cok) ? b6[d] : 0.f;
+            float cs2 = 0.f, cs6 = 0.f;
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int row = erow(mw, i, r, lane);
+                    if (!(cok && row < M)) continue;
+                    const float xv = bf2f(xr[(int64_t)(row % Mx) * ldx + d]);
+                    const float a2 = acc[i][j][r] + bb2;
+                    const float y = sigmoidf(a2);
+                    float lpv, g2, g6 = 0.f;
+                    if constexpr (!GAUSS) {
+                        lpv = xv * a2 - softplusf(a2);
+                        g2 = sl * (xv - y);
+                    } else {
+                        const float a6 = acc[i][j + 2][r] + bb6;
+                        const float rr = xv - y, e6 = fexp(-a6);
+                        lpv = -kHalfLog2Pi - 0.5f * a6 - 0.5f * rr * rr * e6;
+                        g2 = sl * rr * e6 * y * (1.f - y);
+                        g6 = sl * (-0.5f + 0.5f * rr * rr * e6);
+                    }
+                    rs[i][r] += lpv;
+                    if (yout) yout[(int64_t)row * D + d] = y;
+                    if (train) {
+                        dA[(int64_t)row * ldd + col] = (bf16_t)f2bf(g2);
+                        cs2 += g2;
+                        if constexpr (GAUSS) {
+                            dA[(int64_t)row * ldd + col + 32] = (bf16_t)f2bf(g6);
+                            cs6 += g6;
+                        }
+                    }
+                }
+            if (train) {
+                cs2 = colsum_lanes(cs2);
+                if (lane < 16 && cok) colpart[(int64_t)(mw >> 6) * N + col] = cs2;
+                if constexpr (GAUSS) {
+                    cs6 = colsum_lanes(cs6);
+                    if (lane < 16 && cok) colpart[(int64_t)(mw >> 6) * N + col + 32] = cs6;
+                }
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const float s = sum16(rs[i][r]);
+                const int row = erow(mw, i, r, lane);
+                if ((lane & 15) == 0 && row < M) lp[(int64_t)row * nlp + (nw >> 6)] = s;
+            }
+    }
+};
+
+// Where element (m, n) of a weight-gradient product lives in the reference-order fp32
+// arena.  mode 0: one array [M x N]; mode 1: [W4 | W5] column split at n0 (each
+// [H x n0]); mode 2: the Gaussian decoder's 32-column interleave of [W2 | W6].
+struct ColMap {
+    int mode, n0;
+    int64_t off0, off1;
+    int ld0, ld1;
+    DEV int64_t at(int m, int n) const {
+        if (mode == 0) return off0 + (int64_t)m * ld0 + n;
+        if (mode == 1) return n < n0 ? off0 + (int64_t)m * ld0 + n : off1 + (int64_t)m * ld1 + (n - n0);
+        const int seg = (n >> 5) & 1, d = ((n >> 6) << 5) | (n & 31);
+        return (seg ? off1 : off0) + (int64_t)m * (seg ? ld1 : ld0) + d;
+    }
+};
+
+// Weight update from the data gradient dsg of one element (VAEB.py:386-444):
+// g = dsg - prior theta; acc += g^2; theta' = theta + lr g / (sqrt(acc) + eps) - decay theta^2.
+struct Opt {
+    const float* th_in; float* th_out; float* accum; float* grad;
+    bf16_t* shadow_out;   // bf16 copy of theta' in GEMM layout (index m * N + n)
+    float lr, eps, prior, decay;
+    int update, store_grad;
+    DEV void apply(int64_t idx, int64_t sidx, float dsg) const {   // sidx < 0: no shadow
+        if (store_grad) grad[idx] = dsg;
+        if (!update) return;
+        const float th = th_in[idx];
+        float a = accum[idx];
+        const float gg = dsg - prior * th;
+        a += gg * gg;
+        const float tn = th + lr * gg / (__builtin_amdgcn_sqrtf(a) + eps) - decay * th * th;
+        accum[idx] = a;
+        th_out[idx] = tn;
+        if (sidx >= 0) shadow_out[sidx] = (bf16_t)f2bf(tn);
+    }
+};
+
+struct EpiAdagrad {
+    ColMap map; Opt opt; int M, N;
+    DEV void operator()(int mw, int nw, f32x4 (&acc)[4][4], int) const {
+        const int lane = threadIdx.x & 63;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int row = erow(mw, i, r, lane), col = ecol(nw, j, lane);
+                    if (row < M && col < N) opt.apply(map.at(row, col), (int64_t)row * N + col, acc[i][j][r]);
+                }
+    }
+};
+
+}  // namespace bf
+}  // namespace vaeb

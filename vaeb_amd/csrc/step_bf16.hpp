@@ -1,0 +1,267 @@
+// step_bf16.hpp -- the non-GEMM kernels of the bf16 large-batch SGVB step.
+//
+// The step (VAEB.update, /root/reference/VAEB.py:408-415) on the bf16 engine is
+//   enc     h     = tanh(X W3 + b3)                      GEMM, KC x KO   VAEB.py:246
+//   heads   [mu|lv] slabs = h [W4|W5]                    GEMM split-K    VAEB.py:248-249
+//   latent  mu, lv (+bias), eps, z, KL / LA row terms    latent_fwd      VAEB.py:41-47, 315-346
+//   dechid  hd    = tanh(z W1 + b1)                      GEMM            VAEB.py:254
+//   decout  log p(x|z) row partials, dA2 (| dA6)         GEMM + EpiDecOut VAEB.py:257-313
+//   dhd     dA1   = ([dA2|dA6] [W2|W6]^T) (1 - hd^2)     GEMM KC x KC
+//   dW26    Adagrad([hd]^T [dA2|dA6])                    GEMM KO x KO + EpiAdagrad
+//   dz      dZ slabs = dA1 W1^T                          GEMM split-K
+//   dW1     slabs z^T dA1 -> wreduce_opt                 GEMM split-K
+//   latentb [dMu|dLv] (sum over l), b4/b5 column sums    latent_bwd      
+//   dh      dA3   = ([dMu|dLv] [W4|W5]^T) (1 - h^2)      GEMM KC x KC
+//   dW45    slabs h^T [dMu|dLv] -> wreduce_opt           GEMM split-K
+//   dW3     Adagrad(X^T dA3)                             GEMM KO x KO + EpiAdagrad
+//   bias    bias gradients from the column partials, Adagrad, ELBO reduce, cursor++
+// Parameters keep fp32 masters in the reference-order arena (ping-pong, as the fp32
+// path) plus a bf16 "shadow" arena in GEMM layout that the optimizer rewrites each step:
+//   W3 [D x H] | W45 [H x 2Z] (row h = [W4 row h | W5 row h]) | W1 [Z x H] |
+//   W26 [H x Dn] (Bernoulli: W2; Gaussian: W2 / W6 interleaved in 32-column groups).
+#pragma once
+#include "gemm_bf16.hpp"
+#include "kernels_aux.hpp"
+
+namespace vaeb {
+namespace bf {
+
+// Arena (reference order) -> shadow index map.
+struct ShadowMap {
+    int64_t offW3, offW4, offW5, offW1, offW2, offW6;   // arena offsets (offW6 < 0: Bernoulli)
+    int64_t s3, s45, s1, s26;                           // shadow offsets
+    int D, H, Z;
+    int64_t nweights;                                   // arena elements before the biases
+    DEV int64_t at(int64_t i) const {
+        if (i >= nweights) return -1;
+        const int Z2 = 2 * Z;
+        if (i < offW4) return s3 + (i - offW3);
+        if (i < offW5) { const int64_t e = i - offW4; return s45 + (e / Z) * Z2 + e % Z; }
+        if (i < offW1) { const int64_t e = i - offW5; return s45 + (e / Z) * Z2 + Z + e % Z; }
+        if (i < offW2) return s1 + (i - offW1);
+        const bool w6 = offW6 >= 0 && i >= offW6;
+        const int64_t e = i - (w6 ? offW6 : offW2);
+        const int64_t h = e / D, d = e % D;
+        if (offW6 < 0) return s26 + h * D + d;
+        return s26 + h * 2 * D + ((d >> 5) << 6) + (w6 ? 32 : 0) + (d & 31);
+    }
+};
+
+// theta (fp32 arena) -> bf16 shadow
+__global__ __launch_bounds__(256) void make_shadow_kernel(const float* th, bf16_t* sh, ShadowMap m) {
+    const int64_t stride = (int64_t)gridDim.x * 256;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < m.nweights; i += stride)
+        sh[m.at(i)] = (bf16_t)f2bf(th[i]);
+}
+
+// fp32 rows -> bf16 (dataset upload)
+__global__ __launch_bounds__(256) void to_bf16_kernel(const float* in, bf16_t* out, int64_t n) {
+    const int64_t stride = (int64_t)gridDim.x * 256;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) out[i] = (bf16_t)f2bf(in[i]);
+}
+
+struct LatentArgs {
+    int M, Z, L, est, mode;        // M rows of this launch; mode: MODE_TRAIN / EVAL / RECON
+    float sc;
+    const float* ml_slab; int nslab;   // heads split-K slabs [nslab][M][2Z]
+    const float *b4, *b5;
+    float *mu, *lv, *eps;              // [M][Z], [M][Z], [L][M][Z]
+    bf16_t* z;                         // [L][M][Z]
+    float* kl_part;                    // LB: [M]; LA: [L][M]
+    // noise (VAEB.py:41-47): Philox keyed by (seed, step, global row, l*Z + j)
+    int eps_mode; uint64_t seed; const int64_t* step; uint32_t domain;
+    const float* eps_in; int64_t eps_in_ld;
+    BatchRef rows; int64_t row_base_add;   // global row of local row 0 = batch*mul + add
+    int64_t row_base_mul;
+    // backward
+    const float* dz_slab; int ndz;     // [ndz][L*M][Z]
+    bf16_t* dmulv;                     // [M][2Z]
+    float* colpart;                    // [ceil(M/64)][2Z]
+};
+
+// One wave per row: mu / lv from the heads slabs (fixed-order sum) + bias; eps; z; the
+// per-row KL (LB, VAEB.py:343) or, per sample, prior - logQ (LA, VAEB.py:322-325).
+__global__ __launch_bounds__(256) void latent_fwd_kernel(LatentArgs a) {
+    const int lane = threadIdx.x & 63;
+    const int m = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (m >= a.M) return;
+    const int Z = a.Z, Z2 = 2 * Z;
+    const int64_t brow = a.rows.order ? (int64_t)a.rows.order[*a.rows.cursor] : 0;
+    const int64_t grow = brow * a.row_base_mul + a.row_base_add + m;
+    const uint64_t c23 = (uint64_t)(*a.step) ^ ((uint64_t)a.domain << 63);
+    float kl = 0.f;
+    float la[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};   // LA: L <= 8 on this path
+    for (int j = lane; j < Z; j += 64) {
+        float mu = a.b4[j], lv = a.b5[j];
+        for (int s = 0; s < a.nslab; ++s) {
+            const float* sl = a.ml_slab + ((int64_t)s * a.M + m) * Z2;
+            mu += sl[j];
+            lv += sl[Z + j];
+        }
+        a.mu[(int64_t)m * Z + j] = mu;
+        a.lv[(int64_t)m * Z + j] = lv;
+        const float sd = fexp(0.5f * lv);
+        kl += 0.5f * (1.f + lv - mu * mu - fexp(lv));
+        for (int l = 0; l < a.L; ++l) {
+            float e = 0.f;
+            if (a.mode != MODE_RECON) {
+                if (a.eps_mode == 0) e = philox_normal(a.seed, (uint32_t)grow, (uint32_t)(l * Z + j), c23);
+                else e = a.eps_in[((int64_t)l * a.eps_in_ld + m) * Z + j];
+            }
+            const float z = mu + sd * e;
+            const int64_t o = ((int64_t)l * a.M + m) * Z + j;
+            a.eps[o] = e;
+            a.z[o] = (bf16_t)f2bf(z);
+            if (a.est == EST_LA && l < 8) {
+                // log p(z) - log q(z|x) = -z^2/2 + lv/2 + (z - mu)^2 e^{-lv} / 2
+                la[l] += -0.5f * z * z + 0.5f * lv + 0.5f * e * e;
+            }
+        }
+    }
+    if (a.est == EST_LA) {
+        for (int l = 0; l < a.L && l < 8; ++l) {
+            float v = la[l];
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+            if (lane == 0) a.kl_part[(int64_t)l * a.M + m] = v;
+        }
+    } else {
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) kl += __shfl_xor(kl, o, 64);
+        if (lane == 0) a.kl_part[m] = kl;
+    }
+}
+
+// [dMu | dLv] from the dZ slabs (LA direct terms folded as in the
+// fp32 path), stored bf16 for the dh / dW45 GEMMs; column sums per 64-row block for the
+// b4 / b5 gradients.  Block = 64 rows x (256 / 64 = 4) column groups; grid.x row blocks.
+__global__ __launch_bounds__(256) void latent_bwd_kernel(LatentArgs a) {
+    const int Z = a.Z, Z2 = 2 * Z;
+    const int m0 = blockIdx.x * 64;
+    const int LM = a.L * a.M;
+    const float sl = a.sc / (float)a.L;
+    for (int c = threadIdx.x >> 6; c < Z2; c += 4) {
+        // each wave: column c of [dMu | dLv] over the block's 64 rows (lane = row)
+        const int m = m0 + (threadIdx.x & 63);
+        const bool isv = c >= Z;
+        const int j = isv ? c - Z : c;
+        float v = 0.f;
+        if (m < a.M) {
+            const int64_t o = (int64_t)m * Z + j;
+            const float mu = a.mu[o], lv = a.lv[o];
+            const float sd = fexp(0.5f * lv);
+            float g = 0.f, t = 0.f;
+            for (int l = 0; l < a.L; ++l) {
+                const int64_t ol = ((int64_t)l * a.M + m) * Z + j;
+                float dz = 0.f;
+                for (int s = 0; s < a.ndz; ++s) dz += a.dz_slab[(int64_t)s * LM * Z + ol];
+                const float e = a.eps[ol];
+                const float z = mu + sd * e;
+                if (!isv) {
+                    g += dz;
+                    if (a.est == EST_LA) t += -z;
+                } else {
+                    g += dz * 0.5f * sd * e;
+                    if (a.est == EST_LA) t += 0.5f - 0.5f * z * sd * e;
+                }
+            }
+            if (a.est == EST_LA) v = g + sl * t;
+            else v = isv ? g + a.sc * 0.5f * (1.f - fexp(lv)) : g - a.sc * mu;
+            a.dmulv[(int64_t)m * Z2 + c] = (bf16_t)f2bf(v);
+        }
+        float s = v;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+        if ((threadIdx.x & 63) == 0) a.colpart[(int64_t)blockIdx.x * Z2 + c] = s;
+    }
+}
+
+// Split-K weight gradients: sum the slabs in fixed order, then the optimizer rule.
+struct WReduceArgs {
+    const float* slab; int nslab; int M, N;   // slabs [nslab][M][N]
+    ColMap map; Opt opt; bf16_t* shadow;      // shadow: this weight's GEMM-layout copy
+};
+__global__ __launch_bounds__(256) void wreduce_opt_kernel(WReduceArgs w) {
+    const int64_t MN = (int64_t)w.M * w.N;
+    const int64_t stride = (int64_t)gridDim.x * 256;
+    for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < MN; e += stride) {
+        float g = 0.f;
+        for (int s = 0; s < w.nslab; ++s) g += w.slab[(int64_t)s * MN + e];
+        const int m = (int)(e / w.N), n = (int)(e % w.N);
+        w.opt.apply(w.map.at(m, n), e, g);
+    }
+}
+
+// Bias gradients from the epilogues' column partials (fixed order), optimizer rule, and
+// one extra workgroup that reduces the ELBO partials and advances cursor / step.
+struct BiasSeg {
+    const float* part; int nrb; int N;   // partials [nrb][N]
+    ColMap map;                           // column -> arena index (biases: ld = 0)
+};
+struct BiasArgs {
+    BiasSeg seg[4]; int nseg;
+    int total;                            // sum of the segments' N
+    Opt opt;
+    ElboArgs elbo;
+};
+__global__ __launch_bounds__(256) void bias_opt_kernel(BiasArgs b) {
+    if (blockIdx.x == gridDim.x - 1) {
+        __shared__ double sh[256];
+        elbo_reduce(b.elbo, sh);
+        return;
+    }
+    int e = blockIdx.x * 256 + threadIdx.x;
+    if (e >= b.total) return;
+    int s = 0;
+    while (s < b.nseg - 1 && e >= b.seg[s].N) { e -= b.seg[s].N; ++s; }
+    const BiasSeg& g = b.seg[s];
+    float v = 0.f;
+    for (int r = 0; r < g.nrb; ++r) v += g.part[(int64_t)r * g.N + e];
+    b.opt.apply(g.map.at(0, e), -1, v);
+}
+
+// DP: after the all-reduce of [grad arena | SGVB], the replicated optimizer over the
+// whole arena, rewriting the bf16 shadow.
+__global__ __launch_bounds__(256) void adagrad_bf16_kernel(Opt o, int64_t P, ShadowMap m, ElboArgs e) {
+    const int64_t stride = (int64_t)gridDim.x * 256;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < P; i += stride) {
+        Opt q = o;
+        q.store_grad = 0;
+        q.apply(i, m.at(i), o.grad[i]);
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        const double v = (double)o.grad[P] * e.inv_bglob;
+        *e.elbo_out = (float)v;
+        e.epoch[0] += v;
+        e.epoch[1] += 1.0;
+        *e.cursor += 1;
+        *e.step += 1;
+    }
+}
+
+}  // namespace bf
+}  // namespace vaeb
+
+namespace vaeb {
+namespace bf {
+
+// Device buffers of the bf16 engine (one context).  Row capacity R = max(B, eval chunk).
+struct BfState {
+    bool on = false;
+    int Dn = 0;                        // decoder output width (D, or 2D interleaved)
+    int64_t S = 0;                     // shadow elements
+    int64_t s3 = 0, s45 = 0, s1 = 0, s26 = 0;
+    bf16_t* shadow2[2] = {nullptr, nullptr};
+    bf16_t* x = nullptr;               // dataset [N x D] bf16
+    bf16_t* xeval = nullptr;           // eval chunk [R x D]
+    bf16_t *h = nullptr, *z = nullptr, *hd = nullptr, *dA = nullptr, *dA1 = nullptr, *dml = nullptr,
+           *dA3 = nullptr;
+    float *ml_slab = nullptr, *dz_slab = nullptr, *w_slab = nullptr;
+    float *cp3 = nullptr, *cp45 = nullptr, *cp1 = nullptr, *cp26 = nullptr, *lp = nullptr, *kl = nullptr;
+    float *mu = nullptr, *lv = nullptr, *eps = nullptr;
+    int ks_heads = 1, ks_dz = 1, ks_w1 = 1, ks_w45 = 1;
+    ShadowMap smap{};
+};
+
+}  // namespace bf
+}  // namespace vaeb

@@ -19,6 +19,7 @@
 #include "../../include/vaeb_hip.h"
 #include "hfuse.hpp"
 #include "latent.hpp"
+#include "step_bf16.hpp"
 
 using namespace vaeb;
 
@@ -55,17 +56,30 @@ int fail(int code, const char* fmt, ...) {
 inline int r16(int x) { return (x + 15) & ~15; }
 inline int cdiv(int64_t a, int64_t b) { return (int)((a + b - 1) / b); }
 
+template <class T>
+int dalloc(T** p, size_t n) {
+    if (n == 0) n = 1;
+    hipError_t e = hipMalloc((void**)p, n * sizeof(T));
+    if (e != hipSuccess) return fail(VAEB_ERR_NOMEM, "hipMalloc(%zu) failed: %s", n * sizeof(T), hipGetErrorString(e));
+    hipMemset(*p, 0, n * sizeof(T));
+    return 0;
+}
+
 // Control block layout (ints): [0] cursor, [1] resolved batch, [2..] batch order.
 constexpr int kOrderCap = 1 << 20;
 constexpr int kFvParts = 512;
 constexpr int kGraphSteps = 32;
-constexpr int kMaxProfKernels = 16;
+constexpr int kMaxProfKernels = 24;
 constexpr int kDbgWG = 1024;      // diagnostics: stamp slots per launch (workgroups)
 
 const char* kKernelNames[] = {"p1_enc", "p2_heads", "p3_dechid", "p4_decout", "p5_dhd_w2", "p6_dz",
                               "p7_dh", "p8_wgrad_w3w45", "allreduce", "adagrad", "fv_update", "elbo",
                               "p23_heads_dechid", "p67_dz_dh_w1", "p8_wgrad_w2", "p8_wgrad_w1",
-                              "p1_enc_latent", "p4_decout_z"};
+                              "p1_enc_latent", "p4_decout_z",
+                              // bf16 engine (step_bf16.hpp), ids 18..34
+                              "bf_enc", "bf_heads", "bf_latent", "bf_dechid", "bf_decout", "bf_dhd", "bf_dW26",
+                              "bf_dz", "bf_dW1", "bf_dW1_opt", "bf_latent_bwd", "bf_dh", "bf_dW45", "bf_dW45_opt",
+                              "bf_dW3", "bf_bias_elbo", "bf_adagrad_dp"};
 
 }  // namespace
 
@@ -120,6 +134,8 @@ struct vaeb_ctx {
     // diagnostics timeline (vaeb_debug_timeline)
     uint64_t* dbg = nullptr;
     int dbg_slot = 0;
+    // bf16 large-batch engine (step_bf16.hpp); off for dtype == VAEB_DTYPE_F32
+    bf::BfState bf;
 };
 
 namespace {
@@ -364,11 +380,14 @@ WGroup make_group(vaeb_ctx* c, const float* at, int ld_at, int klim, int at_is_x
     return G;
 }
 
+#include "engine_bf16.inc"
+
 // One training step reading parameter arena `par` and writing arena par ^ 1.
 // One stream: P1 -> P23 -> P4 -> [P5 | dW2 (| dW6)] -> [P67 | dW1] -> [dW3 | dW45 + ELBO]
 // (bracketed groups share one grid, see hfuse.hpp); DP adds all-reduce -> Adagrad.
 // `prof` brackets every launch with timing events.
 int enqueue_train_step(vaeb_ctx* c, int par, bool prof) {
+    if (is_bf16(c)) return bf_train_step(c, par, prof);
     Prof pr{c, prof};
     if (prof) pr.reps = c->prof_reps;
     const vaeb_config& g = c->c;
@@ -558,14 +577,6 @@ int check_batches(vaeb_ctx* c, const int32_t* idx, int n) {
     return 0;
 }
 
-template <class T>
-int dalloc(T** p, size_t n) {
-    if (n == 0) n = 1;
-    hipError_t e = hipMalloc((void**)p, n * sizeof(T));
-    if (e != hipSuccess) return fail(VAEB_ERR_NOMEM, "hipMalloc(%zu) failed: %s", n * sizeof(T), hipGetErrorString(e));
-    hipMemset(*p, 0, n * sizeof(T));
-    return 0;
-}
 
 }  // namespace
 
@@ -589,6 +600,15 @@ int vaeb_create(const vaeb_config* cfg, vaeb_ctx** out) {
         return fail(VAEB_ERR_ARG, "bad decoder/estimator/objective enum");
     if (g.estimator == VAEB_EST_FV && g.L != 1)
         return fail(VAEB_ERR_ARG, "the literal full-variational estimator supports L == 1 only (VAEB.py:361)");
+    if (g.dtype != VAEB_DTYPE_F32 && g.dtype != VAEB_DTYPE_BF16) return fail(VAEB_ERR_ARG, "bad dtype %d", g.dtype);
+    if (g.dtype == VAEB_DTYPE_BF16) {
+        if (g.D % 8 || g.H % 8 || g.Z % 8)
+            return fail(VAEB_ERR_ARG, "bf16 engine: D, H, Z must be multiples of 8 (got %d, %d, %d)", g.D, g.H, g.Z);
+        if (g.decoder == VAEB_DEC_GAUSSIAN && g.D % 32)
+            return fail(VAEB_ERR_ARG, "bf16 engine: the Gaussian decoder needs D %% 32 == 0 (got %d)", g.D);
+        if (g.estimator == VAEB_EST_FV) return fail(VAEB_ERR_ARG, "bf16 engine: the FV estimator runs on the fp32 path");
+        if (g.estimator == VAEB_EST_LA && g.L > 8) return fail(VAEB_ERR_ARG, "bf16 engine: LA supports L <= 8");
+    }
     auto* c = new vaeb_ctx();
     c->c = g;
     if (c->c.B_global <= 0) c->c.B_global = g.B;
@@ -649,6 +669,7 @@ int vaeb_create(const vaeb_config* cfg, vaeb_ctx** out) {
         rc = rc ? rc : dalloc(&c->cnt_ml, (size_t)(Bp / 16));
         rc = rc ? rc : dalloc(&c->cnt_dz, (size_t)(Bp / 16));
     }
+    if (!rc && is_bf16(c)) rc = bf_alloc(c);
     if (rc) { vaeb_destroy(c); return rc; }
     if (hipHostMalloc((void**)&c->h_ctl, sizeof(int) * (kOrderCap + 2), 0) != hipSuccess ||
         hipHostMalloc((void**)&c->h_elbo, sizeof(float) * 4, 0) != hipSuccess ||
@@ -668,6 +689,7 @@ int vaeb_destroy(vaeb_ctx* c) {
     if (!c) return 0;
     if (c->s) hipStreamSynchronize(c->s);
     free_graphs(c);
+    bf_free(c);
     if (c->comm) ncclCommDestroy(c->comm);
     float* fp[] = {c->theta2[0], c->theta2[1], c->acc, c->grad, c->fvmu, c->fvsg, c->fvam, c->fvas, c->fv_part, c->data, c->xeval,
                    c->elbo_out, c->eps_in, c->h, c->mu, c->lv, c->eps, c->z, c->hd, c->y, c->dA2, c->dA6, c->dA1,
@@ -701,6 +723,16 @@ int vaeb_set_data(vaeb_ctx* c, const float* x, int64_t n_rows) {
     if (c->data) { hipFree(c->data); c->data = nullptr; }
     free_graphs(c);  // graphs hold the data pointer
     c->graph_failed = false;
+    if (is_bf16(c)) {
+        // the bf16 engine keeps only a bf16 copy; c->data stays a 16-byte placeholder
+        if (c->bf.x) { hipFree(c->bf.x); c->bf.x = nullptr; }
+        if (int rc = dalloc(&c->bf.x, (size_t)n_rows * c->c.D)) return rc;
+        if (int rc = dalloc(&c->data, 4)) return rc;
+        if (int rc = bf_upload_rows(c, x, n_rows, c->bf.x)) return rc;
+        HIP_TRY(hipStreamSynchronize(c->s));
+        c->nrows = n_rows;
+        return 0;
+    }
     if (int rc = dalloc(&c->data, (size_t)n_rows * c->c.D)) return rc;
     HIP_TRY(hipMemcpy(c->data, x, sizeof(float) * (size_t)n_rows * c->c.D, hipMemcpyHostToDevice));
     c->nrows = n_rows;
@@ -717,7 +749,14 @@ static int xfer(vaeb_ctx* c, float* dev, const float* hin, float* hout, int64_t 
     return 0;
 }
 
-int vaeb_set_params(vaeb_ctx* c, const float* f, int64_t n) { return xfer(c, c ? c->theta2[c->par] : nullptr, f, nullptr, n, c ? c->P : 0); }
+int vaeb_set_params(vaeb_ctx* c, const float* f, int64_t n) {
+    if (int rc = xfer(c, c ? c->theta2[c->par] : nullptr, f, nullptr, n, c ? c->P : 0)) return rc;
+    if (is_bf16(c)) {
+        if (int rc = bf_make_shadow(c, c->par)) return rc;
+        HIP_TRY(hipStreamSynchronize(c->s));
+    }
+    return 0;
+}
 int vaeb_get_params(vaeb_ctx* c, float* f, int64_t n) { return xfer(c, c ? c->theta2[c->par] : nullptr, nullptr, f, n, c ? c->P : 0); }
 int vaeb_set_adagrad_state(vaeb_ctx* c, const float* f, int64_t n) { return xfer(c, c ? c->acc : nullptr, f, nullptr, n, c ? c->P : 0); }
 int vaeb_get_adagrad_state(vaeb_ctx* c, float* f, int64_t n) { return xfer(c, c ? c->acc : nullptr, nullptr, f, n, c ? c->P : 0); }
@@ -837,6 +876,11 @@ static int eval_rows(vaeb_ctx* c, const float* x, int64_t n, int mode, float* ou
     HIP_TRY(hipMemsetAsync(c->eval_acc, 0, 2 * sizeof(double), c->s));
     for (int64_t r0 = 0; r0 < n; r0 += chunk) {
         const int rows = (int)std::min<int64_t>(chunk, n - r0);
+        if (is_bf16(c)) {
+            if (int rc = bf_eval_chunk(c, x + r0 * g.D, rows, r0, mode, out_y ? out_y + r0 * g.D : nullptr)) return rc;
+            HIP_TRY(hipStreamSynchronize(c->s));
+            continue;
+        }
         HIP_TRY(hipMemcpyAsync(c->xeval, x + r0 * g.D, sizeof(float) * (size_t)rows * g.D, hipMemcpyHostToDevice, c->s));
         StepArgs a = make_args(c, c->par, rows, mode, c->xeval, false);
         a.row_base_add = r0;
@@ -983,6 +1027,49 @@ int vaeb_debug_timeline(vaeb_ctx* c, int32_t batch_index, uint64_t* out, int64_t
     hipFree(d);
     if (out_launches) *out_launches = launches;
     return 0;
+}
+
+int vaeb_test_gemm_bf16(vaeb_ctx* c, int32_t ako, int32_t bko, int32_t M, int32_t N, int32_t K, const float* A,
+                        const float* B, float* C, int32_t ksplit) {
+    if (!c || !A || !B || !C || M <= 0 || N <= 0 || K <= 0 || ksplit <= 0) return fail(VAEB_ERR_ARG, "bad arguments");
+    if (K % 8 || (ako && M % 8) || (bko && N % 8))
+        return fail(VAEB_ERR_ARG, "bf16 GEMM: K (and a K-outer operand's rows) must be multiples of 8");
+    const size_t na = (size_t)M * K, nb = (size_t)N * K;
+    const int nz = bf_slices(K, ksplit);
+    float *fa = nullptr, *fb = nullptr, *fc = nullptr;
+    bf16_t *ba = nullptr, *bb = nullptr;
+    int rc = 0;
+    rc = rc ? rc : dalloc(&fa, na);
+    rc = rc ? rc : dalloc(&fb, nb);
+    rc = rc ? rc : dalloc(&ba, na);
+    rc = rc ? rc : dalloc(&bb, nb);
+    rc = rc ? rc : dalloc(&fc, (size_t)nz * M * N);
+    if (!rc) {
+        hipMemcpy(fa, A, na * 4, hipMemcpyHostToDevice);
+        hipMemcpy(fb, B, nb * 4, hipMemcpyHostToDevice);
+        hipLaunchKernelGGL(bf::to_bf16_kernel, dim3(256), dim3(256), 0, c->s, fa, ba, (int64_t)na);
+        hipLaunchKernelGGL(bf::to_bf16_kernel, dim3(256), dim3(256), 0, c->s, fb, bb, (int64_t)nb);
+        const bf::EpiF32 e{fc, N, M, N, (int64_t)M * N};
+        const int lda = ako ? M : K, ldb = bko ? N : K;
+        const int64_t ab = (int64_t)na * 2, bbytes = (int64_t)nb * 2;
+        if (!ako && !bko) rc = bf_gemm<bf::KC, bf::KC>(c->s, ba, lda, ab, bb, ldb, bbytes, M, N, K, ksplit, e);
+        else if (!ako && bko) rc = bf_gemm<bf::KC, bf::KO>(c->s, ba, lda, ab, bb, ldb, bbytes, M, N, K, ksplit, e);
+        else if (ako && !bko) rc = bf_gemm<bf::KO, bf::KC>(c->s, ba, lda, ab, bb, ldb, bbytes, M, N, K, ksplit, e);
+        else rc = bf_gemm<bf::KO, bf::KO>(c->s, ba, lda, ab, bb, ldb, bbytes, M, N, K, ksplit, e);
+    }
+    if (!rc) {
+        std::vector<float> slabs((size_t)nz * M * N);
+        hipError_t e = hipStreamSynchronize(c->s);
+        if (e == hipSuccess) e = hipMemcpy(slabs.data(), fc, slabs.size() * 4, hipMemcpyDeviceToHost);
+        if (e != hipSuccess) rc = fail(VAEB_ERR_HIP, "test gemm: %s", hipGetErrorString(e));
+        for (size_t i = 0; !rc && i < (size_t)M * N; ++i) {
+            float v = 0.f;
+            for (int z = 0; z < nz; ++z) v += slabs[(size_t)z * M * N + i];
+            C[i] = v;
+        }
+    }
+    for (void* p : {(void*)fa, (void*)fb, (void*)fc, (void*)ba, (void*)bb}) if (p) hipFree(p);
+    return rc;
 }
 
 int vaeb_kernel_name(int32_t id, char* out, int32_t cap) {
