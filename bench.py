@@ -1,13 +1,18 @@
 #!/usr/bin/env python3
 """Benchmark: SGVB training images/sec + ELBO at MNIST 784-500-20, batch 100 per GPU.
 
-A "step" is one VAEB.update (/root/reference/VAEB.py:408-415) on one minibatch of 100
-synthetic MNIST-shaped rows: encoder -> reparameterised sample -> decoder -> ELBO + KL ->
-gradient -> Adagrad, all on the GPU (libvaeb_hip.so); the training set is resident in
-HBM before timing starts.  With N GPUs every rank processes its own 100 rows of a
-100*N-row global minibatch and the gradients are all-reduced over RCCL ("weak" scaling).
+A "step" is one VAEB.update (/root/reference/VAEB.py:408-415) on one minibatch of
+synthetic rows: encoder -> reparameterised sample -> decoder -> ELBO + KL -> gradient ->
+Adagrad, all on the GPU (libvaeb_hip.so); the training set is resident in HBM before
+timing starts.  With N GPUs every rank processes its own B rows of a B*N-row global
+minibatch and the gradients are all-reduced over RCCL ("weak" scaling).
 
-Usage:  python bench.py [--gpus N] [--steps K] [--warmup W]
+Configs (BASELINE.json):
+  --config mnist (default, the headline metric): 784-500-20 Bernoulli, B=100, fp32 MFMA
+  --config synth (config 5, roofline stress): 4096-2048-128 Bernoulli, B=8192 per GPU,
+                 bf16 MFMA operands / fp32 accumulation and master weights
+
+Usage:  python bench.py [--gpus N] [--steps K] [--warmup W] [--config mnist|synth]
         (N > 1: torch.distributed.run, one process per GPU)
 Prints ONE JSON line on rank 0.
 """
@@ -24,7 +29,8 @@ sys.path.insert(0, ROOT)
 
 import numpy as np  # noqa: E402
 
-PEAK_F32_TFLOPS = 157.3   # MI355X f32 MFMA / vector peak (MI355X_MICROARCH.md)
+PEAK_F32_TFLOPS = 157.3    # MI355X f32 MFMA / vector peak (MI355X_MICROARCH.md)
+PEAK_BF16_TFLOPS = 2500.0  # MI355X dense bf16 MFMA peak (no sparsity)
 PEAK_HBM_GBS = 8000.0
 
 
@@ -49,20 +55,45 @@ def phase_flops(D, H, Z, B, L=1, gaussian=False):
         # folded latent block (latent.hpp): encoder GEMM + heads; hd recompute + decoder GEMM
         "p1_enc_latent": 2 * B * D * H + 2 * B * H * 2 * Z,
         "p4_decout_z": 2 * L * B * Z * H + 2 * L * B * H * D * g,
+        # bf16 engine (step_bf16.hpp)
+        "bf_enc": 2 * B * D * H,
+        "bf_heads": 2 * B * H * 2 * Z,
+        "bf_dechid": 2 * L * B * Z * H,
+        "bf_decout": 2 * L * B * H * D * g,
+        "bf_dhd": 2 * L * B * D * g * H,
+        "bf_dW26": 2 * L * B * H * D * g,
+        "bf_dz": 2 * L * B * H * Z,
+        "bf_dW1": 2 * L * B * Z * H,
+        "bf_dh": 2 * B * 2 * Z * H,
+        "bf_dW45": 2 * B * H * 2 * Z,
+        "bf_dW3": 2 * B * D * H,
     }
+
+
+def step_flops(D, H, Z, B, L=1, gaussian=False):
+    """2B(2DH + 9HZ + 3HD) (Bernoulli, L=1)."""
+    g = 2 if gaussian else 1
+    return 2 * B * (D * H + 2 * H * Z) + 2 * L * B * (Z * H + g * H * D) + \
+        2 * L * B * (g * D * H + H * Z + Z * H + g * H * D) + 2 * B * (2 * Z * H + H * 2 * Z + D * H)
 
 
 KERNEL_SYMBOLS = {"p1_enc": "PEnc", "p23_heads_dechid": "heads_dechid_kernel", "p4_decout": "PDecOut",
                   "p5_dhd_w2": "vaeb::tile_wgrad_kernel", "p67_dz_dh_w1": "vaeb::dz_dh_wgrad_kernel",
                   "p8_wgrad_w3w45": "vaeb::wgrad_kernel", "p1_enc_latent": "vaeb::enc_latent_kernel",
-                  "p4_decout_z": "vaeb::decout_z_kernel"}
-PMC_FILE = os.path.join(ROOT, "profiles", "r1", "pmc_per_launch.json")
+                  "p4_decout_z": "vaeb::decout_z_kernel",
+                  # bf16 GEMMs are one template: the epilogue / layout pair names the launch
+                  "bf_enc": "gemm_kernel<0, 1, vaeb::bf::EpiBiasAct>", "bf_decout": "EpiDecOut<false>",
+                  "bf_dhd": "gemm_kernel<0, 0, vaeb::bf::EpiDTanh>", "bf_dW26": "EpiAdagrad",
+                  "bf_dW3": "EpiAdagrad"}
+PMC_FILES = {"mnist": os.path.join(ROOT, "profiles", "r1", "pmc_per_launch.json"),
+             "synth": os.path.join(ROOT, "profiles", "r1", "pmc_synth_per_launch.json")}
 
 
-def committed_traffic(kernel, path=PMC_FILE, symbols=KERNEL_SYMBOLS):
+def committed_traffic(kernel, path=PMC_FILES["mnist"], symbols=KERNEL_SYMBOLS):
     """HBM bytes per launch of `kernel` from the rocprofv3 PMC passes committed under
     profiles/ (separate FETCH_SIZE / WRITE_SIZE passes folded by scripts/pmc_summary.py,
-    FETCH_SIZE doubled per MI355X_MICROARCH.md §HBM)."""
+    FETCH_SIZE doubled per MI355X_MICROARCH.md §HBM).  Kernels whose symbol
+    is shared by several launches of a step report the per-launch average of all of them."""
     try:
         data = json.load(open(path))
     except Exception:
@@ -74,7 +105,7 @@ def committed_traffic(kernel, path=PMC_FILE, symbols=KERNEL_SYMBOLS):
     return None
 
 
-def cpu_baseline(D, H, Z, B, x, budget_s=10.0):
+def cpu_baseline(D, H, Z, B, x, budget_s=10.0, max_steps=20000):
     """The oracle's float32 NumPy restatement of the same step, on the host cores."""
     from oracle import vaeb_oracle as O
     try:
@@ -89,7 +120,7 @@ def cpu_baseline(D, H, Z, B, x, budget_s=10.0):
     nb = x.shape[0] // B
     ctx = threadpool_limits(limits=threads) if threadpool_limits else None
     try:
-        for i in range(3):  # warm-up
+        for i in range(min(3, max_steps)):  # warm-up
             eps = rng.standard_normal((1, B, Z)).astype(np.float32)
             _, params, acc, _ = O.step(params, acc, x[i * B:(i + 1) * B], eps, cfg)
         n = 0
@@ -100,25 +131,40 @@ def cpu_baseline(D, H, Z, B, x, budget_s=10.0):
             _, params, acc, _ = O.step(params, acc, x[b * B:(b + 1) * B], eps, cfg)
             n += 1
             dt = time.perf_counter() - t0
-            if dt >= budget_s or n >= 20000:
+            if dt >= budget_s or n >= max_steps:
                 break
     finally:
         if ctx is not None:
             ctx.unregister() if hasattr(ctx, "unregister") else None
     return {"value": n * B / dt, "unit": "images/s", "cores": threads, "kind": "port",
-            "sample": f"{n} float32 NumPy oracle steps (784-500-20, B={B}) in {dt:.1f} s, OpenBLAS {threads} threads"}
+            "sample": f"{n} float32 NumPy oracle steps ({D}-{H}-{Z}, B={B}) in {dt:.1f} s, OpenBLAS {threads} threads"}
+
+
+CONFIGS = {
+    "mnist": dict(D=784, H=500, Z=20, B=100, N=50000, dtype="f32", steps=2000, warmup=200,
+                  metric="SGVB training images/sec + ELBO at MNIST 784-500-20, batch 100",
+                  workload="MNIST 784-500-20 Bernoulli decoder, LB estimator, L=1, Adagrad lr 0.01"),
+    "synth": dict(D=4096, H=2048, Z=128, B=8192, N=16 * 8192, dtype="bf16", steps=50, warmup=5,
+                  metric="SGVB training images/sec, synthetic 4096-2048-128, batch 8192 per GPU, bf16 MFMA",
+                  workload="synthetic 4096-2048-128 Bernoulli decoder, LB, L=1, Adagrad lr 0.01, bf16 operands / "
+                           "fp32 accumulate + fp32 master weights (BASELINE config 5)"),
+}
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=2000)
-    ap.add_argument("--warmup", type=int, default=200)
-    ap.add_argument("--batch", type=int, default=100)
+    ap.add_argument("--config", choices=sorted(CONFIGS), default="mnist")
+    ap.add_argument("--steps", type=int, default=None)
+    ap.add_argument("--warmup", type=int, default=None)
+    ap.add_argument("--batch", type=int, default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=10.0)
     args = ap.parse_args()
+    C = CONFIGS[args.config]
+    steps = args.steps if args.steps is not None else C["steps"]
+    warmup = args.warmup if args.warmup is not None else C["warmup"]
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -133,13 +179,20 @@ def main():
     from oracle import vaeb_oracle as O  # synthetic data generator + initial theta (not the compute path)
     from vaeb_amd import _lib
 
-    D, H, Z, B = 784, 500, 20, args.batch
+    D, H, Z = C["D"], C["H"], C["Z"]
+    B = args.batch if args.batch is not None else C["B"]
     Bg = B * world
-    N = 50000
-    x = O.synthetic_mnist(n=N, D=D)
+    N = max(C["N"], 4 * Bg)
+    bf16 = C["dtype"] == "bf16"
+    if bf16:
+        rng = np.random.default_rng(3)   # synth x ~ Bernoulli(0.5)
+        x = (rng.random((N, D), dtype=np.float32) < 0.5).astype(np.float32)
+    else:
+        x = O.synthetic_mnist(n=N, D=D)
     cfg = O.Config(D=D, H=H, Z=Z)
     ctx = _lib.Context(D, H, Z, B, B_global=Bg, row_offset=rank * B, device=local,
-                       use_graph=not args.no_graph, max_eval_rows=1000)
+                       use_graph=not args.no_graph, max_eval_rows=B if bf16 else 1000,
+                       dtype=_lib.DTYPE_BF16 if bf16 else _lib.DTYPE_F32)
     if world > 1:
         uid = [_lib.Context.comm_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
@@ -158,10 +211,10 @@ def main():
             out.extend(o.tolist())
         return np.array(out[:n], np.int32)
 
-    ctx.update_many(order(args.warmup))
+    ctx.update_many(order(warmup))
     ctx.synchronize()
     ctx.epoch_elbo()
-    timed_order = order(args.steps)
+    timed_order = order(steps)
     if dist:
         dist.barrier()
     ctx.synchronize()
@@ -180,35 +233,42 @@ def main():
     elbo_sum, nsteps = ctx.epoch_elbo()
 
     # per-kernel device time (HIP events on the context's stream), after the timed region
-    prof = ctx.profile_steps(50)
+    prof = ctx.profile_steps(50 if not bf16 else 5)
     fl = phase_flops(D, H, Z, B)
     dom = max((k for k in prof if k[0] in fl), key=lambda k: k[1])
     achieved = fl[dom[0]] / (dom[1] * 1e-3) / 1e12
-    traffic = committed_traffic(dom[0])
+    traffic = committed_traffic(dom[0], PMC_FILES[args.config])
+    peak = PEAK_BF16_TFLOPS if bf16 else PEAK_F32_TFLOPS
+    sflops = step_flops(D, H, Z, B)
 
     res = {
-        "metric": "SGVB training images/sec + ELBO at MNIST 784-500-20, batch 100",
-        "value": world * B * args.steps / el,
+        "metric": C["metric"],
+        "value": world * B * steps / el,
         "unit": "images/s",
         "n_gpus": world,
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "ms_per_step": el / args.steps * 1e3,
+        "steps": steps,
+        "warmup": warmup,
+        "ms_per_step": el / steps * 1e3,
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "f32",
-        "data": f"synthetic MNIST-shaped binary pixels (N={N}, D={D}), resident in HBM; random init RandomState(10)",
-        "config": {"workload": "MNIST 784-500-20 Bernoulli decoder, LB estimator, L=1, Adagrad lr 0.01",
-                   "global_batch": Bg, "batch_per_gpu": B, "seq_len": None, "parallelism": f"dp{world}"},
+        "dtype": C["dtype"],
+        "data": (f"synthetic {'Bernoulli(0.5)' if bf16 else 'MNIST-shaped binary'} pixels (N={N}, D={D}), "
+                 f"resident in HBM; random init RandomState(10)"),
+        "config": {"workload": C["workload"], "global_batch": Bg, "batch_per_gpu": B, "seq_len": None,
+                   "parallelism": f"dp{world}"},
         "elbo": elbo_sum / max(nsteps, 1),
+        "step_tflops": sflops / (el / steps) / 1e12,
         "kernels_ms": {k: round(v, 5) for k, v in prof},
-        "roofline": {"bound": "mfma", "kernel": dom[0], "achieved": achieved, "peak": PEAK_F32_TFLOPS,
-                     "unit": "TFLOP/s", "frac": achieved / PEAK_F32_TFLOPS, "traffic": traffic,
+        "roofline": {"bound": "mfma", "kernel": dom[0], "achieved": achieved, "peak": peak,
+                     "unit": "TFLOP/s", "frac": achieved / peak, "traffic": traffic,
                      "flops_per_launch": fl[dom[0]], "avg_launch_ms": dom[1]},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        res["cpu_baseline"] = cpu_baseline(D, H, Z, B, x, budget_s=args.cpu_budget)
+        if bf16:
+            res["cpu_baseline"] = cpu_baseline(D, H, Z, B, x[:4 * B], budget_s=args.cpu_budget * 2, max_steps=8)
+        else:
+            res["cpu_baseline"] = cpu_baseline(D, H, Z, B, x, budget_s=args.cpu_budget)
     if rank == 0:
         print(json.dumps(res), flush=True)
     ctx.close()

@@ -213,7 +213,19 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_kernel(GemmArgs g, Epi e) {
         }
         __syncthreads();
     }
-    e(m0 + wm * 64, n0 + wn * 64, acc, kz);
+    // Epilogue.  The LDS is free again (the loop ended on a barrier): epilogues with a
+    // bf16 input tile (x, h, hd at the output positions) fetch it with coalesced 16-B
+    // loads into a padded LDS tile; bf16 results go back through the same tile and
+    // leave with 16-B stores.
+    if constexpr (Epi::kIn) {
+        e.load_in(m0, n0, smem);
+        __syncthreads();
+    }
+    e(m0 + wm * 64, n0 + wn * 64, acc, kz, smem);
+    if constexpr (Epi::kOut) {
+        __syncthreads();
+        e.store_out(m0, n0, smem);
+    }
 }
 
 // ------------------------------------------------------------------ helpers
@@ -230,11 +242,62 @@ DEV float colsum_lanes(float s) {
     return s;
 }
 
+// ------------------------------------------------------------------ epilogue tiles
+// A 128 x 128 bf16 tile in LDS with a 288-B row pitch: the four 16-lane groups of a
+// per-element access (rows 4(l>>4)+r, 16 consecutive columns) land on disjoint banks.
+constexpr int kEP = 288;
+constexpr int kEpiTileBytes = BM * kEP;   // 36 KiB
+DEV int eoff(int row, int col) { return row * kEP + col * 2; }
+DEV float lds_bf(const char* t, int row, int col) {
+    return bf2f(*reinterpret_cast<const uint16_t*>(t + eoff(row, col)));
+}
+DEV void lds_st_bf(char* t, int row, int col, float v) {
+    *reinterpret_cast<uint16_t*>(t + eoff(row, col)) = (uint16_t)f2bf(v);
+}
+// Cooperative tile copies: rows [0, 128) x columns [0, W) of the tile at (r0, c0) of a
+// [rows x ld] bf16 matrix; rows >= rlim or columns >= clim read 0 / are not stored
+// (clim % 8 == 0).  rmod > 0: source row = (r0 + row) % rmod (the L noise planes share
+// the data rows).  GI: source column c goes to tile column (c & 31) + 64 (c >> 5) -- the
+// W2 slots of the Gaussian decoder's 32-column interleave.
+template <int W, bool GI = false>
+DEV void tile_load(char* t, rsrc_t src, int ld, int r0, int c0, int rlim, int clim, int rmod) {
+    constexpr int CPR = W / 8;                 // 16-B chunks per row
+    constexpr int N = BM * CPR / NTHR;
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+        const int id = threadIdx.x + NTHR * i;
+        const int row = id / CPR, ch = id % CPR;
+        const int gr = r0 + row, gc = c0 + ch * 8;
+        const int sr = rmod > 0 ? gr % rmod : gr;
+        const uint32_t off = (gr < rlim && gc < clim) ? ((uint32_t)sr * (uint32_t)ld + (uint32_t)gc) * 2u : kOOB;
+        const v4u v = __builtin_bit_cast(v4u, __builtin_amdgcn_raw_buffer_load_b128(src, off, 0, 0));
+        const int tc = GI ? ((ch * 8) & 31) + ((ch * 8) >> 5) * 64 : ch * 8;
+        *reinterpret_cast<v4u*>(t + row * kEP + tc * 2) = v;
+    }
+}
+template <int W>
+DEV void tile_store(const char* t, bf16_t* dst, int ld, int r0, int c0, int rlim, int clim) {
+    constexpr int CPR = W / 8;
+    constexpr int N = BM * CPR / NTHR;
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+        const int id = threadIdx.x + NTHR * i;
+        const int row = id / CPR, ch = id % CPR;
+        const int gr = r0 + row, gc = c0 + ch * 8;
+        if (gr < rlim && gc < clim)
+            *reinterpret_cast<v4u*>(dst + (int64_t)gr * ld + gc) = *reinterpret_cast<const v4u*>(t + row * kEP + ch * 16);
+    }
+}
+
 // ------------------------------------------------------------------ epilogues
+// Interface: static constexpr bool kIn, kOut;  void load_in(m0, n0, smem) (kIn);
+// void operator()(mw, nw, acc, kz, smem);  void store_out(m0, n0, smem) (kOut).
+// Wave (wm, wn)'s block starts at tile-local (64 wm, 64 wn).
 // Plain fp32 store (split-K slabs: slice kz at out + kz * slab).
 struct EpiF32 {
+    static constexpr bool kIn = false, kOut = false;
     float* out; int ldo; int M, N; int64_t slab;
-    DEV void operator()(int mw, int nw, f32x4 (&acc)[4][4], int kz) const {
+    DEV void operator()(int mw, int nw, f32x4 (&acc)[4][4], int kz, char*) const {
         const int lane = threadIdx.x & 63;
         float* o = out + (int64_t)kz * slab;
 #pragma unroll
@@ -249,60 +312,65 @@ struct EpiF32 {
     }
 };
 
-// v = act(acc + bias[col]) stored as bf16 (and optionally fp32).
+// v = act(acc + bias[col]) stored as bf16 (via the LDS tile, 16-B stores).
 struct EpiBiasAct {
+    static constexpr bool kIn = false, kOut = true;
     const float* bias; int tanh_act; int M, N;
     bf16_t* out; int ldo;
-    DEV void operator()(int mw, int nw, f32x4 (&acc)[4][4], int) const {
+    DEV void operator()(int mw, int nw, f32x4 (&acc)[4][4], int, char* smem) const {
         const int lane = threadIdx.x & 63;
+        const int lr0 = mw & (BM - 1), lc0 = nw & (BN - 1);
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             const int col = ecol(nw, j, lane);
-            if (col >= N) continue;
-            const float b = bias[col];
+            const float b = col < N ? bias[col] : 0.f;
 #pragma unroll
             for (int i = 0; i < 4; ++i)
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
-                    const int row = erow(mw, i, r, lane);
                     float v = acc[i][j][r] + b;
                     if (tanh_act) v = ftanh(v);
-                    if (row < M) out[(int64_t)row * ldo + col] = (bf16_t)f2bf(v);
+                    lds_st_bf(smem, erow(lr0, i, r, lane), ecol(lc0, j, lane), v);
                 }
         }
     }
+    DEV void store_out(int m0, int n0, char* smem) const { tile_store<BN>(smem, out, ldo, m0, n0, M, N); }
 };
 
 // Backward through tanh: out = acc * (1 - t^2) with t the stored bf16 activation at the
-// same (row, col); column sums of out (fp32, before rounding) -> colpart[mw/64][col]
-// (the bias gradient, reduced in fixed order by the optimizer).
+// same (row, col), staged through the LDS tile and overwritten there by the result;
+// column sums of out (fp32, before rounding) -> colpart[mw/64][col] (the bias gradient,
+// reduced in fixed order by the optimizer).
 struct EpiDTanh {
+    static constexpr bool kIn = true, kOut = true;
     const bf16_t* t; int ldt; int M, N;
     bf16_t* out; int ldo;
     float* colpart;
-    DEV void operator()(int mw, int nw, f32x4 (&acc)[4][4], int) const {
+    DEV void load_in(int m0, int n0, char* smem) const {
+        tile_load<BN>(smem, mkbuf(t, (int64_t)M * ldt * 2), ldt, m0, n0, M, N, 0);
+    }
+    DEV void operator()(int mw, int nw, f32x4 (&acc)[4][4], int, char* smem) const {
         const int lane = threadIdx.x & 63;
+        const int lr0 = mw & (BM - 1), lc0 = nw & (BN - 1);
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             const int col = ecol(nw, j, lane);
-            const bool cok = col < N;
             float cs = 0.f;
 #pragma unroll
             for (int i = 0; i < 4; ++i)
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
-                    const int row = erow(mw, i, r, lane);
-                    if (cok && row < M) {
-                        const float tv = bf2f(t[(int64_t)row * ldt + col]);
-                        const float v = acc[i][j][r] * (1.f - tv * tv);
-                        out[(int64_t)row * ldo + col] = (bf16_t)f2bf(v);
-                        cs += v;
-                    }
+                    const int lr = erow(lr0, i, r, lane), lc = ecol(lc0, j, lane);
+                    const float tv = lds_bf(smem, lr, lc);
+                    const float v = acc[i][j][r] * (1.f - tv * tv);
+                    lds_st_bf(smem, lr, lc, v);
+                    cs += (erow(mw, i, r, lane) < M) ? v : 0.f;
                 }
             cs = colsum_lanes(cs);
-            if (lane < 16 && cok) colpart[(int64_t)(mw >> 6) * N + col] = cs;
+            if (lane < 16 && col < N) colpart[(int64_t)(mw >> 6) * N + col] = cs;
         }
     }
+    DEV void store_out(int m0, int n0, char* smem) const { tile_store<BN>(smem, out, ldo, m0, n0, M, N); }
 };
 
 // Decoder output (VAEB.py:257-263, 302-313) on the [M_e x Dn] block of a2 (| a6):
@@ -311,10 +379,13 @@ struct EpiDTanh {
 //             wave's tiles j and j + 2 hold a2 and a6 of the same 32 data columns:
 //             y = sigmoid(a2), r = x - y, log p += -1/2 log 2pi - a6/2 - r^2 e^-a6 / 2,
 //             dA2 = sl r e^-a6 y (1 - y), dA6 = sl (-1/2 + r^2 e^-a6 / 2).
-// Per-row log p partials -> lp[row * nlp + nw/64]; bias-gradient column sums of dA ->
+// The x tile (the block's data columns) is staged in the LDS output tile at the dA2
+// positions and overwritten there by dA2 (| dA6) by the lane that read it.  Per-row log p
+// partials -> lp[row * nlp + nw/64]; bias-gradient column sums of dA ->
 // colpart[mw/64][col]; y (decoder mean, reconstruction) when yout != nullptr.
 template <bool GAUSS>
 struct EpiDecOut {
+    static constexpr bool kIn = true, kOut = true;
     const float *b2, *b6;
     const bf16_t* x; int ldx; int Mx;   // data row of output row m is m % Mx
     int M, N, D;                        // N = Dn (D or 2D)
@@ -325,10 +396,14 @@ struct EpiDecOut {
     float* lp; int nlp;
     float* colpart;
     float* yout;
-    DEV void operator()(int mw, int nw, f32x4 (&acc)[4][4], int) const {
+    DEV void load_in(int m0, int n0, char* smem) const {
+        const rsrc_t src = mkbuf(x + xb.offset(), (int64_t)Mx * ldx * 2);
+        if constexpr (GAUSS) tile_load<BN / 2, true>(smem, src, ldx, m0, n0 / 2, M, D, Mx);
+        else tile_load<BN>(smem, src, ldx, m0, n0, M, D, Mx);
+    }
+    DEV void operator()(int mw, int nw, f32x4 (&acc)[4][4], int, char* smem) const {
         const int lane = threadIdx.x & 63;
-        if (nw >= N) return;
-        const bf16_t* xr = x + xb.offset();
+        const int lr0 = mw & (BM - 1), lc0 = nw & (BN - 1);
         float rs[4][4];
 #pragma unroll
         for (int i = 0; i < 4; ++i)
@@ -347,9 +422,9 @@ struct EpiDecOut {
             for (int i = 0; i < 4; ++i)
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
-                    const int row = erow(mw, i, r, lane);
-                    if (!(cok && row < M)) continue;
-                    const float xv = bf2f(xr[(int64_t)(row % Mx) * ldx + d]);
+                    const int row = erow(mw, i, r, lane), lr = erow(lr0, i, r, lane);
+                    const bool ok = cok && row < M;
+                    const float xv = lds_bf(smem, lr, ecol(lc0, j, lane));
                     const float a2 = acc[i][j][r] + bb2;
                     const float y = sigmoidf(a2);
                     float lpv, g2, g6 = 0.f;
@@ -363,14 +438,14 @@ struct EpiDecOut {
                         g2 = sl * rr * e6 * y * (1.f - y);
                         g6 = sl * (-0.5f + 0.5f * rr * rr * e6);
                     }
-                    rs[i][r] += lpv;
-                    if (yout) yout[(int64_t)row * D + d] = y;
+                    rs[i][r] += ok ? lpv : 0.f;
+                    if (yout && ok) yout[(int64_t)row * D + d] = y;
                     if (train) {
-                        dA[(int64_t)row * ldd + col] = (bf16_t)f2bf(g2);
-                        cs2 += g2;
+                        lds_st_bf(smem, lr, ecol(lc0, j, lane), g2);
+                        cs2 += ok ? g2 : 0.f;
                         if constexpr (GAUSS) {
-                            dA[(int64_t)row * ldd + col + 32] = (bf16_t)f2bf(g6);
-                            cs6 += g6;
+                            lds_st_bf(smem, lr, ecol(lc0, j, lane) + 32, g6);
+                            cs6 += ok ? g6 : 0.f;
                         }
                     }
                 }
@@ -383,14 +458,19 @@ struct EpiDecOut {
                 }
             }
         }
+        if (nw < N) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
+            for (int i = 0; i < 4; ++i)
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const float s = sum16(rs[i][r]);
-                const int row = erow(mw, i, r, lane);
-                if ((lane & 15) == 0 && row < M) lp[(int64_t)row * nlp + (nw >> 6)] = s;
-            }
+                for (int r = 0; r < 4; ++r) {
+                    const float s = sum16(rs[i][r]);
+                    const int row = erow(mw, i, r, lane);
+                    if ((lane & 15) == 0 && row < M) lp[(int64_t)row * nlp + (nw >> 6)] = s;
+                }
+        }
+    }
+    DEV void store_out(int m0, int n0, char* smem) const {
+        if (train) tile_store<BN>(smem, dA, ldd, m0, n0, M, N);
     }
 };
 
@@ -431,8 +511,9 @@ struct Opt {
 };
 
 struct EpiAdagrad {
+    static constexpr bool kIn = false, kOut = false;
     ColMap map; Opt opt; int M, N;
-    DEV void operator()(int mw, int nw, f32x4 (&acc)[4][4], int) const {
+    DEV void operator()(int mw, int nw, f32x4 (&acc)[4][4], int, char*) const {
         const int lane = threadIdx.x & 63;
 #pragma unroll
         for (int i = 0; i < 4; ++i)

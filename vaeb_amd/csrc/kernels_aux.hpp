@@ -36,6 +36,8 @@ DEV double block_sum256(double v, double* sh) {
     return r;
 }
 
+DEV void elbo_emit(const ElboArgs& e, double lp, double kl, double fv);
+
 // Deterministic (fixed-order) reduction by one 256-thread workgroup.
 DEV void elbo_reduce(const ElboArgs& e, double* sh) {
     double lp = 0, kl = 0, fv = 0;
@@ -46,6 +48,11 @@ DEV void elbo_reduce(const ElboArgs& e, double* sh) {
     kl = block_sum256(kl, sh);
     fv = block_sum256(fv, sh);
     if (threadIdx.x != 0) return;
+    elbo_emit(e, lp, kl, fv);
+}
+
+// The step's scalar outputs from the reduced sums (thread 0 of the reducing workgroup).
+DEV void elbo_emit(const ElboArgs& e, double lp, double kl, double fv) {
     // LB: sum logp / L + sum KL (VAEB.py:339-344); LA: (sum logp + sum(prior-logQ)) / L
     // (VAEB.py:327-328); FV: B * (sum logp + sum KL) + thetaPrior (VAEB.py:364).
     const double data = (e.est == EST_LA) ? (lp + kl) / e.L : lp / e.L + kl;

@@ -134,19 +134,24 @@ __global__ __launch_bounds__(256) void latent_fwd_kernel(LatentArgs a) {
 
 // [dMu | dLv] from the dZ slabs (LA direct terms folded as in the
 // fp32 path), stored bf16 for the dh / dW45 GEMMs; column sums per 64-row block for the
-// b4 / b5 gradients.  Block = 64 rows x (256 / 64 = 4) column groups; grid.x row blocks.
+// b4 / b5 gradients.  Grid (row blocks of 64, column blocks of 64); a wave owns 64
+// consecutive columns of [dMu | dLv] (coalesced along the latent index) and every 4th
+// row of the block; the 4 waves' column sums are combined in fixed order.
 __global__ __launch_bounds__(256) void latent_bwd_kernel(LatentArgs a) {
+    __shared__ float red[4][64];
     const int Z = a.Z, Z2 = 2 * Z;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int c = blockIdx.y * 64 + lane;
     const int m0 = blockIdx.x * 64;
-    const int LM = a.L * a.M;
+    const int m1 = min(a.M, m0 + 64);
+    const int64_t LMZ = (int64_t)a.L * a.M * Z;
     const float sl = a.sc / (float)a.L;
-    for (int c = threadIdx.x >> 6; c < Z2; c += 4) {
-        // each wave: column c of [dMu | dLv] over the block's 64 rows (lane = row)
-        const int m = m0 + (threadIdx.x & 63);
-        const bool isv = c >= Z;
-        const int j = isv ? c - Z : c;
-        float v = 0.f;
-        if (m < a.M) {
+    const bool isv = c >= Z;
+    const int j = isv ? c - Z : c;
+    float cs = 0.f;
+    if (c < Z2) {
+#pragma unroll 4
+        for (int m = m0 + w; m < m1; m += 4) {
             const int64_t o = (int64_t)m * Z + j;
             const float mu = a.mu[o], lv = a.lv[o];
             const float sd = fexp(0.5f * lv);
@@ -154,7 +159,7 @@ __global__ __launch_bounds__(256) void latent_bwd_kernel(LatentArgs a) {
             for (int l = 0; l < a.L; ++l) {
                 const int64_t ol = ((int64_t)l * a.M + m) * Z + j;
                 float dz = 0.f;
-                for (int s = 0; s < a.ndz; ++s) dz += a.dz_slab[(int64_t)s * LM * Z + ol];
+                for (int s = 0; s < a.ndz; ++s) dz += a.dz_slab[(int64_t)s * LMZ + ol];
                 const float e = a.eps[ol];
                 const float z = mu + sd * e;
                 if (!isv) {
@@ -165,15 +170,17 @@ __global__ __launch_bounds__(256) void latent_bwd_kernel(LatentArgs a) {
                     if (a.est == EST_LA) t += 0.5f - 0.5f * z * sd * e;
                 }
             }
+            float v;
             if (a.est == EST_LA) v = g + sl * t;
             else v = isv ? g + a.sc * 0.5f * (1.f - fexp(lv)) : g - a.sc * mu;
             a.dmulv[(int64_t)m * Z2 + c] = (bf16_t)f2bf(v);
+            cs += v;
         }
-        float s = v;
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
-        if ((threadIdx.x & 63) == 0) a.colpart[(int64_t)blockIdx.x * Z2 + c] = s;
     }
+    red[w][lane] = cs;
+    __syncthreads();
+    if (w == 0 && c < Z2)
+        a.colpart[(int64_t)blockIdx.x * Z2 + c] = ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
 }
 
 // Split-K weight gradients: sum the slabs in fixed order, then the optimizer rule.
@@ -192,8 +199,39 @@ __global__ __launch_bounds__(256) void wreduce_opt_kernel(WReduceArgs w) {
     }
 }
 
+// ELBO partials, stage 1: block b sums a contiguous chunk of the per-row log p and
+// KL / LA partials in fp64 (fixed order) -> parts[2b], parts[2b + 1].
+constexpr int kElboBlocks = 256;
+__global__ __launch_bounds__(256) void elbo_partial_kernel(ElboArgs e, double* parts) {
+    __shared__ double sh[256];
+    const int64_t clp = (e.n_lp + gridDim.x - 1) / gridDim.x, ckl = (e.n_kl + gridDim.x - 1) / gridDim.x;
+    const int64_t lp0 = blockIdx.x * clp, lp1 = min(e.n_lp, lp0 + clp);
+    const int64_t kl0 = blockIdx.x * ckl, kl1 = min(e.n_kl, kl0 + ckl);
+    double lp = 0, kl = 0;
+    for (int64_t i = lp0 + threadIdx.x; i < lp1; i += 256) lp += e.lp_part[i];
+    for (int64_t i = kl0 + threadIdx.x; i < kl1; i += 256) kl += e.kl_part[i];
+    lp = block_sum256(lp, sh);
+    kl = block_sum256(kl, sh);
+    if (threadIdx.x == 0) { parts[2 * blockIdx.x] = lp; parts[2 * blockIdx.x + 1] = kl; }
+}
+
+// ELBO stage 2 (one workgroup): the stage-1 sums in fixed order, then the step outputs.
+DEV void elbo_finish(const ElboArgs& e, const double* parts, int n) {
+    __shared__ double sh[256];
+    double lp = 0, kl = 0;
+    for (int i = threadIdx.x; i < n; i += 256) { lp += parts[2 * i]; kl += parts[2 * i + 1]; }
+    lp = block_sum256(lp, sh);
+    kl = block_sum256(kl, sh);
+    if (threadIdx.x == 0) elbo_emit(e, lp, kl, 0.0);
+}
+__global__ __launch_bounds__(256) void elbo_final_kernel(ElboArgs e, const double* parts, int n) {
+    elbo_finish(e, parts, n);
+}
+
 // Bias gradients from the epilogues' column partials (fixed order), optimizer rule, and
-// one extra workgroup that reduces the ELBO partials and advances cursor / step.
+// one extra workgroup that finishes the ELBO and advances cursor / step.  A block owns
+// 64 consecutive bias columns; its 4 waves split the partial rows (lane = column) with
+// 8 loads in flight each, then wave 0 sums the 4 wave totals in order.
 struct BiasSeg {
     const float* part; int nrb; int N;   // partials [nrb][N]
     ColMap map;                           // column -> arena index (biases: ld = 0)
@@ -203,21 +241,39 @@ struct BiasArgs {
     int total;                            // sum of the segments' N
     Opt opt;
     ElboArgs elbo;
+    const double* elbo_parts; int n_elbo_parts;
 };
 __global__ __launch_bounds__(256) void bias_opt_kernel(BiasArgs b) {
     if (blockIdx.x == gridDim.x - 1) {
-        __shared__ double sh[256];
-        elbo_reduce(b.elbo, sh);
+        elbo_finish(b.elbo, b.elbo_parts, b.n_elbo_parts);
         return;
     }
-    int e = blockIdx.x * 256 + threadIdx.x;
-    if (e >= b.total) return;
+    __shared__ float red[4][64];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    int e = blockIdx.x * 64 + lane;
+    const bool ok = e < b.total;
     int s = 0;
-    while (s < b.nseg - 1 && e >= b.seg[s].N) { e -= b.seg[s].N; ++s; }
-    const BiasSeg& g = b.seg[s];
+    if (ok)
+        while (s < b.nseg - 1 && e >= b.seg[s].N) { e -= b.seg[s].N; ++s; }
     float v = 0.f;
-    for (int r = 0; r < g.nrb; ++r) v += g.part[(int64_t)r * g.N + e];
-    b.opt.apply(g.map.at(0, e), -1, v);
+    if (ok) {
+        const BiasSeg& g = b.seg[s];
+        float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        int r = w;
+        for (; r + 28 < g.nrb; r += 32) {
+#pragma unroll
+            for (int u = 0; u < 8; ++u) acc[u] += g.part[(int64_t)(r + 4 * u) * g.N + e];
+        }
+        for (; r < g.nrb; r += 4) acc[0] += g.part[(int64_t)r * g.N + e];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v += acc[u];
+    }
+    red[w][lane] = v;
+    __syncthreads();
+    if (w == 0 && ok) {
+        const float t = ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
+        b.opt.apply(b.seg[s].map.at(0, e), -1, t);
+    }
 }
 
 // DP: after the all-reduce of [grad arena | SGVB], the replicated optimizer over the
@@ -259,6 +315,7 @@ struct BfState {
     float *ml_slab = nullptr, *dz_slab = nullptr, *w_slab = nullptr;
     float *cp3 = nullptr, *cp45 = nullptr, *cp1 = nullptr, *cp26 = nullptr, *lp = nullptr, *kl = nullptr;
     float *mu = nullptr, *lv = nullptr, *eps = nullptr;
+    double* elbo_parts = nullptr;      // [kElboBlocks][2] stage-1 ELBO sums
     int ks_heads = 1, ks_dz = 1, ks_w1 = 1, ks_w45 = 1;
     ShadowMap smap{};
 };
