@@ -43,10 +43,15 @@ typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 typedef uint16_t bf16_t;   // raw bf16 bits in memory
 
 enum : int { KC = 0, KO = 1 };
-constexpr int BM = 128, BN = 128, BK = 64, NTHR = 256;
-constexpr int kTileBytes = BM * BK * 2;          // one operand tile image (16 KiB)
-constexpr int kStageBytes = 2 * kTileBytes;      // A + B
-constexpr int kLdsBytes = 2 * kStageBytes;       // double buffer (64 KiB)
+constexpr int BM = 256, BN = 128, BK = 64, NTHR = 512, NWAVE = 8;
+constexpr int kATileBytes = BM * BK * 2;         // A operand tile image (32 KiB)
+constexpr int kBTileBytes = BN * BK * 2;         // B operand tile image (16 KiB)
+constexpr int kStageBytes = kATileBytes + kBTileBytes;
+constexpr int kStages = 3;
+constexpr int kLdsBytes = kStages * kStageBytes;  // 144 KiB: one block per CU
+constexpr int kGldsA = kATileBytes / 1024 / NWAVE;   // 1-KiB LDS-DMA pieces per wave per tile
+constexpr int kGldsB = kBTileBytes / 1024 / NWAVE;
+constexpr int kGldsPerTile = kGldsA + kGldsB;        // 6: the counted vmcnt of the ring
 
 // f32 -> bf16, round to nearest even (inputs here are finite)
 DEV uint32_t f2bf(float f) {
@@ -58,50 +63,72 @@ DEV float bf2f(uint32_t b) { return __builtin_bit_cast(float, b << 16); }
 DEV int swz_kc(int r) { return (r >> 1) & 7; }
 DEV int swz_ko(int r) { return ((r & 3) << 1) | (((r >> 3) & 1) << 3); }
 
-// One 128-row x 64-k operand tile: 4 x 16 B per thread, global -> registers -> LDS.
-template <int LAY>
-struct TileLoader {
-    rsrc_t buf;
+// One R-row x 64-k operand tile, HBM -> LDS directly (buffer_load_dwordx4 ... lds): each
+// wave-instruction writes 1 KiB of the tile image linearly (lane l at byte 16 l), so the
+// XOR swizzle is applied to the SOURCE chunk each lane fetches (guide rule 21): the lane
+// that fills physical chunk p of a row loads logical chunk p ^ swz(row).  KC image:
+// [R rows][64 k] (128-B rows); KO image: [64 k-rows][R] (2R-byte rows).  Out-of-range
+// chunks are redirected past the buffer end and land as zeros.
+typedef int v4i __attribute__((ext_vector_type(4)));
+// Buffer descriptor as four SGPRs (base, stride 0, num_records, raw-buffer flags).
+DEV v4i mkdesc(const void* p, int64_t nbytes) {
+    const uint64_t a = reinterpret_cast<uint64_t>(p);
+    v4i d;
+    d.x = __builtin_amdgcn_readfirstlane((int)(uint32_t)a);
+    d.y = __builtin_amdgcn_readfirstlane((int)((uint32_t)(a >> 32) & 0xFFFFu));
+    d.z = __builtin_amdgcn_readfirstlane((int)(nbytes < 0x7FFFFFF0ll ? nbytes : 0x7FFFFFF0ll));
+    d.w = 0x00020000;
+    return d;
+}
+// One 16-B-per-lane LDS-DMA piece (buffer_load_dwordx4 ... lds) to the wave-uniform LDS
+// address `lds`.  Issued from inline asm ON PURPOSE: hipcc cannot prove the MFMA loop's
+// ds_reads miss the DMA'd stage and would drain the whole ring (vmcnt(0)) before every
+// read; here the kernel counts the queue itself (s_waitcnt vmcnt(6) per step).
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"
+DEV void dma16(v4i rsrc, uint32_t voff, uint32_t lds) {
+    asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds"
+                 :: "v"(voff), "s"(rsrc), "s"(lds) : "memory", "m0");
+}
+#pragma clang diagnostic pop
+
+template <int LAY, int R>
+struct TileDma {
+    v4i buf;
     int ld;        // row stride (elements) of the stored matrix
     int rlim;      // valid rows (M or N extent)
     int klim;      // end of this block's K range
     int r0;        // first row of the tile
-    DEV void load(v4u (&st)[4], int k0) const {
+    static constexpr int kPieces = R * BK * 2 / 1024 / NWAVE;
+    DEV void issue(char* img, int k0, int wave, int lane) const {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int id = threadIdx.x + NTHR * i;
+        for (int i = 0; i < kPieces; ++i) {
+            const int piece = wave * kPieces + i;             // 1-KiB piece of the image
+            const int byte = piece * 1024 + lane * 16;
             uint32_t off;
             if constexpr (LAY == KC) {
-                const int r = r0 + (id >> 3), k = k0 + (id & 7) * 8;
+                const int row = byte >> 7, p = (byte >> 4) & 7;
+                const int c = p ^ swz_kc(row);
+                const int r = r0 + row, k = k0 + c * 8;
                 off = (r < rlim && k < klim) ? ((uint32_t)r * (uint32_t)ld + (uint32_t)k) * 2u : kOOB;
             } else {
-                const int k = k0 + (id >> 4), r = r0 + (id & 15) * 8;
+                constexpr int RB = 2 * R;                     // image row bytes
+                const int kr = byte / RB, pb = byte % RB;
+                const int p = pb >> 4;
+                const int c = (p & ~15) | ((p & 15) ^ swz_ko(kr));
+                const int k = k0 + kr, r = r0 + c * 8;
                 off = (k < klim && r < rlim) ? ((uint32_t)k * (uint32_t)ld + (uint32_t)r) * 2u : kOOB;
             }
-            st[i] = __builtin_bit_cast(v4u, __builtin_amdgcn_raw_buffer_load_b128(buf, off, 0, 0));
-        }
-    }
-    DEV void store(const v4u (&st)[4], char* img) const {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int id = threadIdx.x + NTHR * i;
-            int o;
-            if constexpr (LAY == KC) {
-                const int r = id >> 3, c = id & 7;
-                o = r * 128 + ((c ^ swz_kc(r)) << 4);
-            } else {
-                const int r = id >> 4, c = id & 15;
-                o = r * 256 + ((c ^ swz_ko(r)) << 4);
-            }
-            *reinterpret_cast<v4u*>(img + o) = st[i];
+            dma16(buf, off, __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(img + piece * 1024)));
         }
     }
 };
 
 // Fragment (8 consecutive k of one row / column) for MFMA k-step kk (k = 32 kk ...)
 // of the 16 rows starting at `row` of the tile image.
-template <int LAY>
+template <int LAY, int R>
 DEV bf16x8 frag(const char* img, int row, int kk, int lane) {
+    constexpr int RB = 2 * R;   // KO image row bytes
     if constexpr (LAY == KC) {
         const int r = row + (lane & 15);
         const int c = 4 * kk + (lane >> 4);
@@ -112,9 +139,9 @@ DEV bf16x8 frag(const char* img, int row, int kk, int lane) {
         const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
         const int kr = 32 * kk + 8 * g + q;
         const int c = (row >> 3) + (p >> 1);
-        const int o = ((c ^ swz_ko(kr)) << 4) + (p & 1) * 8;   // swz_ko(kr + 4) == swz_ko(kr)
-        const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + kr * 256 + o));
-        const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + (kr + 4) * 256 + o));
+        const int o = (((c & ~15) | ((c & 15) ^ swz_ko(kr))) << 4) + (p & 1) * 8;   // swz_ko(kr+4) == swz_ko(kr)
+        const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + kr * RB + o));
+        const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + (kr + 4) * RB + o));
         const s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
         return __builtin_bit_cast(bf16x8, v);
     }
@@ -156,19 +183,20 @@ DEV void tile_of(const GemmArgs& g, int& tm, int& tn) {
 }
 
 template <int LA, int LB, class Epi>
-__global__ __launch_bounds__(NTHR, 2) void gemm_kernel(GemmArgs g, Epi e) {
-    __shared__ __attribute__((aligned(16))) char smem[kLdsBytes];
+__global__ __launch_bounds__(NTHR, 1) void gemm_kernel(GemmArgs g, Epi e) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
     int tm, tn;
     tile_of(g, tm, tn);
     const int m0 = tm * BM, n0 = tn * BN;
     const int kz = blockIdx.y;
     const int kbeg = kz * g.kslice;
     const int kend = min(g.K, kbeg + g.kslice);
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int wm = wave >> 1, wn = wave & 1;
 
-    TileLoader<LA> la{mkbuf(g.A + g.ab.offset(), g.a_bytes), g.lda, g.M, kend, m0};
-    TileLoader<LB> lb{mkbuf(g.B, g.b_bytes), g.ldb, g.N, kend, n0};
+    const TileDma<LA, BM> la{mkdesc(g.A + g.ab.offset(), g.a_bytes), g.lda, g.M, kend, m0};
+    const TileDma<LB, BN> lb{mkdesc(g.B, g.b_bytes), g.ldb, g.N, kend, n0};
 
     f32x4 acc[4][4];
 #pragma unroll
@@ -177,41 +205,45 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_kernel(GemmArgs g, Epi e) {
         for (int j = 0; j < 4; ++j) acc[i][j] = zero4();
 
     const int nkt = (kend - kbeg + BK - 1) / BK;
-    v4u sa[4], sb[4];
-    if (nkt > 0) {
-        la.load(sa, kbeg);
-        lb.load(sb, kbeg);
-        la.store(sa, smem);
-        lb.store(sb, smem + kTileBytes);
-    }
-    __syncthreads();
+    auto stage = [&](int s) { return smem + s * kStageBytes; };
+    auto issue = [&](int t) {
+        char* st = stage(t % kStages);
+        la.issue(st, kbeg + t * BK, wave, lane);
+        lb.issue(st + kATileBytes, kbeg + t * BK, wave, lane);
+    };
+    // Ring of 3 LDS stages, prefetch distance 2: tile t + 2 streams in while tile t is
+    // multiplied.  Each wave waits only for its own pieces of tile t + 1 (counted vmcnt:
+    // tile t + 2's 6 pieces stay in flight) before the step's one barrier, and a stage is
+    // read only after the barrier that follows that wait (guide §5, "Read a staged buffer
+    // one phase AFTER the wait that retires it").  Raw s_barrier: __syncthreads() would
+    // drain every LDS-DMA (vmcnt(0)).
+    if (nkt > 0) issue(0);
+    if (nkt > 1) issue(1);
+    if (nkt > 1) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
     for (int t = 0; t < nkt; ++t) {
-        char* As = smem + (t & 1) * kStageBytes;
-        char* Bs = As + kTileBytes;
-        const bool more = t + 1 < nkt;
-        if (more) {
-            la.load(sa, kbeg + (t + 1) * BK);
-            lb.load(sb, kbeg + (t + 1) * BK);
-        }
+        if (t + 2 < nkt) issue(t + 2);
+        const char* As = stage(t % kStages);
+        const char* Bs = As + kATileBytes;
 #pragma unroll
         for (int kk = 0; kk < 2; ++kk) {
             bf16x8 af[4], bfr[4];
 #pragma unroll
-            for (int i = 0; i < 4; ++i) af[i] = frag<LA>(As, wm * 64 + 16 * i, kk, lane);
+            for (int i = 0; i < 4; ++i) af[i] = frag<LA, BM>(As, wm * 64 + 16 * i, kk, lane);
 #pragma unroll
-            for (int j = 0; j < 4; ++j) bfr[j] = frag<LB>(Bs, wn * 64 + 16 * j, kk, lane);
+            for (int j = 0; j < 4; ++j) bfr[j] = frag<LB, BN>(Bs, wn * 64 + 16 * j, kk, lane);
 #pragma unroll
             for (int i = 0; i < 4; ++i)
 #pragma unroll
                 for (int j = 0; j < 4; ++j)
                     acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
         }
-        if (more) {
-            char* nx = smem + ((t + 1) & 1) * kStageBytes;
-            la.store(sa, nx);
-            lb.store(sb, nx + kTileBytes);
-        }
-        __syncthreads();
+        if (t + 2 < nkt) asm volatile("s_waitcnt vmcnt(6) lgkmcnt(0)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
     }
     // Epilogue.  The LDS is free again (the loop ended on a barrier): epilogues with a
     // bf16 input tile (x, h, hd at the output positions) fetch it with coalesced 16-B

@@ -19,7 +19,10 @@ __global__ __launch_bounds__(512) void tile_wgrad_kernel(P p0, WGradArgs w, int 
     static_assert(WM * WN * KS == 8, "fused launches are 512 threads");
     __shared__ float sa[kWKB][kWP];
     __shared__ float sb[kWKB][kWP];
-    const int bid = blockIdx.x;
+    // XCD remap within each part: the phase tiles (critical path) stay spread over all
+    // XCDs, each XCD's share contiguous in tile order
+    const int b0 = blockIdx.x;
+    const int bid = b0 < ntile ? xcd_remap(b0, ntile) : ntile + xcd_remap(b0 - ntile, (int)gridDim.x - ntile);
     if (bid < ntile) {
         P p = p0;
         VAEB_STAMP(p.a, 0);
@@ -34,7 +37,8 @@ template <int NCT, bool VEC>
 __global__ __launch_bounds__(512) void dz_dh_wgrad_kernel(StepArgs a, WGradArgs w, int nrow) {
     __shared__ float sa[kWKB][kWP];
     __shared__ float sb[kWKB][kWP];
-    const int bid = blockIdx.x;
+    const int b0 = blockIdx.x;
+    const int bid = b0 < nrow ? b0 : nrow + xcd_remap(b0 - nrow, (int)gridDim.x - nrow);
     if (bid < nrow) {
         VAEB_STAMP(a, 0);
         dz_dh_body<NCT>(a, bid * 16);

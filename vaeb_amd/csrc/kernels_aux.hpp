@@ -287,7 +287,7 @@ template <bool VEC>
 __global__ __launch_bounds__(256) void wgrad_kernel(WGradArgs p) {
     __shared__ float sa[kWKB][kWP];
     __shared__ float sb[kWKB][kWP];
-    const int bid = blockIdx.x;
+    const int bid = (int)blockIdx.x < p.total_wgs ? xcd_remap(blockIdx.x, p.total_wgs) : (int)blockIdx.x;
     if (p.dbg && threadIdx.x == 0) p.dbg[bid * 8 + 0] = __builtin_amdgcn_s_memrealtime();
     if (bid >= p.total_wgs) {  // the extra workgroup: ELBO of this step
         elbo_reduce(p.elbo, reinterpret_cast<double*>(&sa[0][0]));

@@ -71,7 +71,8 @@ __global__ __launch_bounds__(512) void enc_latent_kernel(StepArgs a) {
     p.prepare();
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int li = lane & 15, q = lane >> 4;
-    const int bx = blockIdx.x, by = blockIdx.y, nctH = gridDim.y;
+    const int lin = xcd_remap(blockIdx.x + blockIdx.y * gridDim.x, gridDim.x * gridDim.y);
+    const int bx = lin % gridDim.x, by = lin / gridDim.x, nctH = gridDim.y;
     const int m0 = bx * 16, n0 = by * 16;
     const int Z = a.Z, H = a.H;
     const rsrc_t bs = mkbuf(a.slab_ml, (int64_t)gridDim.x * nctH * 2 * Z * 16 * 4);
@@ -217,9 +218,11 @@ __global__ __launch_bounds__(512, 4) void decout_z_kernel(StepArgs a) {
     p.prepare();
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int li = lane & 15, q = lane >> 4;
-    const int m0 = blockIdx.x * 16, n0 = blockIdx.y * 16;
+    const int lin = xcd_remap(blockIdx.x + blockIdx.y * gridDim.x, gridDim.x * gridDim.y);
+    const int bxr = lin % gridDim.x, byr = lin / gridDim.x;
+    const int m0 = bxr * 16, n0 = byr * 16;
     const int Z = a.Z, H = a.H;
-    const bool col0 = blockIdx.y == 0;
+    const bool col0 = byr == 0;
     const bool rowok = ((m0 + li) % a.Mbp) < a.Mb;
     const rsrc_t bw1 = mkbuf(a.W1, (int64_t)Z * H * 4);
     const rsrc_t bb1 = mkbuf(a.b1, (int64_t)H * 4);

@@ -51,6 +51,18 @@ namespace vaeb {
 
 DEV f32x4 zero4() { f32x4 z = {0.f, 0.f, 0.f, 0.f}; return z; }
 
+// XCD-aware block order (guide T1): the dispatcher deals linear workgroup ids round-robin
+// over the 8 XCDs (id % 8 labels the blocks that share one L2), so remap them to give
+// each XCD one contiguous run of logical ids -- blocks that share an operand panel (the
+// row blocks of one weight-column tile) then share that XCD's L2 instead of fetching
+// the panel once per XCD.  Bijective for any n; a speed choice only (the kernels are
+// placement independent).
+DEV int xcd_remap(int b, int n) {
+    if (n < 16) return b;
+    const int xcd = b & 7, q = n >> 3, r = n & 7;
+    return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (b >> 3);
+}
+
 // ------------------------------------------------------------------ buffer operands
 // Every operand fetch is a raw buffer load through a 128-bit descriptor built from
 // wave-uniform kernel arguments: a 32-bit per-lane byte offset, and the hardware range
