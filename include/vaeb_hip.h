@@ -129,6 +129,53 @@ int vaeb_kernel_name(int32_t kernel_id, char* out, int32_t cap);
 int vaeb_debug_timeline(vaeb_ctx* ctx, int32_t batch_index, uint64_t* out, int64_t cap,
                         int32_t* out_launches);
 
+/* ------------------------------------------------------------------------------------------
+ * degenerate-vae deterministic autoencoder (/root/reference/degenerate-vae/ae.py:41-117):
+ * encoder MLP -> linear latent Z -> decoder MLP -> Bernoulli (otype "binary") or Gaussian
+ * ("cont") output, logjoint = loglik + N(0, s2) prior on theta + N(0, 1) prior on Z, AdaGrad.
+ * Parameters are flat float32 in the reference's theta order (ae.py:51,56,64,72):
+ *   Wenc0..Wenc{n_enc-1}, benc0.., Wz, bz, Wdec0.., bdec0.., then Wout, bout (binary) or
+ *   Wmu, Wlogs2, bmu, blogs2 (cont); W row-major [in x out].
+ * ------------------------------------------------------------------------------------------ */
+#define VAEB_AE_MAX_LAYERS 8
+enum vaeb_ae_otype { VAEB_AE_BINARY = 0, VAEB_AE_CONT = 1 };   /* ae.py:58 / :65 */
+enum vaeb_act      { VAEB_ACT_TANH = 0, VAEB_ACT_SIGMOID = 1, VAEB_ACT_RELU = 2 };   /* f, ae.py:41 */
+
+typedef struct vaeb_ae_config {
+    int32_t Dobs;                         /* observation size                                */
+    int32_t n_enc;                        /* len(Denc) >= 1                                  */
+    int32_t Denc[VAEB_AE_MAX_LAYERS];     /* encoder hidden sizes                            */
+    int32_t Dz;                           /* latent size                                     */
+    int32_t n_dec;                        /* len(Ddec) >= 1                                  */
+    int32_t Ddec[VAEB_AE_MAX_LAYERS];     /* decoder hidden sizes                            */
+    int32_t otype;                        /* enum vaeb_ae_otype                              */
+    int32_t act;                          /* enum vaeb_act                                   */
+    float   s2;                           /* prior variance on theta (ae.py:41, default 1.0) */
+    float   eta;                          /* AdaGrad learning rate (infalg.py:144)           */
+    int32_t max_batch;                    /* largest idx list / predict chunk                */
+    int32_t device;
+    int32_t reserved[4];
+} vaeb_ae_config;
+
+typedef struct vaeb_ae vaeb_ae;
+
+int vaeb_ae_create(const vaeb_ae_config* cfg, vaeb_ae** out);   /* ConstructAE (ae.py:41)    */
+int vaeb_ae_destroy(vaeb_ae* ae);
+int vaeb_ae_num_params(const vaeb_ae* ae, int64_t* n);
+int vaeb_ae_set_data(vaeb_ae* ae, const float* x, int64_t n_rows);   /* Xtr (ae.py:87)        */
+int vaeb_ae_set_params(vaeb_ae* ae, const float* flat, int64_t n);
+int vaeb_ae_get_params(vaeb_ae* ae, float* flat, int64_t n);
+int vaeb_ae_set_adagrad_state(vaeb_ae* ae, const float* flat, int64_t n);
+int vaeb_ae_get_adagrad_state(vaeb_ae* ae, float* flat, int64_t n);
+/* train(idx) (ae.py:82-89): one AdaGrad step on rows Xtr[idx]; writes loglik / n. */
+int vaeb_ae_train(vaeb_ae* ae, const int32_t* idx, int32_t n, float* out_loglik_per_row);
+/* An epoch of train() calls on consecutive `batch`-sized slices of idx, the last partial
+ * slice kept (ae.py:145-151); out[j] = train's value for slice j.  One host sync. */
+int vaeb_ae_train_many(vaeb_ae* ae, const int32_t* idx, int32_t n, int32_t batch, float* out);
+int vaeb_ae_reconstruct(vaeb_ae* ae, const float* x, int64_t n, float* out);   /* ae.py:92-98  */
+int vaeb_ae_encode(vaeb_ae* ae, const float* x, int64_t n, float* z_out);      /* ae.py:101-107 */
+int vaeb_ae_decode(vaeb_ae* ae, const float* z, int64_t n, float* out);        /* ae.py:110-116 */
+
 /* Test hook for the bf16 GEMM engine: C[M x N] = sum_k A(m, k) B(k, n) with the operands
  * rounded to bf16 on device.  a_kouter = 0: A is stored [M x K], 1: [K x M]; b_kouter = 0:
  * B is stored [N x K], 1: [K x N].  ksplit K slices are summed in fixed order.  Uses the

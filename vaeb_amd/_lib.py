@@ -29,7 +29,13 @@ EXPORTS = [
     "vaeb_epoch_elbo", "vaeb_synchronize", "vaeb_validate", "vaeb_reconstruct",
     "vaeb_comm_unique_id", "vaeb_comm_init", "vaeb_get_grads", "vaeb_get_activation",
     "vaeb_profile_steps", "vaeb_kernel_name", "vaeb_debug_timeline", "vaeb_test_gemm_bf16",
+    "vaeb_ae_create", "vaeb_ae_destroy", "vaeb_ae_num_params", "vaeb_ae_set_data", "vaeb_ae_set_params",
+    "vaeb_ae_get_params", "vaeb_ae_set_adagrad_state", "vaeb_ae_get_adagrad_state", "vaeb_ae_train",
+    "vaeb_ae_train_many", "vaeb_ae_reconstruct", "vaeb_ae_encode", "vaeb_ae_decode",
 ]
+AE_MAX_LAYERS = 8
+AE_BINARY, AE_CONT = 0, 1
+ACT = {"tanh": 0, "sigmoid": 1, "relu": 2}
 
 
 class VaebConfig(ctypes.Structure):
@@ -40,6 +46,15 @@ class VaebConfig(ctypes.Structure):
         ("lr", ctypes.c_float), ("adagrad_eps", ctypes.c_float), ("device", ctypes.c_int32),
         ("max_eval_rows", ctypes.c_int32), ("use_graph", ctypes.c_int32), ("keep_grads", ctypes.c_int32),
         ("dtype", ctypes.c_int32), ("reserved", ctypes.c_int32 * 5),
+    ]
+
+
+class AEConfigC(ctypes.Structure):
+    _fields_ = [
+        ("Dobs", ctypes.c_int32), ("n_enc", ctypes.c_int32), ("Denc", ctypes.c_int32 * 8),
+        ("Dz", ctypes.c_int32), ("n_dec", ctypes.c_int32), ("Ddec", ctypes.c_int32 * 8),
+        ("otype", ctypes.c_int32), ("act", ctypes.c_int32), ("s2", ctypes.c_float), ("eta", ctypes.c_float),
+        ("max_batch", ctypes.c_int32), ("device", ctypes.c_int32), ("reserved", ctypes.c_int32 * 4),
     ]
 
 
@@ -95,6 +110,19 @@ def load():
         "vaeb_debug_timeline": ([_P, ctypes.c_int32, ctypes.POINTER(ctypes.c_uint64), _I64,
                                  ctypes.POINTER(ctypes.c_int32)], ctypes.c_int),
         "vaeb_test_gemm_bf16": ([_P] + [ctypes.c_int32] * 5 + [_F, _F, _F, ctypes.c_int32], ctypes.c_int),
+        "vaeb_ae_create": ([ctypes.POINTER(AEConfigC), ctypes.POINTER(_P)], ctypes.c_int),
+        "vaeb_ae_destroy": ([_P], ctypes.c_int),
+        "vaeb_ae_num_params": ([_P, ctypes.POINTER(_I64)], ctypes.c_int),
+        "vaeb_ae_set_data": ([_P, _F, _I64], ctypes.c_int),
+        "vaeb_ae_set_params": ([_P, _F, _I64], ctypes.c_int),
+        "vaeb_ae_get_params": ([_P, _F, _I64], ctypes.c_int),
+        "vaeb_ae_set_adagrad_state": ([_P, _F, _I64], ctypes.c_int),
+        "vaeb_ae_get_adagrad_state": ([_P, _F, _I64], ctypes.c_int),
+        "vaeb_ae_train": ([_P, ctypes.POINTER(ctypes.c_int32), ctypes.c_int32, _F], ctypes.c_int),
+        "vaeb_ae_train_many": ([_P, ctypes.POINTER(ctypes.c_int32), ctypes.c_int32, ctypes.c_int32, _F], ctypes.c_int),
+        "vaeb_ae_reconstruct": ([_P, _F, _I64, _F], ctypes.c_int),
+        "vaeb_ae_encode": ([_P, _F, _I64, _F], ctypes.c_int),
+        "vaeb_ae_decode": ([_P, _F, _I64, _F], ctypes.c_int),
     }
     for name, (args, res) in sig.items():
         fn = getattr(lib, name)
@@ -277,3 +305,95 @@ class Context:
             check(self.lib.vaeb_kernel_name(int(ids[k]), buf, 64))
             out.append((buf.value.decode(), float(ms[k])))
         return out
+
+
+class AEContext:
+    """One degenerate-vae autoencoder (vaeb_ae_*) on one GPU."""
+
+    def __init__(self, Dobs, Denc, Dz, Ddec, otype="binary", act="tanh", s2=1.0, eta=0.01, max_batch=100,
+                 device=0):
+        self.lib = load()
+        c = AEConfigC()
+        c.Dobs, c.Dz = int(Dobs), int(Dz)
+        Denc, Ddec = list(Denc), list(Ddec)
+        if not (1 <= len(Denc) <= AE_MAX_LAYERS and 1 <= len(Ddec) <= AE_MAX_LAYERS):
+            raise VaebError(f"1..{AE_MAX_LAYERS} encoder / decoder hidden layers are supported")
+        c.n_enc, c.n_dec = len(Denc), len(Ddec)
+        for i, d in enumerate(Denc):
+            c.Denc[i] = int(d)
+        for i, d in enumerate(Ddec):
+            c.Ddec[i] = int(d)
+        c.otype = {"binary": AE_BINARY, "cont": AE_CONT}[otype]
+        c.act = ACT[act]
+        c.s2, c.eta = float(s2), float(eta)
+        c.max_batch, c.device = int(max_batch), int(device)
+        self.cfg = c
+        self.Dobs, self.Dz = c.Dobs, c.Dz
+        self.h = _P()
+        check(self.lib.vaeb_ae_create(ctypes.byref(c), ctypes.byref(self.h)))
+        n = _I64()
+        check(self.lib.vaeb_ae_num_params(self.h, ctypes.byref(n)))
+        self.P = n.value
+
+    def close(self):
+        if getattr(self, "h", None) is not None and self.h.value:
+            self.lib.vaeb_ae_destroy(self.h)
+            self.h = _P()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_data(self, x):
+        x = np.ascontiguousarray(x, np.float32)
+        check(self.lib.vaeb_ae_set_data(self.h, fptr(x), x.shape[0]))
+
+    def set_params(self, flat):
+        flat = np.ascontiguousarray(flat, np.float32)
+        check(self.lib.vaeb_ae_set_params(self.h, fptr(flat), flat.size))
+
+    def get_params(self):
+        out = np.empty(self.P, np.float32)
+        check(self.lib.vaeb_ae_get_params(self.h, fptr(out), out.size))
+        return out
+
+    def set_adagrad_state(self, flat):
+        flat = np.ascontiguousarray(flat, np.float32)
+        check(self.lib.vaeb_ae_set_adagrad_state(self.h, fptr(flat), flat.size))
+
+    def get_adagrad_state(self):
+        out = np.empty(self.P, np.float32)
+        check(self.lib.vaeb_ae_get_adagrad_state(self.h, fptr(out), out.size))
+        return out
+
+    def train(self, idx):
+        idx = np.ascontiguousarray(idx, np.int32)
+        out = ctypes.c_float()
+        check(self.lib.vaeb_ae_train(self.h, idx.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), idx.size,
+                                     ctypes.byref(out)))
+        return out.value
+
+    def train_many(self, idx, batch):
+        idx = np.ascontiguousarray(idx, np.int32)
+        nb = -(-idx.size // int(batch))
+        out = np.empty(nb, np.float32)
+        check(self.lib.vaeb_ae_train_many(self.h, idx.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), idx.size,
+                                          int(batch), fptr(out)))
+        return out
+
+    def _predict(self, fn, x, width_out):
+        x = np.ascontiguousarray(x, np.float32)
+        out = np.empty((x.shape[0], width_out), np.float32)
+        check(fn(self.h, fptr(x), x.shape[0], fptr(out)))
+        return out
+
+    def reconstruct(self, x):
+        return self._predict(self.lib.vaeb_ae_reconstruct, x, self.Dobs)
+
+    def encode(self, x):
+        return self._predict(self.lib.vaeb_ae_encode, x, self.Dz)
+
+    def decode(self, z):
+        return self._predict(self.lib.vaeb_ae_decode, z, self.Dobs)

@@ -20,6 +20,7 @@
 #include "hfuse.hpp"
 #include "latent.hpp"
 #include "step_bf16.hpp"
+#include "ae_mlp.hpp"
 
 using namespace vaeb;
 
@@ -1081,3 +1082,6 @@ int vaeb_kernel_name(int32_t id, char* out, int32_t cap) {
 }
 
 }  // extern "C"
+
+// degenerate-vae autoencoder (vaeb_ae_*) on the same fp32 tile engine
+#include "engine_ae.inc"
