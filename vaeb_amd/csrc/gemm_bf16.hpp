@@ -43,15 +43,20 @@ typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 typedef uint16_t bf16_t;   // raw bf16 bits in memory
 
 enum : int { KC = 0, KO = 1 };
-constexpr int BM = 256, BN = 128, BK = 64, NTHR = 512, NWAVE = 8;
-constexpr int kATileBytes = BM * BK * 2;         // A operand tile image (32 KiB)
-constexpr int kBTileBytes = BN * BK * 2;         // B operand tile image (16 KiB)
-constexpr int kStageBytes = kATileBytes + kBTileBytes;
-constexpr int kStages = 3;
-constexpr int kLdsBytes = kStages * kStageBytes;  // 144 KiB: one block per CU
-constexpr int kGldsA = kATileBytes / 1024 / NWAVE;   // 1-KiB LDS-DMA pieces per wave per tile
-constexpr int kGldsB = kBTileBytes / 1024 / NWAVE;
-constexpr int kGldsPerTile = kGldsA + kGldsB;        // 6: the counted vmcnt of the ring
+// Block tile BM x BNT x BK with BNT = 256 (8 waves as 2 x 4, 128 x 64 each) or 128
+// (8 waves as 4 x 2, 64 x 64 each; for products with too few 256-wide tiles to fill the
+// chip).  BN is the widest tile (it sizes the epilogue LDS tile).
+constexpr int BM = 256, BN = 256, BK = 32, NTHR = 512, NWAVE = 8;
+constexpr int kATileBytes = BM * BK * 2;         // A operand tile image (16 KiB)
+constexpr int kStages = 4;                       // prefetch distance 3
+template <int BNT>
+struct Shape {
+    static constexpr int WGN = BNT / 64, WGM = NWAVE / WGN;   // wave grid
+    static constexpr int TM = BM / WGM / 16, TN = 4;          // MFMA tiles per wave
+    static constexpr int kB = BNT * BK * 2;                   // B operand tile image
+    static constexpr int kStage = kATileBytes + kB;
+    static constexpr int kPieces = (kATileBytes + kB) / 1024 / NWAVE;   // vmcnt unit per tile
+};
 
 // f32 -> bf16, round to nearest even (inputs here are finite)
 DEV uint32_t f2bf(float f) {
@@ -60,7 +65,10 @@ DEV uint32_t f2bf(float f) {
 }
 DEV float bf2f(uint32_t b) { return __builtin_bit_cast(float, b << 16); }
 
-DEV int swz_kc(int r) { return (r >> 1) & 7; }
+// KC images have 64-B rows (BK = 32): chunk c (0..3) of row r lives at c ^ g[(r >> 2) & 3],
+// g = {0, 2, 3, 1}, which makes the four ds_read_b128 lane groups of a 16-row fragment read
+// (MI355X_MICROARCH.md §LDS) hit 16 distinct 16-B slots.
+DEV int swz_kc(int r) { return (0x78 >> (((r >> 2) & 3) * 2)) & 3; }   // g = {0, 2, 3, 1}
 DEV int swz_ko(int r) { return ((r & 3) << 1) | (((r >> 3) & 1) << 3); }
 
 // One R-row x 64-k operand tile, HBM -> LDS directly (buffer_load_dwordx4 ... lds): each
@@ -107,7 +115,7 @@ struct TileDma {
             const int byte = piece * 1024 + lane * 16;
             uint32_t off;
             if constexpr (LAY == KC) {
-                const int row = byte >> 7, p = (byte >> 4) & 7;
+                const int row = byte >> 6, p = (byte >> 4) & 3;
                 const int c = p ^ swz_kc(row);
                 const int r = r0 + row, k = k0 + c * 8;
                 off = (r < rlim && k < klim) ? ((uint32_t)r * (uint32_t)ld + (uint32_t)k) * 2u : kOOB;
@@ -132,7 +140,7 @@ DEV bf16x8 frag(const char* img, int row, int kk, int lane) {
     if constexpr (LAY == KC) {
         const int r = row + (lane & 15);
         const int c = 4 * kk + (lane >> 4);
-        return *reinterpret_cast<const bf16x8*>(img + r * 128 + ((c ^ swz_kc(r)) << 4));
+        return *reinterpret_cast<const bf16x8*>(img + r * (BK * 2) + ((c ^ swz_kc(r)) << 4));
     } else {
         // ds_read_b64_tr_b16: lane 4q+p of each 16-lane group supplies k-row q of its
         // 4-row block, columns 4p..4p+3; lane i receives column i, k-row q in element q.
@@ -182,81 +190,100 @@ DEV void tile_of(const GemmArgs& g, int& tm, int& tn) {
     tn = in / gm;
 }
 
-template <int LA, int LB, class Epi>
+template <int P>
+DEV void ring_wait(int after) {   // wait for all but `after` tiles' worth of LDS-DMA pieces
+    if constexpr (P == 4) {
+        if (after >= 2) asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)" ::: "memory");
+        else if (after == 1) asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    } else {
+        static_assert(P == 3, "ring piece count");
+        if (after >= 2) asm volatile("s_waitcnt vmcnt(6) lgkmcnt(0)" ::: "memory");
+        else if (after == 1) asm volatile("s_waitcnt vmcnt(3) lgkmcnt(0)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+}
+
+template <int LA, int LB, int BNT, class Epi>
 __global__ __launch_bounds__(NTHR, 1) void gemm_kernel(GemmArgs g, Epi e) {
+    using S = Shape<BNT>;
+    constexpr int TM = S::TM, TN = S::TN;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     int tm, tn;
     tile_of(g, tm, tn);
-    const int m0 = tm * BM, n0 = tn * BN;
+    const int m0 = tm * BM, n0 = tn * BNT;
     const int kz = blockIdx.y;
     const int kbeg = kz * g.kslice;
     const int kend = min(g.K, kbeg + g.kslice);
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int wm = wave >> 1, wn = wave & 1;
+    const int wm = wave / S::WGN, wn = wave % S::WGN;
 
     const TileDma<LA, BM> la{mkdesc(g.A + g.ab.offset(), g.a_bytes), g.lda, g.M, kend, m0};
-    const TileDma<LB, BN> lb{mkdesc(g.B, g.b_bytes), g.ldb, g.N, kend, n0};
+    const TileDma<LB, BNT> lb{mkdesc(g.B, g.b_bytes), g.ldb, g.N, kend, n0};
 
-    f32x4 acc[4][4];
+    f32x4 acc[TM][TN];
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = zero4();
+        for (int j = 0; j < TN; ++j) acc[i][j] = zero4();
 
     const int nkt = (kend - kbeg + BK - 1) / BK;
-    auto stage = [&](int s) { return smem + s * kStageBytes; };
+    auto stage = [&](int s) { return smem + s * S::kStage; };
     auto issue = [&](int t) {
         char* st = stage(t % kStages);
         la.issue(st, kbeg + t * BK, wave, lane);
         lb.issue(st + kATileBytes, kbeg + t * BK, wave, lane);
     };
-    // Ring of 3 LDS stages, prefetch distance 2: tile t + 2 streams in while tile t is
+    // Ring of 4 LDS stages, prefetch distance 3: tiles t+1..t+3 stream in while tile t is
     // multiplied.  Each wave waits only for its own pieces of tile t + 1 (counted vmcnt:
-    // tile t + 2's 6 pieces stay in flight) before the step's one barrier, and a stage is
-    // read only after the barrier that follows that wait (guide §5, "Read a staged buffer
-    // one phase AFTER the wait that retires it").  Raw s_barrier: __syncthreads() would
-    // drain every LDS-DMA (vmcnt(0)).
-    if (nkt > 0) issue(0);
-    if (nkt > 1) issue(1);
-    if (nkt > 1) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
+    // the pieces of the tiles issued after it stay in flight) before the step's one
+    // barrier, and a stage is read only after the barrier that follows that wait (guide
+    // §5, "Read a staged buffer one phase AFTER the wait that retires it").  Raw s_barrier:
+    // __syncthreads() would drain every LDS-DMA (vmcnt(0)).
+    for (int t = 0; t < 3 && t < nkt; ++t) issue(t);
+    ring_wait<S::kPieces>(min(nkt - 1, 2));
     for (int t = 0; t < nkt; ++t) {
-        if (t + 2 < nkt) issue(t + 2);
+        if (t + 3 < nkt) issue(t + 3);
         const char* As = stage(t % kStages);
         const char* Bs = As + kATileBytes;
+        bf16x8 af[TM], bfr[TN];
 #pragma unroll
-        for (int kk = 0; kk < 2; ++kk) {
-            bf16x8 af[4], bfr[4];
+        for (int i = 0; i < TM; ++i) af[i] = frag<LA, BM>(As, wm * (16 * TM) + 16 * i, 0, lane);
 #pragma unroll
-            for (int i = 0; i < 4; ++i) af[i] = frag<LA, BM>(As, wm * 64 + 16 * i, kk, lane);
+        for (int j = 0; j < TN; ++j) bfr[j] = frag<LB, BNT>(Bs, wn * (16 * TN) + 16 * j, 0, lane);
 #pragma unroll
-            for (int j = 0; j < 4; ++j) bfr[j] = frag<LB, BN>(Bs, wn * 64 + 16 * j, kk, lane);
+        for (int i = 0; i < TM; ++i)
 #pragma unroll
-            for (int i = 0; i < 4; ++i)
-#pragma unroll
-                for (int j = 0; j < 4; ++j)
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
-        }
-        if (t + 2 < nkt) asm volatile("s_waitcnt vmcnt(6) lgkmcnt(0)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        asm volatile("" ::: "memory");
+            for (int j = 0; j < TN; ++j)
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+        ring_wait<S::kPieces>(min(nkt - 1, t + 3) - (t + 1));
     }
-    // Epilogue.  The LDS is free again (the loop ended on a barrier): epilogues with a
-    // bf16 input tile (x, h, hd at the output positions) fetch it with coalesced 16-B
-    // loads into a padded LDS tile; bf16 results go back through the same tile and
-    // leave with 16-B stores.
+    // Epilogue.  The LDS is free again (the loop ended on a barrier with nothing in
+    // flight): epilogues with a bf16 input tile (x, h, hd at the output positions) fetch
+    // it with coalesced 16-B loads into a padded LDS tile; bf16 results go back through the
+    // same tile and leave with 16-B stores.  Waves hand 64 x 64 blocks to the epilogue.
     if constexpr (Epi::kIn) {
-        e.load_in(m0, n0, smem);
+        e.template load_in<BNT>(m0, n0, smem);
         __syncthreads();
     }
-    e(m0 + wm * 64, n0 + wn * 64, acc, kz, smem);
+    const int mw = m0 + wm * (16 * TM), nw = n0 + wn * (16 * TN);
+    if constexpr (TM == 4) {
+        e(mw, nw, acc, kz, smem);
+    } else {
+        f32x4 lo[4][4], hi[4][4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) { lo[i][j] = acc[i][j]; hi[i][j] = acc[i + 4][j]; }
+        e(mw, nw, lo, kz, smem);
+        e(mw + 64, nw, hi, kz, smem);
+    }
     if constexpr (Epi::kOut) {
         __syncthreads();
-        e.store_out(m0, n0, smem);
+        e.template store_out<BNT>(m0, n0, smem);
     }
 }
 
@@ -275,10 +302,14 @@ DEV float colsum_lanes(float s) {
 }
 
 // ------------------------------------------------------------------ epilogue tiles
-// A 128 x 128 bf16 tile in LDS with a 288-B row pitch: the four 16-lane groups of a
+// A BM x BN bf16 tile in LDS with a 544-B row pitch: the four 16-lane groups of a
 // per-element access (rows 4(l>>4)+r, 16 consecutive columns) land on disjoint banks.
-constexpr int kEP = 288;
-constexpr int kEpiTileBytes = BM * kEP;   // 36 KiB
+constexpr int kEP = BN * 2 + 32;          // 544 B: 136 dwords = 8 (mod 32)
+constexpr int kEpiTileBytes = BM * kEP;   // 136 KiB
+template <int BNT>
+constexpr int lds_bytes() {
+    return kStages * Shape<BNT>::kStage > kEpiTileBytes ? kStages * Shape<BNT>::kStage : kEpiTileBytes;
+}
 DEV int eoff(int row, int col) { return row * kEP + col * 2; }
 DEV float lds_bf(const char* t, int row, int col) {
     return bf2f(*reinterpret_cast<const uint16_t*>(t + eoff(row, col)));
@@ -292,7 +323,7 @@ DEV void lds_st_bf(char* t, int row, int col, float v) {
 // the data rows).  GI: source column c goes to tile column (c & 31) + 64 (c >> 5) -- the
 // W2 slots of the Gaussian decoder's 32-column interleave.
 template <int W, bool GI = false>
-DEV void tile_load(char* t, rsrc_t src, int ld, int r0, int c0, int rlim, int clim, int rmod) {
+DEV void tile_load(char* t, rsrc_t src, int ld, int r0, int c0, int rlim, int clim, int rmod, int lc0) {
     constexpr int CPR = W / 8;                 // 16-B chunks per row
     constexpr int N = BM * CPR / NTHR;
 #pragma unroll
@@ -303,12 +334,12 @@ DEV void tile_load(char* t, rsrc_t src, int ld, int r0, int c0, int rlim, int cl
         const int sr = rmod > 0 ? gr % rmod : gr;
         const uint32_t off = (gr < rlim && gc < clim) ? ((uint32_t)sr * (uint32_t)ld + (uint32_t)gc) * 2u : kOOB;
         const v4u v = __builtin_bit_cast(v4u, __builtin_amdgcn_raw_buffer_load_b128(src, off, 0, 0));
-        const int tc = GI ? ((ch * 8) & 31) + ((ch * 8) >> 5) * 64 : ch * 8;
+        const int tc = lc0 + (GI ? ((ch * 8) & 31) + ((ch * 8) >> 5) * 64 : ch * 8);
         *reinterpret_cast<v4u*>(t + row * kEP + tc * 2) = v;
     }
 }
 template <int W>
-DEV void tile_store(const char* t, bf16_t* dst, int ld, int r0, int c0, int rlim, int clim) {
+DEV void tile_store(const char* t, bf16_t* dst, int ld, int r0, int c0, int rlim, int clim, int lc0) {
     constexpr int CPR = W / 8;
     constexpr int N = BM * CPR / NTHR;
 #pragma unroll
@@ -317,7 +348,8 @@ DEV void tile_store(const char* t, bf16_t* dst, int ld, int r0, int c0, int rlim
         const int row = id / CPR, ch = id % CPR;
         const int gr = r0 + row, gc = c0 + ch * 8;
         if (gr < rlim && gc < clim)
-            *reinterpret_cast<v4u*>(dst + (int64_t)gr * ld + gc) = *reinterpret_cast<const v4u*>(t + row * kEP + ch * 16);
+            *reinterpret_cast<v4u*>(dst + (int64_t)gr * ld + gc) =
+                *reinterpret_cast<const v4u*>(t + row * kEP + lc0 * 2 + ch * 16);
     }
 }
 
@@ -366,7 +398,8 @@ struct EpiBiasAct {
                 }
         }
     }
-    DEV void store_out(int m0, int n0, char* smem) const { tile_store<BN>(smem, out, ldo, m0, n0, M, N); }
+    template <int W>
+    DEV void store_out(int m0, int n0, char* smem) const { tile_store<W>(smem, out, ldo, m0, n0, M, N, n0 & (BN - 1)); }
 };
 
 // Backward through tanh: out = acc * (1 - t^2) with t the stored bf16 activation at the
@@ -378,8 +411,9 @@ struct EpiDTanh {
     const bf16_t* t; int ldt; int M, N;
     bf16_t* out; int ldo;
     float* colpart;
+    template <int W>
     DEV void load_in(int m0, int n0, char* smem) const {
-        tile_load<BN>(smem, mkbuf(t, (int64_t)M * ldt * 2), ldt, m0, n0, M, N, 0);
+        tile_load<W>(smem, mkbuf(t, (int64_t)M * ldt * 2), ldt, m0, n0, M, N, 0, n0 & (BN - 1));
     }
     DEV void operator()(int mw, int nw, f32x4 (&acc)[4][4], int, char* smem) const {
         const int lane = threadIdx.x & 63;
@@ -402,7 +436,8 @@ struct EpiDTanh {
             if (lane < 16 && col < N) colpart[(int64_t)(mw >> 6) * N + col] = cs;
         }
     }
-    DEV void store_out(int m0, int n0, char* smem) const { tile_store<BN>(smem, out, ldo, m0, n0, M, N); }
+    template <int W>
+    DEV void store_out(int m0, int n0, char* smem) const { tile_store<W>(smem, out, ldo, m0, n0, M, N, n0 & (BN - 1)); }
 };
 
 // Decoder output (VAEB.py:257-263, 302-313) on the [M_e x Dn] block of a2 (| a6):
@@ -428,10 +463,11 @@ struct EpiDecOut {
     float* lp; int nlp;
     float* colpart;
     float* yout;
+    template <int W>
     DEV void load_in(int m0, int n0, char* smem) const {
         const rsrc_t src = mkbuf(x + xb.offset(), (int64_t)Mx * ldx * 2);
-        if constexpr (GAUSS) tile_load<BN / 2, true>(smem, src, ldx, m0, n0 / 2, M, D, Mx);
-        else tile_load<BN>(smem, src, ldx, m0, n0, M, D, Mx);
+        if constexpr (GAUSS) tile_load<W / 2, true>(smem, src, ldx, m0, n0 / 2, M, D, Mx, n0 & (BN - 1));
+        else tile_load<W>(smem, src, ldx, m0, n0, M, D, Mx, n0 & (BN - 1));
     }
     DEV void operator()(int mw, int nw, f32x4 (&acc)[4][4], int, char* smem) const {
         const int lane = threadIdx.x & 63;
@@ -501,8 +537,9 @@ struct EpiDecOut {
                 }
         }
     }
+    template <int W>
     DEV void store_out(int m0, int n0, char* smem) const {
-        if (train) tile_store<BN>(smem, dA, ldd, m0, n0, M, N);
+        if (train) tile_store<W>(smem, dA, ldd, m0, n0, M, N, n0 & (BN - 1));
     }
 };
 

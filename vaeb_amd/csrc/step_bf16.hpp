@@ -133,25 +133,27 @@ __global__ __launch_bounds__(256) void latent_fwd_kernel(LatentArgs a) {
 }
 
 // [dMu | dLv] from the dZ slabs (LA direct terms folded as in the
-// fp32 path), stored bf16 for the dh / dW45 GEMMs; column sums per 64-row block for the
-// b4 / b5 gradients.  Grid (row blocks of 64, column blocks of 64); a wave owns 64
-// consecutive columns of [dMu | dLv] (coalesced along the latent index) and every 4th
-// row of the block; the 4 waves' column sums are combined in fixed order.
+// fp32 path), stored bf16 for the dh / dW45 GEMMs; column sums per 16-row block for the
+// b4 / b5 gradients.  Grid (row blocks of 16, column blocks of 64); wave w owns rows
+// 4w..4w+3 of the block and lane = one of 64 consecutive columns of [dMu | dLv]
+// (coalesced along the latent index); the 4 rows' loads are independent (unrolled), and
+// the 4 waves' column sums are combined in fixed order.
+constexpr int kLbRows = 16;
 __global__ __launch_bounds__(256) void latent_bwd_kernel(LatentArgs a) {
     __shared__ float red[4][64];
     const int Z = a.Z, Z2 = 2 * Z;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int c = blockIdx.y * 64 + lane;
-    const int m0 = blockIdx.x * 64;
-    const int m1 = min(a.M, m0 + 64);
     const int64_t LMZ = (int64_t)a.L * a.M * Z;
     const float sl = a.sc / (float)a.L;
     const bool isv = c >= Z;
     const int j = isv ? c - Z : c;
     float cs = 0.f;
     if (c < Z2) {
-#pragma unroll 4
-        for (int m = m0 + w; m < m1; m += 4) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int m = blockIdx.x * kLbRows + 4 * w + r;
+            if (m >= a.M) continue;
             const int64_t o = (int64_t)m * Z + j;
             const float mu = a.mu[o], lv = a.lv[o];
             const float sd = fexp(0.5f * lv);
