@@ -82,9 +82,10 @@ KERNEL_SYMBOLS = {"p1_enc": "PEnc", "p23_heads_dechid": "heads_dechid_kernel", "
                   "p8_wgrad_w3w45": "vaeb::wgrad_kernel", "p1_enc_latent": "vaeb::enc_latent_kernel",
                   "p4_decout_z": "vaeb::decout_z_kernel",
                   # bf16 GEMMs are one template: the epilogue / layout pair names the launch
-                  "bf_enc": "gemm_kernel<0, 1, vaeb::bf::EpiBiasAct>", "bf_decout": "EpiDecOut<false>",
-                  "bf_dhd": "gemm_kernel<0, 0, vaeb::bf::EpiDTanh>", "bf_dW26": "EpiAdagrad",
-                  "bf_dW3": "EpiAdagrad"}
+                  # (all listed substrings must appear: the tile width is a template argument)
+                  "bf_enc": ("gemm_kernel<0, 1,", "EpiBiasAct>"), "bf_decout": ("EpiDecOut<false>",),
+                  "bf_dhd": ("gemm_kernel<0, 0,", "EpiDTanh>"), "bf_dW26": ("EpiAdagrad",),
+                  "bf_dW3": ("EpiAdagrad",)}
 PMC_FILES = {"mnist": os.path.join(ROOT, "profiles", "r1", "pmc_per_launch.json"),
              "synth": os.path.join(ROOT, "profiles", "r1", "pmc_synth_per_launch.json")}
 
@@ -99,8 +100,10 @@ def committed_traffic(kernel, path=PMC_FILES["mnist"], symbols=KERNEL_SYMBOLS):
     except Exception:
         return None
     sym = symbols.get(kernel)
+    if isinstance(sym, str):
+        sym = (sym,)
     for name, v in data.items():
-        if sym and sym in name and "hbm_bytes_per_launch" in v:
+        if sym and all(t in name for t in sym) and "hbm_bytes_per_launch" in v:
             return v["hbm_bytes_per_launch"]
     return None
 

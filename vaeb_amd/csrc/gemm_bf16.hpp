@@ -254,11 +254,13 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_kernel(GemmArgs g, Epi e) {
         for (int i = 0; i < TM; ++i) af[i] = frag<LA, BM>(As, wm * (16 * TM) + 16 * i, 0, lane);
 #pragma unroll
         for (int j = 0; j < TN; ++j) bfr[j] = frag<LB, BNT>(Bs, wn * (16 * TN) + 16 * j, 0, lane);
+        __builtin_amdgcn_s_setprio(1);   // keeps the MFMA cluster between the barriers (guide T5)
 #pragma unroll
         for (int i = 0; i < TM; ++i)
 #pragma unroll
             for (int j = 0; j < TN; ++j)
                 acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+        __builtin_amdgcn_s_setprio(0);
         ring_wait<S::kPieces>(min(nkt - 1, t + 3) - (t + 1));
     }
     // Epilogue.  The LDS is free again (the loop ended on a barrier with nothing in

@@ -79,6 +79,23 @@ struct LatentArgs {
     float* colpart;                    // [ceil(M/64)][2Z]
 };
 
+// Fixed-order sum of n fp32 split-K slab values (v[s * stride + off], s = 0..n-1) added to
+// `init`: the loads go out in groups of 8 through a buffer descriptor (slot s >= n reads 0
+// from the hardware range check), so a group is ONE memory round trip instead of n
+// dependent ones, and the running sum keeps the slab order.
+DEV float slab_sum(rsrc_t b, uint32_t off, uint32_t stride, int n, bool ok, float init) {
+    float acc = init;
+    for (int s0 = 0; s0 < n; s0 += 8) {
+        float v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+            v[u] = bld(b, (ok && s0 + u < n) ? off + (uint32_t)(s0 + u) * stride : kOOB);
+#pragma unroll
+        for (int u = 0; u < 8; ++u) acc += v[u];
+    }
+    return acc;
+}
+
 // One wave per row: mu / lv from the heads slabs (fixed-order sum) + bias; eps; z; the
 // per-row KL (LB, VAEB.py:343) or, per sample, prior - logQ (LA, VAEB.py:322-325).
 __global__ __launch_bounds__(256) void latent_fwd_kernel(LatentArgs a) {
@@ -89,15 +106,14 @@ __global__ __launch_bounds__(256) void latent_fwd_kernel(LatentArgs a) {
     const int64_t brow = a.rows.order ? (int64_t)a.rows.order[*a.rows.cursor] : 0;
     const int64_t grow = brow * a.row_base_mul + a.row_base_add + m;
     const uint64_t c23 = (uint64_t)(*a.step) ^ ((uint64_t)a.domain << 63);
+    const rsrc_t bsl = mkbuf(a.ml_slab, (int64_t)a.nslab * a.M * Z2 * 4);
+    const uint32_t sstride = (uint32_t)a.M * Z2 * 4u;
     float kl = 0.f;
     float la[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};   // LA: L <= 8 on this path
     for (int j = lane; j < Z; j += 64) {
-        float mu = a.b4[j], lv = a.b5[j];
-        for (int s = 0; s < a.nslab; ++s) {
-            const float* sl = a.ml_slab + ((int64_t)s * a.M + m) * Z2;
-            mu += sl[j];
-            lv += sl[Z + j];
-        }
+        const uint32_t o = ((uint32_t)m * Z2 + j) * 4u;
+        const float mu = slab_sum(bsl, o, sstride, a.nslab, true, a.b4[j]);
+        const float lv = slab_sum(bsl, o + Z * 4u, sstride, a.nslab, true, a.b5[j]);
         a.mu[(int64_t)m * Z + j] = mu;
         a.lv[(int64_t)m * Z + j] = lv;
         const float sd = fexp(0.5f * lv);
@@ -144,44 +160,76 @@ __global__ __launch_bounds__(256) void latent_bwd_kernel(LatentArgs a) {
     const int Z = a.Z, Z2 = 2 * Z;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int c = blockIdx.y * 64 + lane;
-    const int64_t LMZ = (int64_t)a.L * a.M * Z;
+    const int LMZ = a.L * a.M * Z;
     const float sl = a.sc / (float)a.L;
     const bool isv = c >= Z;
     const int j = isv ? c - Z : c;
-    float cs = 0.f;
-    if (c < Z2) {
+    const bool cok = c < Z2;
+    const rsrc_t bdz = mkbuf(a.dz_slab, (int64_t)a.ndz * LMZ * 4);
+    const rsrc_t bmu = mkbuf(a.mu, (int64_t)a.M * Z * 4), blv = mkbuf(a.lv, (int64_t)a.M * Z * 4);
+    const rsrc_t bep = mkbuf(a.eps, (int64_t)LMZ * 4);
+    int mr[4];
+    bool ok[4];
+    float mu[4], lv[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        mr[r] = blockIdx.x * kLbRows + 4 * w + r;
+        ok[r] = cok && mr[r] < a.M;
+        const uint32_t o = ok[r] ? (uint32_t)(mr[r] * Z + j) * 4u : kOOB;
+        mu[r] = bld(bmu, o);
+        lv[r] = bld(blv, o);
+    }
+    float g[4] = {0.f, 0.f, 0.f, 0.f}, t[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int l = 0; l < a.L; ++l) {
+        float dz[4], e[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-            const int m = blockIdx.x * kLbRows + 4 * w + r;
-            if (m >= a.M) continue;
-            const int64_t o = (int64_t)m * Z + j;
-            const float mu = a.mu[o], lv = a.lv[o];
-            const float sd = fexp(0.5f * lv);
-            float g = 0.f, t = 0.f;
-            for (int l = 0; l < a.L; ++l) {
-                const int64_t ol = ((int64_t)l * a.M + m) * Z + j;
-                float dz = 0.f;
-                for (int s = 0; s < a.ndz; ++s) dz += a.dz_slab[(int64_t)s * LMZ + ol];
-                const float e = a.eps[ol];
-                const float z = mu + sd * e;
-                if (!isv) {
-                    g += dz;
-                    if (a.est == EST_LA) t += -z;
-                } else {
-                    g += dz * 0.5f * sd * e;
-                    if (a.est == EST_LA) t += 0.5f - 0.5f * z * sd * e;
+            const uint32_t ol = (uint32_t)((l * a.M + mr[r]) * Z + j) * 4u;
+            e[r] = bld(bep, ok[r] ? ol : kOOB);
+            dz[r] = 0.f;
+        }
+        // the four rows' slab loads go out together, 8 slabs per round trip
+        for (int s0 = 0; s0 < a.ndz; s0 += 8) {
+            float v[4][8];
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    const uint32_t ol = (uint32_t)(((s0 + u) * a.L * a.M + l * a.M + mr[r]) * Z + j) * 4u;
+                    v[r][u] = bld(bdz, (ok[r] && s0 + u < a.ndz) ? ol : kOOB);
                 }
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+#pragma unroll
+                for (int u = 0; u < 8; ++u) dz[r] += v[r][u];
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const float sd = fexp(0.5f * lv[r]);
+            const float z = mu[r] + sd * e[r];
+            if (!isv) {
+                g[r] += dz[r];
+                if (a.est == EST_LA) t[r] += -z;
+            } else {
+                g[r] += dz[r] * 0.5f * sd * e[r];
+                if (a.est == EST_LA) t[r] += 0.5f - 0.5f * z * sd * e[r];
             }
-            float v;
-            if (a.est == EST_LA) v = g + sl * t;
-            else v = isv ? g + a.sc * 0.5f * (1.f - fexp(lv)) : g - a.sc * mu;
-            a.dmulv[(int64_t)m * Z2 + c] = (bf16_t)f2bf(v);
+        }
+    }
+    float cs = 0.f;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        float v;
+        if (a.est == EST_LA) v = g[r] + sl * t[r];
+        else v = isv ? g[r] + a.sc * 0.5f * (1.f - fexp(lv[r])) : g[r] - a.sc * mu[r];
+        if (ok[r]) {
+            a.dmulv[(int64_t)mr[r] * Z2 + c] = (bf16_t)f2bf(v);
             cs += v;
         }
     }
     red[w][lane] = cs;
     __syncthreads();
-    if (w == 0 && c < Z2)
+    if (w == 0 && cok)
         a.colpart[(int64_t)blockIdx.x * Z2 + c] = ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
 }
 
@@ -193,9 +241,9 @@ struct WReduceArgs {
 __global__ __launch_bounds__(256) void wreduce_opt_kernel(WReduceArgs w) {
     const int64_t MN = (int64_t)w.M * w.N;
     const int64_t stride = (int64_t)gridDim.x * 256;
+    const rsrc_t bs = mkbuf(w.slab, (int64_t)w.nslab * MN * 4);
     for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < MN; e += stride) {
-        float g = 0.f;
-        for (int s = 0; s < w.nslab; ++s) g += w.slab[(int64_t)s * MN + e];
+        const float g = slab_sum(bs, (uint32_t)e * 4u, (uint32_t)MN * 4u, w.nslab, true, 0.f);
         const int m = (int)(e / w.N), n = (int)(e % w.N);
         w.opt.apply(w.map.at(m, n), e, g);
     }
@@ -210,8 +258,22 @@ __global__ __launch_bounds__(256) void elbo_partial_kernel(ElboArgs e, double* p
     const int64_t lp0 = blockIdx.x * clp, lp1 = min(e.n_lp, lp0 + clp);
     const int64_t kl0 = blockIdx.x * ckl, kl1 = min(e.n_kl, kl0 + ckl);
     double lp = 0, kl = 0;
-    for (int64_t i = lp0 + threadIdx.x; i < lp1; i += 256) lp += e.lp_part[i];
-    for (int64_t i = kl0 + threadIdx.x; i < kl1; i += 256) kl += e.kl_part[i];
+    // 8 loads per round trip (buffer range check zero-fills the tail), fixed order
+    const rsrc_t blp = mkbuf(e.lp_part, e.n_lp * 4), bkl = mkbuf(e.kl_part, e.n_kl * 4);
+    for (int64_t i0 = lp0 + threadIdx.x; i0 < lp1; i0 += 8 * 256) {
+        float v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = bld(blp, i0 + u * 256 < lp1 ? (uint32_t)(i0 + u * 256) * 4u : kOOB);
+#pragma unroll
+        for (int u = 0; u < 8; ++u) lp += v[u];
+    }
+    for (int64_t i0 = kl0 + threadIdx.x; i0 < kl1; i0 += 8 * 256) {
+        float v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = bld(bkl, i0 + u * 256 < kl1 ? (uint32_t)(i0 + u * 256) * 4u : kOOB);
+#pragma unroll
+        for (int u = 0; u < 8; ++u) kl += v[u];
+    }
     lp = block_sum256(lp, sh);
     kl = block_sum256(kl, sh);
     if (threadIdx.x == 0) { parts[2 * blockIdx.x] = lp; parts[2 * blockIdx.x + 1] = kl; }

@@ -255,6 +255,15 @@ DEV float ftanh(float x) {
 }
 DEV float softplusf(float a) { return fmaxf(a, 0.f) + flog(1.f + fexp(-fabsf(a))); }
 DEV float sigmoidf(float a) { return frcp(1.f + fexp(-a)); }
+// sigmoid(a) and softplus(a) from ONE exponential: t = e^{-|a|}, sigmoid = 1/(1+t) (a >= 0)
+// or t/(1+t), softplus = max(a, 0) + log(1 + t)  (the Bernoulli decoder's y and BCE).
+DEV void sigmoid_softplus(float a, float& y, float& sp) {
+    const float t = fexp(-fabsf(a));
+    const float d = 1.f + t;
+    const float r = frcp(d);
+    y = a >= 0.f ? r : t * r;
+    sp = fmaxf(a, 0.f) + flog(d);
+}
 
 // One standard normal for the 128-bit counter (Box-Muller on the first two words;
 // v_cos_f32 takes its argument in revolutions).
