@@ -107,6 +107,11 @@ int vaeb_validate(vaeb_ctx* ctx, const float* x, int64_t n, double* out_sum);
 /* Decoder means y for host x with z = mu (n_samples <= 0 branch of VAEB.reconstruct,
  * VAEB.py:267-270): writes [n x D]. */
 int vaeb_reconstruct(vaeb_ctx* ctx, const float* x, int64_t n, float* out_y);
+/* VAEB.reconstruct(x, n_samples) (VAEB.py:267-300): n_samples <= 0 as vaeb_reconstruct;
+ * otherwise the decoder output averaged over n_samples posterior draws z = mu + exp(lv/2) eps
+ * (Philox validation streams 1..n_samples, or in host eps mode rows [s*n, (s+1)*n) of the
+ * pushed eps, which must hold n * n_samples rows).  Writes [n x D]. */
+int vaeb_reconstruct_sampled(vaeb_ctx* ctx, const float* x, int64_t n, int32_t n_samples, float* out_y);
 
 /* Data parallel (one ctx per rank): the library owns an RCCL communicator; the 128-byte
  * unique id is produced on rank 0 and broadcast by the host (e.g. torch.distributed). */

@@ -264,6 +264,32 @@ def validate(params, x, eps, cfg: Config, q=None):
     return out["sgvb"]
 
 
+def reconstruct(params, x, eps, cfg: Config):
+    """VAEB.reconstruct (VAEB.py:267-300).  eps: None (n_samples <= 0: decoder at z = mu,
+    :269-270) or [S, B, Z] standard normals, one draw per sample (:279-280); the decoder
+    outputs are summed in sample order and divided by S (:277-291).  Returns the Bernoulli
+    means y, or for the continuous decoder the averaged decoder mean (the reference's closing
+    np.random.multivariate_normal over a [B x D] mean, :292-296, cannot run)."""
+    p = _unpack(params, cfg)
+    dt = p["W3"].dtype
+    x = np.asarray(x, dt)
+    h = np.tanh(x @ p["W3"] + p["b3"])
+    mu = h @ p["W4"] + p["b4"]
+    lv = h @ p["W5"] + p["b5"]
+
+    def dec(z):
+        hd = np.tanh(z @ p["W1"] + p["b1"])
+        return sigmoid(hd @ p["W2"] + p["b2"])
+
+    if eps is None:
+        return dec(mu)
+    eps = np.asarray(eps, dt)
+    y = np.zeros((x.shape[0], cfg.D), dt)
+    for s in range(eps.shape[0]):
+        y = y + dec(mu + np.exp(dt.type(0.5) * lv) * eps[s])
+    return y / dt.type(eps.shape[0])
+
+
 # ---------------------------------------------------------------- full variational
 def fv_theta_prior(mu_list, sig_list):
     """VAEB.py:359-363: sum over params of 1/2 sum(1 + log sigma^2 - mu^2 - sigma^2)."""

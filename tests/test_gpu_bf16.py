@@ -147,6 +147,12 @@ def test_bf16_validate_and_reconstruct():
     out = O.forward_backward(p64, xv.astype(np.float64), np.zeros((1, 300, cfg.Z)), cfg, need_grad=False,
                              q=O.bf16_round)
     assert np.abs(y - out["y"]).max() <= 2e-3
+    # posterior-sample reconstruction (VAEB.py:271-291), 2 samples over 3 device chunks
+    eps2 = np.random.default_rng(2).standard_normal((2, 300, cfg.Z)).astype(np.float32)
+    ctx.push_eps(eps2.reshape(1, 600, cfg.Z))
+    ys = ctx.reconstruct_sampled(xv, 2)
+    ref_s = O.reconstruct(p64, xv.astype(np.float64), eps2.astype(np.float64), cfg)
+    assert np.abs(ys - ref_s).max() <= 2e-2
     ctx.close()
 
 

@@ -160,6 +160,46 @@ def test_reconstruct_matches_oracle():
     assert np.abs(y - out["y"]).max() <= 1e-5
 
 
+@pytest.mark.parametrize("continuous", [False, True])
+def test_reconstruct_sampled_matches_oracle(continuous):
+    """VAEB.reconstruct(x, n_samples > 0) (VAEB.py:271-291) with host-injected eps: the
+    decoder output averaged over the samples, |diff| <= 1e-5."""
+    cfg = O.Config(D=560, H=200, Z=2, continuous=True) if continuous else O.Config(D=784, H=500, Z=20)
+    x = data_for(cfg, 250, seed=11)
+    params = O.init_params(cfg)
+    rng = np.random.default_rng(12)
+    S = 3
+    eps = rng.standard_normal((S, 250, cfg.Z)).astype(np.float32)
+    ctx = make_ctx(cfg, 100, max_eval_rows=128)   # two device chunks
+    ctx.set_data(x)
+    ctx.set_params(O.flatten(params))
+    from vaeb_amd import _lib
+    ctx.set_eps_mode(_lib.EPS_HOST)
+    ctx.push_eps(eps.reshape(1, S * 250, cfg.Z))
+    y = ctx.reconstruct_sampled(x, S)
+    ref = O.reconstruct([q.astype(np.float64) for q in params], x.astype(np.float64), eps.astype(np.float64), cfg)
+    assert np.abs(y - ref).max() <= 1e-5
+    # n_samples <= 0 is the z = mu branch
+    y0 = ctx.reconstruct_sampled(x, 0)
+    assert np.abs(y0 - O.reconstruct([q.astype(np.float64) for q in params], x.astype(np.float64), None, cfg)).max() <= 1e-5
+
+
+def test_reconstruct_sampled_philox():
+    """Device-drawn samples: deterministic, distinct from z = mu, and converging to the
+    posterior-mean reconstruction as S grows (statistical)."""
+    cfg = O.Config(D=784, H=500, Z=20)
+    x = data_for(cfg, 100, seed=13)
+    params = O.init_params(cfg)
+    ctx = make_ctx(cfg, 100)
+    ctx.set_data(x)
+    ctx.set_params(O.flatten(params))
+    y1 = ctx.reconstruct_sampled(x, 4)
+    y2 = ctx.reconstruct_sampled(x, 4)
+    assert np.array_equal(y1, y2)
+    assert np.abs(y1 - ctx.reconstruct(x)).max() > 0
+    assert np.all((y1 > 0) & (y1 < 1))
+
+
 def test_fv_literal_step():
     cfg = O.Config(D=560, H=200, Z=2, continuous=True, estimator="FV")
     B = 100

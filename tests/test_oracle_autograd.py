@@ -82,3 +82,16 @@ def test_fv_gradients_closed_form():
     assert np.allclose(mu.grad.numpy(), -2 * mu.detach().numpy())
     s = sig.detach().numpy()
     assert np.allclose(sig.grad.numpy(), 1 / s - 2 * s)
+
+
+def test_oracle_reconstruct_branches():
+    """VAEB.reconstruct restatement (VAEB.py:267-300): S all-zero draws reproduce the
+    z = mu branch; one draw equals the decoder at mu + exp(lv/2) eps."""
+    cfg = O.Config(D=40, H=16, Z=3)
+    params = [p.astype(np.float64) for p in O.init_params(cfg)]
+    x = O.synthetic_mnist(n=7, D=40, seed=1).astype(np.float64)
+    y0 = O.reconstruct(params, x, None, cfg)
+    assert np.allclose(O.reconstruct(params, x, np.zeros((3, 7, 3)), cfg), y0, atol=1e-15)
+    eps = np.random.default_rng(0).standard_normal((1, 7, 3))
+    out = O.forward_backward(params, x, eps, cfg, need_grad=False)
+    assert np.allclose(O.reconstruct(params, x, eps, cfg), out["y"], atol=1e-15)

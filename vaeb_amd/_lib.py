@@ -26,7 +26,7 @@ EXPORTS = [
     "vaeb_set_data", "vaeb_set_params", "vaeb_get_params", "vaeb_set_adagrad_state",
     "vaeb_get_adagrad_state", "vaeb_set_fv_state", "vaeb_get_fv_state", "vaeb_set_eps_mode",
     "vaeb_push_eps", "vaeb_set_step", "vaeb_update", "vaeb_update_async", "vaeb_update_many",
-    "vaeb_epoch_elbo", "vaeb_synchronize", "vaeb_validate", "vaeb_reconstruct",
+    "vaeb_epoch_elbo", "vaeb_synchronize", "vaeb_validate", "vaeb_reconstruct", "vaeb_reconstruct_sampled",
     "vaeb_comm_unique_id", "vaeb_comm_init", "vaeb_get_grads", "vaeb_get_activation",
     "vaeb_profile_steps", "vaeb_kernel_name", "vaeb_debug_timeline", "vaeb_test_gemm_bf16",
     "vaeb_ae_create", "vaeb_ae_destroy", "vaeb_ae_num_params", "vaeb_ae_set_data", "vaeb_ae_set_params",
@@ -100,6 +100,7 @@ def load():
         "vaeb_synchronize": ([_P], ctypes.c_int),
         "vaeb_validate": ([_P, _F, _I64, ctypes.POINTER(ctypes.c_double)], ctypes.c_int),
         "vaeb_reconstruct": ([_P, _F, _I64, _F], ctypes.c_int),
+        "vaeb_reconstruct_sampled": ([_P, _F, _I64, ctypes.c_int32, _F], ctypes.c_int),
         "vaeb_comm_unique_id": ([ctypes.POINTER(ctypes.c_uint8)], ctypes.c_int),
         "vaeb_comm_init": ([_P, ctypes.POINTER(ctypes.c_uint8), ctypes.c_int32, ctypes.c_int32], ctypes.c_int),
         "vaeb_get_grads": ([_P, _F, _I64], ctypes.c_int),
@@ -260,6 +261,13 @@ class Context:
         x = np.ascontiguousarray(x, np.float32)
         y = np.empty((x.shape[0], self.cfg.D), np.float32)
         check(self.lib.vaeb_reconstruct(self.h, fptr(x), x.shape[0], fptr(y)))
+        return y
+
+    def reconstruct_sampled(self, x, n_samples):
+        """Decoder output averaged over n_samples posterior draws (VAEB.py:271-291)."""
+        x = np.ascontiguousarray(x, np.float32)
+        y = np.empty((x.shape[0], self.cfg.D), np.float32)
+        check(self.lib.vaeb_reconstruct_sampled(self.h, fptr(x), x.shape[0], int(n_samples), fptr(y)))
         return y
 
     # ---- data parallel

@@ -122,7 +122,7 @@ __global__ __launch_bounds__(512) void heads_dechid_kernel(StepArgs a) {
         lv = valid ? lv + b5n : 0.f;
         const float sd = fexp(0.5f * lv);
         const float elv = fexp(lv);
-        const uint64_t c23 = (uint64_t)stp ^ ((uint64_t)a.domain << 63);
+        const uint64_t c23 = philox_c23(stp, a.domain);
         for (int l = 0; l < a.L; ++l) {
             float e = 0.f;
             if (valid) {

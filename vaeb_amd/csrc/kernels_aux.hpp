@@ -78,6 +78,17 @@ __global__ __launch_bounds__(64) void delay_kernel(uint64_t ticks) {
     while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(8);
 }
 
+// Posterior-sample reconstruction (VAEB.py:277-291): acc = acc + y in sample order
+// (first sample: acc = y), and on the last sample acc /= n_samples.
+__global__ __launch_bounds__(256) void recon_accum_kernel(float* acc, const float* y, int64_t n, int first,
+                                                          float scale) {
+    const int64_t stride = (int64_t)gridDim.x * 256;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) {
+        float v = first ? y[i] : acc[i] + y[i];
+        acc[i] = scale != 0.f ? v / scale : v;
+    }
+}
+
 __global__ __launch_bounds__(256) void elbo_kernel(ElboArgs e) {
     __shared__ double sh[256];
     elbo_reduce(e, sh);

@@ -46,7 +46,7 @@ struct StepArgs {
     int eps_mode;          // 0 philox, 1 host buffer, 2 zero (reconstruct)
     uint64_t seed;
     const int64_t* step;   // Philox step counter (device)
-    uint32_t domain;       // 0 training, 1 validation
+    uint32_t domain;       // bit 0: validation; >> 1: reconstruction sample stream
     const float* eps_in;   // host-pushed [L][Mb][Z] (+ eps_in_off rows)
     int64_t eps_in_ld;     // rows per l-plane of eps_in
     // activations / deltas ([rows][cols] row-major; pad rows written as 0)
@@ -134,7 +134,7 @@ struct PHeads {
         const int ct = n0 >> 4;
         const int64_t grow0 = global_row0(a);
         const int64_t stp = a.step ? *a.step : 0;
-        const uint64_t c23 = (uint64_t)stp ^ ((uint64_t)a.domain << 63);
+        const uint64_t c23 = philox_c23(stp, a.domain);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const int m = m0 + 4 * (lane >> 4) + r;

@@ -105,7 +105,7 @@ __global__ __launch_bounds__(256) void latent_fwd_kernel(LatentArgs a) {
     const int Z = a.Z, Z2 = 2 * Z;
     const int64_t brow = a.rows.order ? (int64_t)a.rows.order[*a.rows.cursor] : 0;
     const int64_t grow = brow * a.row_base_mul + a.row_base_add + m;
-    const uint64_t c23 = (uint64_t)(*a.step) ^ ((uint64_t)a.domain << 63);
+    const uint64_t c23 = philox_c23(*a.step, a.domain);
     const rsrc_t bsl = mkbuf(a.ml_slab, (int64_t)a.nslab * a.M * Z2 * 4);
     const uint32_t sstride = (uint32_t)a.M * Z2 * 4u;
     float kl = 0.f;

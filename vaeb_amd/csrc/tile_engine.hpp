@@ -265,6 +265,12 @@ DEV void sigmoid_softplus(float a, float& y, float& sp) {
     sp = fmaxf(a, 0.f) + flog(d);
 }
 
+// Counter words 2-3 of a draw: the step, the validation flag (domain bit 0) in bit 63 and
+// the reconstruction sample stream (domain >> 1, VAEB.py:279-280) in bits 40..62.
+DEV uint64_t philox_c23(int64_t step, uint32_t domain) {
+    return (uint64_t)step ^ ((uint64_t)(domain & 1u) << 63) ^ ((uint64_t)(domain >> 1) << 40);
+}
+
 // One standard normal for the 128-bit counter (Box-Muller on the first two words;
 // v_cos_f32 takes its argument in revolutions).
 DEV float philox_normal(uint64_t seed, uint32_t c0, uint32_t c1, uint64_t c23) {

@@ -115,6 +115,7 @@ struct vaeb_ctx {
     float *h = nullptr, *mu = nullptr, *lv = nullptr, *eps = nullptr, *z = nullptr, *hd = nullptr,
           *y = nullptr, *dA2 = nullptr, *dA6 = nullptr, *dA1 = nullptr, *dZ = nullptr,
           *dMuLv = nullptr, *dA3 = nullptr, *kl_part = nullptr, *lp_part = nullptr;
+    float* yacc = nullptr;        // sampled reconstruction sum (allocated on first use)
     float *slab_ml = nullptr, *slab_dz = nullptr;  // folded-latent partial slabs (latent.hpp)
     int *cnt_ml = nullptr, *cnt_dz = nullptr;      // their per-row-block arrival counters
     // host staging (pinned)
@@ -694,7 +695,7 @@ int vaeb_destroy(vaeb_ctx* c) {
     if (c->comm) ncclCommDestroy(c->comm);
     float* fp[] = {c->theta2[0], c->theta2[1], c->acc, c->grad, c->fvmu, c->fvsg, c->fvam, c->fvas, c->fv_part, c->data, c->xeval,
                    c->elbo_out, c->eps_in, c->h, c->mu, c->lv, c->eps, c->z, c->hd, c->y, c->dA2, c->dA6, c->dA1,
-                   c->dZ, c->dMuLv, c->dA3, c->kl_part, c->lp_part, c->slab_ml, c->slab_dz};
+                   c->dZ, c->dMuLv, c->dA3, c->kl_part, c->lp_part, c->slab_ml, c->slab_dz, c->yacc};
     for (float* p : fp) if (p) hipFree(p);
     if (c->cnt_ml) hipFree(c->cnt_ml);
     if (c->cnt_dz) hipFree(c->cnt_dz);
@@ -926,6 +927,63 @@ int vaeb_validate(vaeb_ctx* c, const float* x, int64_t n, double* out_sum) {
 int vaeb_reconstruct(vaeb_ctx* c, const float* x, int64_t n, float* out_y) {
     if (!out_y) return fail(VAEB_ERR_ARG, "null out_y");
     return eval_rows(c, x, n, MODE_RECON, out_y, nullptr);
+}
+
+// VAEB.reconstruct with n_samples > 0 (VAEB.py:271-291): the decoder output averaged over
+// n_samples posterior draws z_s = mu + exp(lv / 2) eps_s, summed on device in sample order.
+// eps_s: Philox stream s + 1 of the validation domain, or (host eps mode) rows
+// [s * n, (s + 1) * n) of the pushed eps.  Continuous decoder: the mean of the decoder
+// means (the reference's final multivariate_normal draw is not reproduced).
+int vaeb_reconstruct_sampled(vaeb_ctx* c, const float* x, int64_t n, int32_t n_samples, float* out_y) {
+    if (!out_y) return fail(VAEB_ERR_ARG, "null out_y");
+    if (n_samples <= 0) return eval_rows(c, x, n, MODE_RECON, out_y, nullptr);
+    if (!c || !x || n <= 0) return fail(VAEB_ERR_ARG, "bad arguments");
+    const bool host = c->eps_mode == VAEB_EPS_HOST;
+    if (host && c->eps_rows != n * n_samples)
+        return fail(VAEB_ERR_STATE, "host eps mode: sampled reconstruct needs eps for %lld rows (n * n_samples), pushed %lld",
+                    (long long)(n * n_samples), (long long)c->eps_rows);
+    const vaeb_config& g = c->c;
+    const int chunk = g.max_eval_rows;
+    if (!c->yacc) {
+        if (int rc = dalloc(&c->yacc, (size_t)chunk * g.D)) return rc;
+    }
+    for (int64_t r0 = 0; r0 < n; r0 += chunk) {
+        const int rows = (int)std::min<int64_t>(chunk, n - r0);
+        const int64_t ny = (int64_t)rows * g.D;
+        if (is_bf16(c)) {
+            if (int rc = bf_upload_rows(c, x + r0 * g.D, rows, c->bf.xeval)) return rc;
+        } else {
+            HIP_TRY(hipMemcpyAsync(c->xeval, x + r0 * g.D, sizeof(float) * (size_t)ny, hipMemcpyHostToDevice, c->s));
+        }
+        for (int sidx = 0; sidx < n_samples; ++sidx) {
+            const uint32_t domain = 1u | ((uint32_t)(sidx + 1) << 1);
+            const float* eps = (host && c->eps_in) ? c->eps_in + ((int64_t)sidx * n + r0) * g.Z : nullptr;
+            Prof pr{c, false};
+            if (is_bf16(c)) {
+                BfFwd f{};
+                f.Mb = rows; f.mode = MODE_EVAL; f.train = false; f.x = c->bf.xeval; f.xb = bf::BatchRef{};
+                f.row_base_mul = 0; f.row_base_add = r0;
+                f.eps_in = eps; f.eps_in_ld = c->eps_rows; f.domain = domain;
+                f.yout = c->y;
+                if (int rc = bf_forward(c, c->par, f, pr)) return rc;
+            } else {
+                StepArgs a = make_args(c, c->par, rows, MODE_RECON, c->xeval, false);
+                a.L = 1; a.Me = a.Mbp;
+                a.eps_mode = host ? 1 : 0;
+                a.domain = domain;
+                a.row_base_add = r0;
+                a.eps_in = eps; a.eps_in_ld = c->eps_rows;
+                if (int rc = enqueue_forward(c, a, pr)) return rc;
+            }
+            const float scale = (sidx == n_samples - 1) ? (float)n_samples : 0.f;
+            hipLaunchKernelGGL(recon_accum_kernel, dim3((unsigned)std::min<int64_t>(1024, cdiv(ny, 256))), dim3(256), 0,
+                               c->s, c->yacc, c->y, ny, sidx == 0 ? 1 : 0, scale);
+            CHECK_LAUNCH();
+        }
+        HIP_TRY(hipMemcpyAsync(out_y + r0 * g.D, c->yacc, sizeof(float) * (size_t)ny, hipMemcpyDeviceToHost, c->s));
+        HIP_TRY(hipStreamSynchronize(c->s));
+    }
+    return 0;
 }
 
 int vaeb_comm_unique_id(uint8_t out_id[128]) {

@@ -205,8 +205,18 @@ class VAEB:
         return v / x.shape[0] if self.objective == "mean_map" else v
 
     def reconstruct(self, x, n_samples=0):
-        """Decoder mean for z = mu (VAEB.reconstruct's n_samples <= 0 branch, VAEB.py:268-270)."""
-        return self._ctx.reconstruct(np.asarray(x, np.float32))
+        """VAEB.reconstruct (VAEB.py:267-300): the decoder mean at z = mu for n_samples <= 0,
+        else the decoder output averaged over n_samples posterior draws.  The continuous
+        decoder returns the (averaged) decoder mean: the reference's closing
+        multivariate_normal draw over a [rows x D] mean cannot run."""
+        x = np.asarray(x, np.float32)
+        if n_samples <= 0:
+            return self._ctx.reconstruct(x)
+        if self._stream is not None:
+            # one srng.normal draw per sample (VAEB.py:280), rows stacked sample-major
+            self._ctx.push_eps(np.concatenate([self._stream.draw(x.shape[0], self.n_latent)
+                                               for _ in range(n_samples)], axis=1))
+        return self._ctx.reconstruct_sampled(x, n_samples)
 
     # ------------------------------------------------------------------ checkpoints
     def save(self, file_name):
