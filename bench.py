@@ -13,6 +13,7 @@ Configs (BASELINE.json):
                  bf16 MFMA operands / fp32 accumulation and master weights
 
 Usage:  python bench.py [--gpus N] [--steps K] [--warmup W] [--config mnist|synth]
+                       [--scaling weak|strong]
         (N > 1: torch.distributed.run, one process per GPU)
 Prints ONE JSON line on rank 0.
 """
@@ -164,6 +165,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=10.0)
+    ap.add_argument("--scaling", choices=["weak", "strong"], default="weak",
+                    help="weak: B rows per GPU (default); strong: one B-row global minibatch split "
+                         "contiguously over the ranks (100 over 8 = 13,13,13,13,12,12,12,12; SURVEY 8(e))")
     args = ap.parse_args()
     C = CONFIGS[args.config]
     steps = args.steps if args.steps is not None else C["steps"]
@@ -181,10 +185,11 @@ def main():
 
     from oracle import vaeb_oracle as O  # synthetic data generator + initial theta (not the compute path)
     from vaeb_amd import _lib
+    from vaeb_amd.dp import row_split
 
     D, H, Z = C["D"], C["H"], C["Z"]
     B = args.batch if args.batch is not None else C["B"]
-    Bg = B * world
+    B, row_off, Bg = row_split(B, world, rank, args.scaling)
     N = max(C["N"], 4 * Bg)
     bf16 = C["dtype"] == "bf16"
     if bf16:
@@ -193,7 +198,7 @@ def main():
     else:
         x = O.synthetic_mnist(n=N, D=D)
     cfg = O.Config(D=D, H=H, Z=Z)
-    ctx = _lib.Context(D, H, Z, B, B_global=Bg, row_offset=rank * B, device=local,
+    ctx = _lib.Context(D, H, Z, B, B_global=Bg, row_offset=row_off, device=local,
                        use_graph=not args.no_graph, max_eval_rows=B if bf16 else 1000,
                        dtype=_lib.DTYPE_BF16 if bf16 else _lib.DTYPE_F32)
     if world > 1:
@@ -246,14 +251,14 @@ def main():
 
     res = {
         "metric": C["metric"],
-        "value": world * B * steps / el,
+        "value": Bg * steps / el,
         "unit": "images/s",
         "n_gpus": world,
         "steps": steps,
         "warmup": warmup,
         "ms_per_step": el / steps * 1e3,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": args.scaling,
         "vs_baseline": None,
         "dtype": C["dtype"],
         "data": (f"synthetic {'Bernoulli(0.5)' if bf16 else 'MNIST-shaped binary'} pixels (N={N}, D={D}), "

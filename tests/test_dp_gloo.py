@@ -14,6 +14,7 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 from oracle import vaeb_oracle as O
+from vaeb_amd.dp import row_split
 
 
 def _rank_main(rank, world, port, mode, q):
@@ -22,14 +23,15 @@ def _rank_main(rank, world, port, mode, q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     cfg = O.Config(D=40, H=24, Z=5, L=2 if mode == "L2" else 1,
                    continuous=(mode == "gauss"), estimator="LA" if mode == "LA" else "LB")
-    B = 12  # per rank (weak scaling: B_global = B * world, row_offset = rank * B)
+    # weak scaling: 12 rows per rank; strong: a 25-row global batch split 13 / 12
+    B, off, Bg = row_split(25 if mode == "strong" else 12, world, rank, "strong" if mode == "strong" else "weak")
     rng = np.random.default_rng(0)
     params = [(rng.standard_normal(s) * 0.2).astype(np.float64) for _, s in O.param_shapes(cfg)]
-    xg = rng.random((B * world, cfg.D))
+    xg = rng.random((Bg, cfg.D))
     if not cfg.continuous:
         xg = (xg < 0.4).astype(np.float64)
-    epsg = rng.standard_normal((cfg.L, B * world, cfg.Z))
-    rows = slice(rank * B, (rank + 1) * B)
+    epsg = rng.standard_normal((cfg.L, Bg, cfg.Z))
+    rows = slice(off, off + B)
     out = O.forward_backward(params, xg[rows], epsg[:, rows], cfg)
     flat = torch.tensor(np.concatenate([g.ravel() for g in out["data_grads"]] + [[out["sgvb"]]]))
     dist.all_reduce(flat, op=dist.ReduceOp.SUM)
@@ -51,7 +53,7 @@ def _rank_main(rank, world, port, mode, q):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("mode", ["LB", "LA", "gauss", "L2"])
+@pytest.mark.parametrize("mode", ["LB", "LA", "gauss", "L2", "strong"])
 def test_two_rank_allreduce_equals_global_step(mode):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -73,3 +75,15 @@ def test_weak_scaling_row_map():
     B, W, b = 100, 8, 17
     cover = np.concatenate([np.arange(b * B * W + r * B, b * B * W + (r + 1) * B) for r in range(W)])
     assert np.array_equal(cover, np.arange(b * B * W, (b + 1) * B * W))
+
+
+def test_strong_scaling_row_map():
+    """bench.py --scaling strong: a 100-row global minibatch over 8 ranks is
+    13,13,13,13,12,12,12,12 contiguous rows, covering it exactly once."""
+    parts = [row_split(100, 8, r, "strong") for r in range(8)]
+    assert [p[0] for p in parts] == [13, 13, 13, 13, 12, 12, 12, 12]
+    assert all(p[2] == 100 for p in parts)
+    cover = np.concatenate([np.arange(off, off + n) for n, off, _ in parts])
+    assert np.array_equal(cover, np.arange(100))
+    with pytest.raises(ValueError):
+        row_split(4, 8, 0, "strong")
