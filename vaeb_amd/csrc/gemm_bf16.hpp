@@ -239,12 +239,34 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_kernel(GemmArgs g, Epi e) {
     };
     // Ring of 4 LDS stages, prefetch distance 3: tiles t+1..t+3 stream in while tile t is
     // multiplied.  Each wave waits only for its own pieces of tile t + 1 (counted vmcnt:
-    // the pieces of the tiles issued after it stay in flight) before the step's one
-    // barrier, and a stage is read only after the barrier that follows that wait (guide
-    // §5, "Read a staged buffer one phase AFTER the wait that retires it").  Raw s_barrier:
-    // __syncthreads() would drain every LDS-DMA (vmcnt(0)).
+    // the pieces of the tiles issued after it stay in flight) before a barrier, and a stage
+    // is read only after the barrier that follows that wait (guide §5, "Read a staged
+    // buffer one phase AFTER the wait that retires it").  Raw s_barrier: __syncthreads()
+    // would drain every LDS-DMA (vmcnt(0)); sched_barrier keeps hipcc from moving MFMAs
+    // across the barriers.
+    //
+    // 256-wide tiles (PP): two wave groups in ping-pong (guide §5 "256² 8-phase
+    // template": its staggered wave rows).  Group g = wave >> 2 puts one wave of each group
+    // on every SIMD; group 1 runs one barrier behind group 0, so in every barrier interval
+    // one group reads its fragments from LDS while the other issues its MFMAs, and each
+    // SIMD's MFMA pipe alternates between its two waves.  Iteration t of a wave:
+    //   R: issue the DMA of tile t + 3; ds_read tile t's fragments; wait for its own
+    //      pieces of tile t + 1 and for its reads;  barrier;  M: MFMAs;  barrier.
+    // Ordering (barrier numbers #k; group 0's R(t) lies between #2t and #2t + 1, group 1's
+    // between #2t + 1 and #2t + 2): tile t + 1 is certified by both groups before #2t + 2,
+    // ahead of every read of it; tile t - 1's stage, refilled by the DMA of tile t + 3
+    // after #2t, was last read before #2t.
+    // 256 x 128 tiles (64 x 64 per wave, 16 MFMAs per K-tile) measured 10-40 % slower with
+    // the ping-pong, so there all waves run R, M, then certify tile t + 1 and barrier once.
+    constexpr bool PP = BNT == 256;
+    const int grp = wave >> 2;
     for (int t = 0; t < 3 && t < nkt; ++t) issue(t);
-    ring_wait<S::kPieces>(min(nkt - 1, 2));
+    ring_wait<S::kPieces>(min(nkt, 3) - 1);   // tile 0 certified
+    __builtin_amdgcn_sched_barrier(0);
+    if (PP && grp == 1) {
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+    }
     for (int t = 0; t < nkt; ++t) {
         if (t + 3 < nkt) issue(t + 3);
         const char* As = stage(t % kStages);
@@ -254,6 +276,10 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_kernel(GemmArgs g, Epi e) {
         for (int i = 0; i < TM; ++i) af[i] = frag<LA, BM>(As, wm * (16 * TM) + 16 * i, 0, lane);
 #pragma unroll
         for (int j = 0; j < TN; ++j) bfr[j] = frag<LB, BNT>(Bs, wn * (16 * TN) + 16 * j, 0, lane);
+        if constexpr (PP) {
+            ring_wait<S::kPieces>(max(0, min(nkt - 1, t + 3) - (t + 1)));
+            __builtin_amdgcn_sched_barrier(0);
+        }
         __builtin_amdgcn_s_setprio(1);   // keeps the MFMA cluster between the barriers (guide T5)
 #pragma unroll
         for (int i = 0; i < TM; ++i)
@@ -261,8 +287,15 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_kernel(GemmArgs g, Epi e) {
             for (int j = 0; j < TN; ++j)
                 acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
         __builtin_amdgcn_s_setprio(0);
-        ring_wait<S::kPieces>(min(nkt - 1, t + 3) - (t + 1));
+        if constexpr (PP) {
+            __builtin_amdgcn_sched_barrier(0);
+            __builtin_amdgcn_s_barrier();
+            __builtin_amdgcn_sched_barrier(0);
+        } else {
+            ring_wait<S::kPieces>(min(nkt - 1, t + 3) - (t + 1));
+        }
     }
+    if (PP && grp == 0) __builtin_amdgcn_s_barrier();   // re-align the groups' barrier counts
     // Epilogue.  The LDS is free again (the loop ended on a barrier with nothing in
     // flight): epilogues with a bf16 input tile (x, h, hd at the output positions) fetch
     // it with coalesced 16-B loads into a padded LDS tile; bf16 results go back through the
