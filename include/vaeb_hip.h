@@ -187,6 +187,11 @@ int vaeb_ae_decode(vaeb_ae* ae, const float* z, int64_t n, float* out);        /
  * context's device and stream. */
 int vaeb_test_gemm_bf16(vaeb_ctx* ctx, int32_t a_kouter, int32_t b_kouter, int32_t M, int32_t N, int32_t K,
                         const float* A, const float* B, float* C, int32_t ksplit);
+/* Diagnostics: mean time (ms) of `reps` back-to-back launches of the bf16 GEMM on
+ * device-generated uniform [-1, 1) operands of the given layouts, bias + bf16-store
+ * epilogue; tile width 128 / 256 (0: the engine's choice). */
+int vaeb_bench_gemm_bf16(vaeb_ctx* ctx, int32_t a_kouter, int32_t b_kouter, int32_t M, int32_t N, int32_t K,
+                         int32_t tile_n, int32_t reps, float* out_ms);
 
 #ifdef __cplusplus
 }

@@ -63,6 +63,10 @@ CASES = [
     ("bern_LA_L2", dict(D=128, H=64, Z=16, estimator="LA", L=2), 136),
     ("gauss_mean_map", dict(D=128, H=64, Z=8, continuous=True, objective="mean_map"), 128),
     ("synth_shape_small_batch", dict(D=4096, H=2048, Z=128), 128),
+    # long-K weight gradients (K = L * B >= 1024) with row / column / K tails
+    ("bern_LB_longk", dict(D=512, H=256, Z=32), 1024),
+    ("gauss_LA_L2_longk", dict(D=256, H=256, Z=16, continuous=True, estimator="LA", L=2), 1024),
+    ("bern_LB_longk_tails", dict(D=520, H=264, Z=24), 1100),
 ]
 
 

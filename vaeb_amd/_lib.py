@@ -28,7 +28,7 @@ EXPORTS = [
     "vaeb_push_eps", "vaeb_set_step", "vaeb_update", "vaeb_update_async", "vaeb_update_many",
     "vaeb_epoch_elbo", "vaeb_synchronize", "vaeb_validate", "vaeb_reconstruct", "vaeb_reconstruct_sampled",
     "vaeb_comm_unique_id", "vaeb_comm_init", "vaeb_get_grads", "vaeb_get_activation",
-    "vaeb_profile_steps", "vaeb_kernel_name", "vaeb_debug_timeline", "vaeb_test_gemm_bf16",
+    "vaeb_profile_steps", "vaeb_kernel_name", "vaeb_debug_timeline", "vaeb_test_gemm_bf16", "vaeb_bench_gemm_bf16",
     "vaeb_ae_create", "vaeb_ae_destroy", "vaeb_ae_num_params", "vaeb_ae_set_data", "vaeb_ae_set_params",
     "vaeb_ae_get_params", "vaeb_ae_set_adagrad_state", "vaeb_ae_get_adagrad_state", "vaeb_ae_train",
     "vaeb_ae_train_many", "vaeb_ae_reconstruct", "vaeb_ae_encode", "vaeb_ae_decode",
@@ -111,6 +111,7 @@ def load():
         "vaeb_debug_timeline": ([_P, ctypes.c_int32, ctypes.POINTER(ctypes.c_uint64), _I64,
                                  ctypes.POINTER(ctypes.c_int32)], ctypes.c_int),
         "vaeb_test_gemm_bf16": ([_P] + [ctypes.c_int32] * 5 + [_F, _F, _F, ctypes.c_int32], ctypes.c_int),
+        "vaeb_bench_gemm_bf16": ([_P] + [ctypes.c_int32] * 7 + [_F], ctypes.c_int),
         "vaeb_ae_create": ([ctypes.POINTER(AEConfigC), ctypes.POINTER(_P)], ctypes.c_int),
         "vaeb_ae_destroy": ([_P], ctypes.c_int),
         "vaeb_ae_num_params": ([_P, ctypes.POINTER(_I64)], ctypes.c_int),
@@ -281,6 +282,13 @@ class Context:
     def comm_init(self, uid: bytes, rank, world):
         buf = (ctypes.c_uint8 * 128).from_buffer_copy(uid)
         check(self.lib.vaeb_comm_init(self.h, buf, rank, world))
+
+    def bench_gemm_bf16(self, a_kouter, b_kouter, M, N, K, tile_n=0, reps=10):
+        """Mean ms per launch of the bf16 GEMM on device-generated operands (diagnostics)."""
+        out = ctypes.c_float()
+        check(self.lib.vaeb_bench_gemm_bf16(self.h, int(a_kouter), int(b_kouter), M, N, K, int(tile_n), int(reps),
+                                            ctypes.byref(out)))
+        return out.value
 
     def test_gemm_bf16(self, A, B, a_kouter, b_kouter, M, N, K, ksplit=1):
         """bf16 GEMM engine test hook: C[M x N] = sum_k A(m,k) B(k,n); A stored [M,K] or

@@ -600,6 +600,7 @@ struct Opt {
     bf16_t* shadow_out;   // bf16 copy of theta' in GEMM layout (index m * N + n)
     float lr, eps, prior, decay;
     int update, store_grad;
+    int64_t n;            // arena elements (buffer-descriptor extent)
     DEV void apply(int64_t idx, int64_t sidx, float dsg) const {   // sidx < 0: no shadow
         if (store_grad) grad[idx] = dsg;
         if (!update) return;
@@ -617,17 +618,46 @@ struct Opt {
 struct EpiAdagrad {
     static constexpr bool kIn = false, kOut = false;
     ColMap map; Opt opt; int M, N;
+    // The optimizer rule of Opt::apply on the wave's 64 x 64 block, one 16-row fragment
+    // row (16 elements per lane) per memory round trip: all theta / accumulator loads of
+    // the fragment row are issued before its stores (buffer loads, masked elements read
+    // out of range), instead of a load -> store chain per element that hipcc cannot
+    // reorder (theta_in / accum may alias the stores, as far as it can tell).
     DEV void operator()(int mw, int nw, f32x4 (&acc)[4][4], int, char*) const {
         const int lane = threadIdx.x & 63;
+        const rsrc_t bth = mkbuf(opt.th_in, opt.n * 4), bac = mkbuf(opt.accum, opt.n * 4);
+        const rsrc_t bto = mkbuf(opt.th_out, opt.n * 4), bgr = mkbuf(opt.grad, opt.n * 4);
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
+        for (int i = 0; i < 4; ++i) {
+            uint32_t off[4][4];
+            float th[4][4], ac[4][4];
 #pragma unroll
             for (int j = 0; j < 4; ++j)
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     const int row = erow(mw, i, r, lane), col = ecol(nw, j, lane);
-                    if (row < M && col < N) opt.apply(map.at(row, col), (int64_t)row * N + col, acc[i][j][r]);
+                    off[j][r] = (row < M && col < N) ? (uint32_t)map.at(row, col) * 4u : kOOB;
+                    th[j][r] = bld(bth, opt.update ? off[j][r] : kOOB);
+                    ac[j][r] = bld(bac, opt.update ? off[j][r] : kOOB);
                 }
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int row = erow(mw, i, r, lane), col = ecol(nw, j, lane);
+                    const float dsg = acc[i][j][r];
+                    if (opt.store_grad) bst(bgr, off[j][r], dsg);
+                    if (opt.update) {
+                        const float gg = dsg - opt.prior * th[j][r];
+                        const float a = ac[j][r] + gg * gg;
+                        const float tn = th[j][r] + opt.lr * gg / (__builtin_amdgcn_sqrtf(a) + opt.eps) -
+                                         opt.decay * th[j][r] * th[j][r];
+                        bst(bac, off[j][r], a);
+                        bst(bto, off[j][r], tn);
+                        if (off[j][r] != kOOB) opt.shadow_out[(int64_t)row * N + col] = (bf16_t)f2bf(tn);
+                    }
+                }
+        }
     }
 };
 

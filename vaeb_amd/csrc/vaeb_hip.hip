@@ -1131,6 +1131,73 @@ int vaeb_test_gemm_bf16(vaeb_ctx* c, int32_t ako, int32_t bko, int32_t M, int32_
     return rc;
 }
 
+extern "C++" {
+// Diagnostics: device-side uniform [-1, 1) bf16 fill (a hash of the index), no host copy.
+__global__ __launch_bounds__(256) void fill_bf16_kernel(bf16_t* p, int64_t n, uint32_t seed) {
+    const int64_t stride = (int64_t)gridDim.x * 256;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) {
+        uint32_t h = (uint32_t)i * 0x9E3779B1u ^ seed;
+        h ^= h >> 15; h *= 0x2C1B3C6Du; h ^= h >> 12; h *= 0x297A2D39u; h ^= h >> 15;
+        p[i] = (bf16_t)bf::f2bf((float)(h >> 8) * (2.0f / 16777216.0f) - 1.0f);
+    }
+}
+
+template <int LA, int LB>
+static int bench_gemm_launch(hipStream_t s, const bf16_t* A, const bf16_t* B, int M, int N, int K, int bn,
+                             const bf::EpiBiasAct& e) {
+    bf::GemmArgs g{};
+    g.A = A; g.lda = LA == bf::KO ? M : K; g.a_bytes = (int64_t)M * K * 2;
+    g.B = B; g.ldb = LB == bf::KO ? N : K; g.b_bytes = (int64_t)N * K * 2;
+    g.M = M; g.N = N; g.K = K;
+    g.tiles_m = cdiv(M, bf::BM); g.tiles_n = cdiv(N, bn);
+    g.kslice = ((K + bf::BK - 1) / bf::BK) * bf::BK;
+    if (bn == 256) return bf_launch<LA, LB, 256>(s, g, 1, e);
+    return bf_launch<LA, LB, 128>(s, g, 1, e);
+}
+}  // extern "C++"
+
+int vaeb_bench_gemm_bf16(vaeb_ctx* c, int32_t ako, int32_t bko, int32_t M, int32_t N, int32_t K, int32_t bn,
+                         int32_t reps, float* out_ms) {
+    if (!c || !out_ms || M <= 0 || N <= 0 || K <= 0 || reps <= 0) return fail(VAEB_ERR_ARG, "bad arguments");
+    if (K % 8 || M % 8 || N % 8) return fail(VAEB_ERR_ARG, "bench gemm: M, N, K must be multiples of 8");
+    if (bn == 0) bn = bf_bn(M, N);
+    if (bn != 128 && bn != 256) return fail(VAEB_ERR_ARG, "bench gemm: tile width 128 or 256");
+    bf16_t *a = nullptr, *b = nullptr, *o = nullptr;
+    float* bias = nullptr;
+    int rc = 0;
+    rc = rc ? rc : dalloc(&a, (size_t)M * K);
+    rc = rc ? rc : dalloc(&b, (size_t)N * K);
+    rc = rc ? rc : dalloc(&o, (size_t)M * N);
+    rc = rc ? rc : dalloc(&bias, (size_t)N);
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (!rc) {
+        hipLaunchKernelGGL(fill_bf16_kernel, dim3(1024), dim3(256), 0, c->s, a, (int64_t)M * K, 1u);
+        hipLaunchKernelGGL(fill_bf16_kernel, dim3(1024), dim3(256), 0, c->s, b, (int64_t)N * K, 2u);
+        const bf::EpiBiasAct e{bias, 0, M, N, o, N};
+        auto one = [&]() {
+            if (!ako && !bko) return bench_gemm_launch<bf::KC, bf::KC>(c->s, a, b, M, N, K, bn, e);
+            if (!ako && bko) return bench_gemm_launch<bf::KC, bf::KO>(c->s, a, b, M, N, K, bn, e);
+            if (ako && !bko) return bench_gemm_launch<bf::KO, bf::KC>(c->s, a, b, M, N, K, bn, e);
+            return bench_gemm_launch<bf::KO, bf::KO>(c->s, a, b, M, N, K, bn, e);
+        };
+        rc = one();   // warm-up
+        hipEventCreate(&e0);
+        hipEventCreate(&e1);
+        hipEventRecord(e0, c->s);
+        for (int r = 0; !rc && r < reps; ++r) rc = one();
+        hipEventRecord(e1, c->s);
+        if (!rc && hipEventSynchronize(e1) == hipSuccess) {
+            float ms = 0.f;
+            hipEventElapsedTime(&ms, e0, e1);
+            *out_ms = ms / (float)reps;
+        }
+    }
+    if (e0) hipEventDestroy(e0);
+    if (e1) hipEventDestroy(e1);
+    for (void* p : {(void*)a, (void*)b, (void*)o, (void*)bias}) if (p) hipFree(p);
+    return rc;
+}
+
 int vaeb_kernel_name(int32_t id, char* out, int32_t cap) {
     if (!out || cap <= 0) return fail(VAEB_ERR_ARG, "bad buffer");
     const int n = (int)(sizeof(kKernelNames) / sizeof(kKernelNames[0]));
