@@ -9,10 +9,11 @@ minibatch and the gradients are all-reduced over RCCL ("weak" scaling).
 
 Configs (BASELINE.json):
   --config mnist (default, the headline metric): 784-500-20 Bernoulli, B=100, fp32 MFMA
+  --config frey  (Frey-shaped, BASELINE config 1 shapes): 560-200-2 Gaussian decoder, B=100, fp32
   --config synth (config 5, roofline stress): 4096-2048-128 Bernoulli, B=8192 per GPU,
                  bf16 MFMA operands / fp32 accumulation and master weights
 
-Usage:  python bench.py [--gpus N] [--steps K] [--warmup W] [--config mnist|synth]
+Usage:  python bench.py [--gpus N] [--steps K] [--warmup W] [--config mnist|frey|synth]
                        [--scaling weak|strong]
         (N > 1: torch.distributed.run, one process per GPU)
 Prints ONE JSON line on rank 0.
@@ -88,6 +89,7 @@ KERNEL_SYMBOLS = {"p1_enc": "PEnc", "p23_heads_dechid": "heads_dechid_kernel", "
                   "bf_dhd": ("gemm_kernel<0, 0,", "EpiDTanh>"), "bf_dW26": ("EpiAdagrad",),
                   "bf_dW3": ("EpiAdagrad",)}
 PMC_FILES = {"mnist": os.path.join(ROOT, "profiles", "r1", "pmc_per_launch.json"),
+             "frey": os.path.join(ROOT, "profiles", "r1", "pmc_frey_per_launch.json"),
              "synth": os.path.join(ROOT, "profiles", "r1", "pmc_synth_per_launch.json")}
 
 
@@ -109,7 +111,7 @@ def committed_traffic(kernel, path=PMC_FILES["mnist"], symbols=KERNEL_SYMBOLS):
     return None
 
 
-def cpu_baseline(D, H, Z, B, x, budget_s=10.0, max_steps=20000):
+def cpu_baseline(D, H, Z, B, x, budget_s=10.0, max_steps=20000, continuous=False):
     """The oracle's float32 NumPy restatement of the same step, on the host cores."""
     from oracle import vaeb_oracle as O
     try:
@@ -117,7 +119,7 @@ def cpu_baseline(D, H, Z, B, x, budget_s=10.0, max_steps=20000):
     except Exception:  # pragma: no cover
         threadpool_limits = None
     threads = min(16, os.cpu_count() or 1)
-    cfg = O.Config(D=D, H=H, Z=Z)
+    cfg = O.Config(D=D, H=H, Z=Z, continuous=continuous)
     params = O.init_params(cfg)
     acc = [np.zeros_like(p) for p in params]
     rng = np.random.default_rng(0)
@@ -148,6 +150,10 @@ CONFIGS = {
     "mnist": dict(D=784, H=500, Z=20, B=100, N=50000, dtype="f32", steps=2000, warmup=200,
                   metric="SGVB training images/sec + ELBO at MNIST 784-500-20, batch 100",
                   workload="MNIST 784-500-20 Bernoulli decoder, LB estimator, L=1, Adagrad lr 0.01"),
+    "frey": dict(D=560, H=200, Z=2, B=100, N=1500, dtype="f32", steps=2000, warmup=200, continuous=True,
+                 metric="SGVB training images/sec + ELBO at Frey-shaped 560-200-2 (Gaussian decoder), batch 100",
+                 workload="Frey-shaped 560-200-2 Gaussian decoder, LB estimator, L=1, Adagrad lr 0.01 "
+                          "(BASELINE config 1 shapes)"),
     "synth": dict(D=4096, H=2048, Z=128, B=8192, N=16 * 8192, dtype="bf16", steps=50, warmup=5,
                   metric="SGVB training images/sec, synthetic 4096-2048-128, batch 8192 per GPU, bf16 MFMA",
                   workload="synthetic 4096-2048-128 Bernoulli decoder, LB, L=1, Adagrad lr 0.01, bf16 operands / "
@@ -192,13 +198,17 @@ def main():
     B, row_off, Bg = row_split(B, world, rank, args.scaling)
     N = max(C["N"], 4 * Bg)
     bf16 = C["dtype"] == "bf16"
+    gauss = C.get("continuous", False)
     if bf16:
         rng = np.random.default_rng(3)   # synth x ~ Bernoulli(0.5)
         x = (rng.random((N, D), dtype=np.float32) < 0.5).astype(np.float32)
+    elif gauss:
+        x = O.synthetic_frey(n=N, D=D)   # Frey-shaped x ~ Beta(2, 2)
     else:
         x = O.synthetic_mnist(n=N, D=D)
-    cfg = O.Config(D=D, H=H, Z=Z)
+    cfg = O.Config(D=D, H=H, Z=Z, continuous=gauss)
     ctx = _lib.Context(D, H, Z, B, B_global=Bg, row_offset=row_off, device=local,
+                       decoder=_lib.DEC_GAUSSIAN if gauss else _lib.DEC_BERNOULLI,
                        use_graph=not args.no_graph, max_eval_rows=B if bf16 else 1000,
                        dtype=_lib.DTYPE_BF16 if bf16 else _lib.DTYPE_F32)
     if world > 1:
@@ -242,12 +252,12 @@ def main():
 
     # per-kernel device time (HIP events on the context's stream), after the timed region
     prof = ctx.profile_steps(50 if not bf16 else 5)
-    fl = phase_flops(D, H, Z, B)
+    fl = phase_flops(D, H, Z, B, gaussian=gauss)
     dom = max((k for k in prof if k[0] in fl), key=lambda k: k[1])
     achieved = fl[dom[0]] / (dom[1] * 1e-3) / 1e12
     traffic = committed_traffic(dom[0], PMC_FILES[args.config])
     peak = PEAK_BF16_TFLOPS if bf16 else PEAK_F32_TFLOPS
-    sflops = step_flops(D, H, Z, B)
+    sflops = step_flops(D, H, Z, B, gaussian=gauss)
 
     res = {
         "metric": C["metric"],
@@ -261,7 +271,8 @@ def main():
         "scaling": args.scaling,
         "vs_baseline": None,
         "dtype": C["dtype"],
-        "data": (f"synthetic {'Bernoulli(0.5)' if bf16 else 'MNIST-shaped binary'} pixels (N={N}, D={D}), "
+        "data": (f"synthetic {'Bernoulli(0.5)' if bf16 else ('Frey-shaped Beta(2,2)' if gauss else 'MNIST-shaped binary')}"
+                 f" pixels (N={N}, D={D}), "
                  f"resident in HBM; random init RandomState(10)"),
         "config": {"workload": C["workload"], "global_batch": Bg, "batch_per_gpu": B, "seq_len": None,
                    "parallelism": f"dp{world}"},
@@ -276,7 +287,7 @@ def main():
         if bf16:
             res["cpu_baseline"] = cpu_baseline(D, H, Z, B, x[:4 * B], budget_s=args.cpu_budget * 2, max_steps=8)
         else:
-            res["cpu_baseline"] = cpu_baseline(D, H, Z, B, x, budget_s=args.cpu_budget)
+            res["cpu_baseline"] = cpu_baseline(D, H, Z, B, x, budget_s=args.cpu_budget, continuous=gauss)
     if rank == 0:
         print(json.dumps(res), flush=True)
     ctx.close()
