@@ -48,7 +48,6 @@ enum : int { KC = 0, KO = 1 };
 // chip).  BN is the widest tile (it sizes the epilogue LDS tile).
 constexpr int BM = 256, BN = 256, BK = 32, NTHR = 512, NWAVE = 8;
 constexpr int kATileBytes = BM * BK * 2;         // A operand tile image (16 KiB)
-constexpr int kStages = 4;                       // prefetch distance 3
 template <int BNT>
 struct Shape {
     static constexpr int WGN = BNT / 64, WGM = NWAVE / WGN;   // wave grid
@@ -56,6 +55,12 @@ struct Shape {
     static constexpr int kB = BNT * BK * 2;                   // B operand tile image
     static constexpr int kStage = kATileBytes + kB;
     static constexpr int kPieces = (kATileBytes + kB) / 1024 / NWAVE;   // vmcnt unit per tile
+    // LDS ring: 4 stages (prefetch distance 3), one block per CU.  Measured and rejected:
+    // a 3-stage ring on the 256 x 128 tile (72 KiB with its epilogue tile, <= 128 VGPRs,
+    // two blocks per CU so one block's epilogue overlaps the other's mainloop) -- the
+    // weight-gradient launches went from 161-169 to 171-183 us.
+    static constexpr int kStages = 4;
+    static constexpr int kBlocksPerCU = 1;
 };
 
 // f32 -> bf16, round to nearest even (inputs here are finite)
@@ -207,7 +212,7 @@ DEV void ring_wait(int after) {   // wait for all but `after` tiles' worth of LD
 }
 
 template <int LA, int LB, int BNT, class Epi>
-__global__ __launch_bounds__(NTHR, 1) void gemm_kernel(GemmArgs g, Epi e) {
+__global__ __launch_bounds__(NTHR, 2 * Shape<BNT>::kBlocksPerCU) void gemm_kernel(GemmArgs g, Epi e) {
     using S = Shape<BNT>;
     constexpr int TM = S::TM, TN = S::TN;
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -233,7 +238,7 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_kernel(GemmArgs g, Epi e) {
     const int nkt = (kend - kbeg + BK - 1) / BK;
     auto stage = [&](int s) { return smem + s * S::kStage; };
     auto issue = [&](int t) {
-        char* st = stage(t % kStages);
+        char* st = stage(t % S::kStages);
         la.issue(st, kbeg + t * BK, wave, lane);
         lb.issue(st + kATileBytes, kbeg + t * BK, wave, lane);
     };
@@ -259,17 +264,18 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_kernel(GemmArgs g, Epi e) {
     // 256 x 128 tiles (64 x 64 per wave, 16 MFMAs per K-tile) measured 10-40 % slower with
     // the ping-pong, so there all waves run R, M, then certify tile t + 1 and barrier once.
     constexpr bool PP = BNT == 256;
+    constexpr int PD = S::kStages - 1;   // prefetch distance
     const int grp = wave >> 2;
-    for (int t = 0; t < 3 && t < nkt; ++t) issue(t);
-    ring_wait<S::kPieces>(min(nkt, 3) - 1);   // tile 0 certified
+    for (int t = 0; t < PD && t < nkt; ++t) issue(t);
+    ring_wait<S::kPieces>(min(nkt, PD) - 1);   // tile 0 certified
     __builtin_amdgcn_sched_barrier(0);
     if (PP && grp == 1) {
         __builtin_amdgcn_s_barrier();
         __builtin_amdgcn_sched_barrier(0);
     }
     for (int t = 0; t < nkt; ++t) {
-        if (t + 3 < nkt) issue(t + 3);
-        const char* As = stage(t % kStages);
+        if (t + PD < nkt) issue(t + PD);
+        const char* As = stage(t % S::kStages);
         const char* Bs = As + kATileBytes;
         bf16x8 af[TM], bfr[TN];
 #pragma unroll
@@ -277,7 +283,7 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_kernel(GemmArgs g, Epi e) {
 #pragma unroll
         for (int j = 0; j < TN; ++j) bfr[j] = frag<LB, BNT>(Bs, wn * (16 * TN) + 16 * j, 0, lane);
         if constexpr (PP) {
-            ring_wait<S::kPieces>(max(0, min(nkt - 1, t + 3) - (t + 1)));
+            ring_wait<S::kPieces>(max(0, min(nkt - 1, t + PD) - (t + 1)));
             __builtin_amdgcn_sched_barrier(0);
         }
         __builtin_amdgcn_s_setprio(1);   // keeps the MFMA cluster between the barriers (guide T5)
@@ -292,7 +298,7 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_kernel(GemmArgs g, Epi e) {
             __builtin_amdgcn_s_barrier();
             __builtin_amdgcn_sched_barrier(0);
         } else {
-            ring_wait<S::kPieces>(min(nkt - 1, t + 3) - (t + 1));
+            ring_wait<S::kPieces>(max(0, min(nkt - 1, t + PD) - (t + 1)));
         }
     }
     if (PP && grp == 0) __builtin_amdgcn_s_barrier();   // re-align the groups' barrier counts
@@ -306,15 +312,15 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_kernel(GemmArgs g, Epi e) {
     }
     const int mw = m0 + wm * (16 * TM), nw = n0 + wn * (16 * TN);
     if constexpr (TM == 4) {
-        e(mw, nw, acc, kz, smem);
+        e.template apply<BNT>(mw, nw, acc, kz, smem);
     } else {
         f32x4 lo[4][4], hi[4][4];
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
             for (int j = 0; j < 4; ++j) { lo[i][j] = acc[i][j]; hi[i][j] = acc[i + 4][j]; }
-        e(mw, nw, lo, kz, smem);
-        e(mw + 64, nw, hi, kz, smem);
+        e.template apply<BNT>(mw, nw, lo, kz, smem);
+        e.template apply<BNT>(mw + 64, nw, hi, kz, smem);
     }
     if constexpr (Epi::kOut) {
         __syncthreads();
@@ -337,29 +343,30 @@ DEV float colsum_lanes(float s) {
 }
 
 // ------------------------------------------------------------------ epilogue tiles
-// A BM x BN bf16 tile in LDS with a 544-B row pitch: the four 16-lane groups of a
-// per-element access (rows 4(l>>4)+r, 16 consecutive columns) land on disjoint banks.
-constexpr int kEP = BN * 2 + 32;          // 544 B: 136 dwords = 8 (mod 32)
-constexpr int kEpiTileBytes = BM * kEP;   // 136 KiB
+// A BM x W bf16 tile in LDS (W = the block's tile width) with a 2W + 32-byte row pitch
+// (544 or 288 B, 8 (mod 32) dwords): the four 16-lane groups of a per-element access
+// (rows 4(l>>4)+r, 16 consecutive columns) land on disjoint banks.
+template <int W> constexpr int epitch() { return W * 2 + 32; }
 template <int BNT>
 constexpr int lds_bytes() {
-    return kStages * Shape<BNT>::kStage > kEpiTileBytes ? kStages * Shape<BNT>::kStage : kEpiTileBytes;
+    constexpr int ring = Shape<BNT>::kStages * Shape<BNT>::kStage, epi = BM * epitch<BNT>();
+    return ring > epi ? ring : epi;   // 128 KiB / 136 KiB at 256 wide, 72 KiB at 128
 }
-DEV int eoff(int row, int col) { return row * kEP + col * 2; }
-DEV float lds_bf(const char* t, int row, int col) {
-    return bf2f(*reinterpret_cast<const uint16_t*>(t + eoff(row, col)));
+template <int W> DEV int eoff(int row, int col) { return row * epitch<W>() + col * 2; }
+template <int W> DEV float lds_bf(const char* t, int row, int col) {
+    return bf2f(*reinterpret_cast<const uint16_t*>(t + eoff<W>(row, col)));
 }
-DEV void lds_st_bf(char* t, int row, int col, float v) {
-    *reinterpret_cast<uint16_t*>(t + eoff(row, col)) = (uint16_t)f2bf(v);
+template <int W> DEV void lds_st_bf(char* t, int row, int col, float v) {
+    *reinterpret_cast<uint16_t*>(t + eoff<W>(row, col)) = (uint16_t)f2bf(v);
 }
-// Cooperative tile copies: rows [0, 128) x columns [0, W) of the tile at (r0, c0) of a
-// [rows x ld] bf16 matrix; rows >= rlim or columns >= clim read 0 / are not stored
-// (clim % 8 == 0).  rmod > 0: source row = (r0 + row) % rmod (the L noise planes share
-// the data rows).  GI: source column c goes to tile column (c & 31) + 64 (c >> 5) -- the
-// W2 slots of the Gaussian decoder's 32-column interleave.
-template <int W, bool GI = false>
-DEV void tile_load(char* t, rsrc_t src, int ld, int r0, int c0, int rlim, int clim, int rmod, int lc0) {
-    constexpr int CPR = W / 8;                 // 16-B chunks per row
+// Cooperative tile copies: rows [0, BM) x columns [0, CW) of the tile at (r0, c0) of a
+// [rows x ld] bf16 matrix into / out of the W-wide LDS tile; rows >= rlim or columns >=
+// clim read 0 / are not stored (clim % 8 == 0).  rmod > 0: source row = (r0 + row) % rmod
+// (the L noise planes share the data rows).  GI: source column c goes to tile column
+// (c & 31) + 64 (c >> 5) -- the W2 slots of the Gaussian decoder's 32-column interleave.
+template <int CW, int W, bool GI = false>
+DEV void tile_load(char* t, rsrc_t src, int ld, int r0, int c0, int rlim, int clim, int rmod) {
+    constexpr int CPR = CW / 8;                // 16-B chunks per row
     constexpr int N = BM * CPR / NTHR;
 #pragma unroll
     for (int i = 0; i < N; ++i) {
@@ -369,12 +376,12 @@ DEV void tile_load(char* t, rsrc_t src, int ld, int r0, int c0, int rlim, int cl
         const int sr = rmod > 0 ? gr % rmod : gr;
         const uint32_t off = (gr < rlim && gc < clim) ? ((uint32_t)sr * (uint32_t)ld + (uint32_t)gc) * 2u : kOOB;
         const v4u v = __builtin_bit_cast(v4u, __builtin_amdgcn_raw_buffer_load_b128(src, off, 0, 0));
-        const int tc = lc0 + (GI ? ((ch * 8) & 31) + ((ch * 8) >> 5) * 64 : ch * 8);
-        *reinterpret_cast<v4u*>(t + row * kEP + tc * 2) = v;
+        const int tc = GI ? ((ch * 8) & 31) + ((ch * 8) >> 5) * 64 : ch * 8;
+        *reinterpret_cast<v4u*>(t + row * epitch<W>() + tc * 2) = v;
     }
 }
 template <int W>
-DEV void tile_store(const char* t, bf16_t* dst, int ld, int r0, int c0, int rlim, int clim, int lc0) {
+DEV void tile_store(const char* t, bf16_t* dst, int ld, int r0, int c0, int rlim, int clim) {
     constexpr int CPR = W / 8;
     constexpr int N = BM * CPR / NTHR;
 #pragma unroll
@@ -384,19 +391,21 @@ DEV void tile_store(const char* t, bf16_t* dst, int ld, int r0, int c0, int rlim
         const int gr = r0 + row, gc = c0 + ch * 8;
         if (gr < rlim && gc < clim)
             *reinterpret_cast<v4u*>(dst + (int64_t)gr * ld + gc) =
-                *reinterpret_cast<const v4u*>(t + row * kEP + lc0 * 2 + ch * 16);
+                *reinterpret_cast<const v4u*>(t + row * epitch<W>() + ch * 16);
     }
 }
 
 // ------------------------------------------------------------------ epilogues
-// Interface: static constexpr bool kIn, kOut;  void load_in(m0, n0, smem) (kIn);
-// void operator()(mw, nw, acc, kz, smem);  void store_out(m0, n0, smem) (kOut).
-// Wave (wm, wn)'s block starts at tile-local (64 wm, 64 wn).
+// Interface (W = the block's tile width): static constexpr bool kIn, kOut;
+// void load_in<W>(m0, n0, smem) (kIn);  void apply<W>(mw, nw, acc, kz, smem);
+// void store_out<W>(m0, n0, smem) (kOut).  A wave's 64 x 64 block starts at tile-local
+// (mw & (BM - 1), nw & (W - 1)).
 // Plain fp32 store (split-K slabs: slice kz at out + kz * slab).
 struct EpiF32 {
     static constexpr bool kIn = false, kOut = false;
     float* out; int ldo; int M, N; int64_t slab;
-    DEV void operator()(int mw, int nw, f32x4 (&acc)[4][4], int kz, char*) const {
+    template <int W>
+    DEV void apply(int mw, int nw, f32x4 (&acc)[4][4], int kz, char*) const {
         const int lane = threadIdx.x & 63;
         float* o = out + (int64_t)kz * slab;
 #pragma unroll
@@ -416,9 +425,10 @@ struct EpiBiasAct {
     static constexpr bool kIn = false, kOut = true;
     const float* bias; int tanh_act; int M, N;
     bf16_t* out; int ldo;
-    DEV void operator()(int mw, int nw, f32x4 (&acc)[4][4], int, char* smem) const {
+    template <int W>
+    DEV void apply(int mw, int nw, f32x4 (&acc)[4][4], int, char* smem) const {
         const int lane = threadIdx.x & 63;
-        const int lr0 = mw & (BM - 1), lc0 = nw & (BN - 1);
+        const int lr0 = mw & (BM - 1), lc0 = nw & (W - 1);
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             const int col = ecol(nw, j, lane);
@@ -429,12 +439,12 @@ struct EpiBiasAct {
                 for (int r = 0; r < 4; ++r) {
                     float v = acc[i][j][r] + b;
                     if (tanh_act) v = ftanh(v);
-                    lds_st_bf(smem, erow(lr0, i, r, lane), ecol(lc0, j, lane), v);
+                    lds_st_bf<W>(smem, erow(lr0, i, r, lane), ecol(lc0, j, lane), v);
                 }
         }
     }
     template <int W>
-    DEV void store_out(int m0, int n0, char* smem) const { tile_store<W>(smem, out, ldo, m0, n0, M, N, n0 & (BN - 1)); }
+    DEV void store_out(int m0, int n0, char* smem) const { tile_store<W>(smem, out, ldo, m0, n0, M, N); }
 };
 
 // Backward through tanh: out = acc * (1 - t^2) with t the stored bf16 activation at the
@@ -448,11 +458,12 @@ struct EpiDTanh {
     float* colpart;
     template <int W>
     DEV void load_in(int m0, int n0, char* smem) const {
-        tile_load<W>(smem, mkbuf(t, (int64_t)M * ldt * 2), ldt, m0, n0, M, N, 0, n0 & (BN - 1));
+        tile_load<W, W>(smem, mkbuf(t, (int64_t)M * ldt * 2), ldt, m0, n0, M, N, 0);
     }
-    DEV void operator()(int mw, int nw, f32x4 (&acc)[4][4], int, char* smem) const {
+    template <int W>
+    DEV void apply(int mw, int nw, f32x4 (&acc)[4][4], int, char* smem) const {
         const int lane = threadIdx.x & 63;
-        const int lr0 = mw & (BM - 1), lc0 = nw & (BN - 1);
+        const int lr0 = mw & (BM - 1), lc0 = nw & (W - 1);
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             const int col = ecol(nw, j, lane);
@@ -462,9 +473,9 @@ struct EpiDTanh {
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     const int lr = erow(lr0, i, r, lane), lc = ecol(lc0, j, lane);
-                    const float tv = lds_bf(smem, lr, lc);
+                    const float tv = lds_bf<W>(smem, lr, lc);
                     const float v = acc[i][j][r] * (1.f - tv * tv);
-                    lds_st_bf(smem, lr, lc, v);
+                    lds_st_bf<W>(smem, lr, lc, v);
                     cs += (erow(mw, i, r, lane) < M) ? v : 0.f;
                 }
             cs = colsum_lanes(cs);
@@ -472,7 +483,7 @@ struct EpiDTanh {
         }
     }
     template <int W>
-    DEV void store_out(int m0, int n0, char* smem) const { tile_store<W>(smem, out, ldo, m0, n0, M, N, n0 & (BN - 1)); }
+    DEV void store_out(int m0, int n0, char* smem) const { tile_store<W>(smem, out, ldo, m0, n0, M, N); }
 };
 
 // Decoder output (VAEB.py:257-263, 302-313) on the [M_e x Dn] block of a2 (| a6):
@@ -501,12 +512,13 @@ struct EpiDecOut {
     template <int W>
     DEV void load_in(int m0, int n0, char* smem) const {
         const rsrc_t src = mkbuf(x + xb.offset(), (int64_t)Mx * ldx * 2);
-        if constexpr (GAUSS) tile_load<W / 2, true>(smem, src, ldx, m0, n0 / 2, M, D, Mx, n0 & (BN - 1));
-        else tile_load<W>(smem, src, ldx, m0, n0, M, D, Mx, n0 & (BN - 1));
+        if constexpr (GAUSS) tile_load<W / 2, W, true>(smem, src, ldx, m0, n0 / 2, M, D, Mx);
+        else tile_load<W, W>(smem, src, ldx, m0, n0, M, D, Mx);
     }
-    DEV void operator()(int mw, int nw, f32x4 (&acc)[4][4], int, char* smem) const {
+    template <int W>
+    DEV void apply(int mw, int nw, f32x4 (&acc)[4][4], int, char* smem) const {
         const int lane = threadIdx.x & 63;
-        const int lr0 = mw & (BM - 1), lc0 = nw & (BN - 1);
+        const int lr0 = mw & (BM - 1), lc0 = nw & (W - 1);
         float rs[4][4];
 #pragma unroll
         for (int i = 0; i < 4; ++i)
@@ -527,7 +539,7 @@ struct EpiDecOut {
                 for (int r = 0; r < 4; ++r) {
                     const int row = erow(mw, i, r, lane), lr = erow(lr0, i, r, lane);
                     const bool ok = cok && row < M;
-                    const float xv = lds_bf(smem, lr, ecol(lc0, j, lane));
+                    const float xv = lds_bf<W>(smem, lr, ecol(lc0, j, lane));
                     const float a2 = acc[i][j][r] + bb2;
                     const float y = sigmoidf(a2);
                     float lpv, g2, g6 = 0.f;
@@ -544,10 +556,10 @@ struct EpiDecOut {
                     rs[i][r] += ok ? lpv : 0.f;
                     if (yout && ok) yout[(int64_t)row * D + d] = y;
                     if (train) {
-                        lds_st_bf(smem, lr, ecol(lc0, j, lane), g2);
+                        lds_st_bf<W>(smem, lr, ecol(lc0, j, lane), g2);
                         cs2 += ok ? g2 : 0.f;
                         if constexpr (GAUSS) {
-                            lds_st_bf(smem, lr, ecol(lc0, j, lane) + 32, g6);
+                            lds_st_bf<W>(smem, lr, ecol(lc0, j, lane) + 32, g6);
                             cs6 += ok ? g6 : 0.f;
                         }
                     }
@@ -574,7 +586,7 @@ struct EpiDecOut {
     }
     template <int W>
     DEV void store_out(int m0, int n0, char* smem) const {
-        if (train) tile_store<W>(smem, dA, ldd, m0, n0, M, N, n0 & (BN - 1));
+        if (train) tile_store<W>(smem, dA, ldd, m0, n0, M, N);
     }
 };
 
@@ -623,7 +635,8 @@ struct EpiAdagrad {
     // the fragment row are issued before its stores (buffer loads, masked elements read
     // out of range), instead of a load -> store chain per element that hipcc cannot
     // reorder (theta_in / accum may alias the stores, as far as it can tell).
-    DEV void operator()(int mw, int nw, f32x4 (&acc)[4][4], int, char*) const {
+    template <int W>
+    DEV void apply(int mw, int nw, f32x4 (&acc)[4][4], int, char*) const {
         const int lane = threadIdx.x & 63;
         const rsrc_t bth = mkbuf(opt.th_in, opt.n * 4), bac = mkbuf(opt.accum, opt.n * 4);
         const rsrc_t bto = mkbuf(opt.th_out, opt.n * 4), bgr = mkbuf(opt.grad, opt.n * 4);
