@@ -10,10 +10,11 @@ minibatch and the gradients are all-reduced over RCCL ("weak" scaling).
 Configs (BASELINE.json):
   --config mnist (default, the headline metric): 784-500-20 Bernoulli, B=100, fp32 MFMA
   --config frey  (Frey-shaped, BASELINE config 1 shapes): 560-200-2 Gaussian decoder, B=100, fp32
+  --config fv    (config 4): literal --full_varational step, MNIST 784-500-20, B=100, fp32
   --config synth (config 5, roofline stress): 4096-2048-128 Bernoulli, B=8192 per GPU,
                  bf16 MFMA operands / fp32 accumulation and master weights
 
-Usage:  python bench.py [--gpus N] [--steps K] [--warmup W] [--config mnist|frey|synth]
+Usage:  python bench.py [--gpus N] [--steps K] [--warmup W] [--config mnist|frey|fv|synth]
                        [--scaling weak|strong]
         (N > 1: torch.distributed.run, one process per GPU)
 Prints ONE JSON line on rank 0.
@@ -81,6 +82,7 @@ def step_flops(D, H, Z, B, L=1, gaussian=False):
 
 KERNEL_SYMBOLS = {"p1_enc": "PEnc", "p23_heads_dechid": "heads_dechid_kernel", "p4_decout": "PDecOut",
                   "p5_dhd_w2": "vaeb::tile_wgrad_kernel", "p67_dz_dh_w1": "vaeb::dz_dh_wgrad_kernel",
+                  "fv_update": "vaeb::fv_kernel",
                   "p8_wgrad_w3w45": "vaeb::wgrad_kernel", "p1_enc_latent": "vaeb::enc_latent_kernel",
                   "p4_decout_z": "vaeb::decout_z_kernel",
                   # bf16 GEMMs are one template: the epilogue / layout pair names the launch
@@ -90,6 +92,7 @@ KERNEL_SYMBOLS = {"p1_enc": "PEnc", "p23_heads_dechid": "heads_dechid_kernel", "
                   "bf_dW3": ("EpiAdagrad",)}
 PMC_FILES = {"mnist": os.path.join(ROOT, "profiles", "r1", "pmc_per_launch.json"),
              "frey": os.path.join(ROOT, "profiles", "r1", "pmc_frey_per_launch.json"),
+             "fv": os.path.join(ROOT, "profiles", "r1", "pmc_fv_per_launch.json"),
              "synth": os.path.join(ROOT, "profiles", "r1", "pmc_synth_per_launch.json")}
 
 
@@ -146,6 +149,38 @@ def cpu_baseline(D, H, Z, B, x, budget_s=10.0, max_steps=20000, continuous=False
             "sample": f"{n} float32 NumPy oracle steps ({D}-{H}-{Z}, B={B}) in {dt:.1f} s, OpenBLAS {threads} threads"}
 
 
+def cpu_baseline_fv(D, H, Z, B, x, budget_s=10.0, max_steps=20000):
+    """The oracle's literal full-variational step (float32 NumPy) on the host cores."""
+    from oracle import vaeb_oracle as O
+    try:
+        from threadpoolctl import threadpool_limits
+    except Exception:  # pragma: no cover
+        threadpool_limits = None
+    threads = min(16, os.cpu_count() or 1)
+    cfg = O.Config(D=D, H=H, Z=Z, estimator="FV")
+    theta = O.init_params(cfg)
+    mu = [t.copy() for t in theta]
+    sig = [np.full_like(t, 1e-3) for t in theta]
+    am = [np.zeros_like(t) for t in theta]
+    as_ = [np.zeros_like(t) for t in theta]
+    rng = np.random.default_rng(0)
+    nb = x.shape[0] // B
+    ctx = threadpool_limits(limits=threads) if threadpool_limits else None
+    n, t0 = 0, time.perf_counter()
+    while True:
+        b = n % nb
+        eps = rng.standard_normal((1, B, Z)).astype(np.float32)
+        _, mu, sig, am, as_, _ = O.fv_step(theta, mu, sig, am, as_, x[b * B:(b + 1) * B], eps, cfg)
+        n += 1
+        dt = time.perf_counter() - t0
+        if dt >= budget_s or n >= max_steps:
+            break
+    if ctx is not None and hasattr(ctx, "unregister"):
+        ctx.unregister()
+    return {"value": n * B / dt, "unit": "images/s", "cores": threads, "kind": "port",
+            "sample": f"{n} float32 NumPy oracle FV steps ({D}-{H}-{Z}, B={B}) in {dt:.1f} s, OpenBLAS {threads} threads"}
+
+
 CONFIGS = {
     "mnist": dict(D=784, H=500, Z=20, B=100, N=50000, dtype="f32", steps=2000, warmup=200,
                   metric="SGVB training images/sec + ELBO at MNIST 784-500-20, batch 100",
@@ -154,6 +189,10 @@ CONFIGS = {
                  metric="SGVB training images/sec + ELBO at Frey-shaped 560-200-2 (Gaussian decoder), batch 100",
                  workload="Frey-shaped 560-200-2 Gaussian decoder, LB estimator, L=1, Adagrad lr 0.01 "
                           "(BASELINE config 1 shapes)"),
+    "fv": dict(D=784, H=500, Z=20, B=100, N=50000, dtype="f32", steps=2000, warmup=200, estimator="FV",
+               metric="Literal full-variational (--full_varational) SGVB step images/sec, MNIST 784-500-20, batch 100",
+               workload="MNIST 784-500-20 Bernoulli decoder, FV estimator (fixed theta, Adagrad on mu_theta / "
+                        "sigma_theta, sigma 1e-3), L=1, lr 0.01 (BASELINE config 4)"),
     "synth": dict(D=4096, H=2048, Z=128, B=8192, N=16 * 8192, dtype="bf16", steps=50, warmup=5,
                   metric="SGVB training images/sec, synthetic 4096-2048-128, batch 8192 per GPU, bf16 MFMA",
                   workload="synthetic 4096-2048-128 Bernoulli decoder, LB, L=1, Adagrad lr 0.01, bf16 operands / "
@@ -207,8 +246,12 @@ def main():
     else:
         x = O.synthetic_mnist(n=N, D=D)
     cfg = O.Config(D=D, H=H, Z=Z, continuous=gauss)
+    fv = C.get("estimator") == "FV"
+    if fv and world > 1:
+        raise SystemExit("the literal full-variational path is single-rank (vaeb_comm_init rejects it)")
     ctx = _lib.Context(D, H, Z, B, B_global=Bg, row_offset=row_off, device=local,
                        decoder=_lib.DEC_GAUSSIAN if gauss else _lib.DEC_BERNOULLI,
+                       estimator=_lib.EST_FV if fv else _lib.EST_LB,
                        use_graph=not args.no_graph, max_eval_rows=B if bf16 else 1000,
                        dtype=_lib.DTYPE_BF16 if bf16 else _lib.DTYPE_F32)
     if world > 1:
@@ -216,7 +259,10 @@ def main():
         dist.broadcast_object_list(uid, src=0)
         ctx.comm_init(uid[0], rank, world)
     ctx.set_data(x)
-    ctx.set_params(O.flatten(O.init_params(cfg)))
+    theta0 = O.flatten(O.init_params(cfg))
+    ctx.set_params(theta0)
+    if fv:   # VAEB.py:120-125: mu_theta = theta, sigma_theta = 1e-3, Adagrad state 0
+        ctx.set_fv_state(theta0, np.full_like(theta0, 1e-3), np.zeros_like(theta0), np.zeros_like(theta0))
     ctx.set_eps_mode(_lib.EPS_PHILOX, seed=10)
     nb = N // Bg
     rs = np.random.RandomState(15485863)  # VAEB.py:526 --seed default
@@ -253,11 +299,17 @@ def main():
     # per-kernel device time (HIP events on the context's stream), after the timed region
     prof = ctx.profile_steps(50 if not bf16 else 5)
     fl = phase_flops(D, H, Z, B, gaussian=gauss)
+    if fv:   # forward only: the backward launches do not exist on this path
+        fl["fv_update"] = 32 * ctx.P   # bytes: mu, sigma and their accumulators read + written
     dom = max((k for k in prof if k[0] in fl), key=lambda k: k[1])
-    achieved = fl[dom[0]] / (dom[1] * 1e-3) / 1e12
-    traffic = committed_traffic(dom[0], PMC_FILES[args.config])
-    peak = PEAK_BF16_TFLOPS if bf16 else PEAK_F32_TFLOPS
-    sflops = step_flops(D, H, Z, B, gaussian=gauss)
+    traffic = committed_traffic(dom[0], PMC_FILES.get(args.config, ""))
+    if dom[0] == "fv_update":   # HBM-bound stream (config 4)
+        achieved = fl[dom[0]] / (dom[1] * 1e-3) / 1e9
+        peak, bound, unit = PEAK_HBM_GBS, "hbm", "GB/s"
+    else:
+        achieved = fl[dom[0]] / (dom[1] * 1e-3) / 1e12
+        peak, bound, unit = (PEAK_BF16_TFLOPS if bf16 else PEAK_F32_TFLOPS), "mfma", "TFLOP/s"
+    sflops = step_flops(D, H, Z, B, gaussian=gauss) if not fv else fl["p1_enc_latent"] + fl["p4_decout_z"]
 
     res = {
         "metric": C["metric"],
@@ -279,13 +331,16 @@ def main():
         "elbo": elbo_sum / max(nsteps, 1),
         "step_tflops": sflops / (el / steps) / 1e12,
         "kernels_ms": {k: round(v, 5) for k, v in prof},
-        "roofline": {"bound": "mfma", "kernel": dom[0], "achieved": achieved, "peak": peak,
-                     "unit": "TFLOP/s", "frac": achieved / peak, "traffic": traffic,
-                     "flops_per_launch": fl[dom[0]], "avg_launch_ms": dom[1]},
+        "roofline": {"bound": bound, "kernel": dom[0], "achieved": achieved, "peak": peak,
+                     "unit": unit, "frac": achieved / peak, "traffic": traffic,
+                     ("bytes_per_launch" if bound == "hbm" else "flops_per_launch"): fl[dom[0]],
+                     "avg_launch_ms": dom[1]},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         if bf16:
             res["cpu_baseline"] = cpu_baseline(D, H, Z, B, x[:4 * B], budget_s=args.cpu_budget * 2, max_steps=8)
+        elif fv:
+            res["cpu_baseline"] = cpu_baseline_fv(D, H, Z, B, x, budget_s=args.cpu_budget)
         else:
             res["cpu_baseline"] = cpu_baseline(D, H, Z, B, x, budget_s=args.cpu_budget, continuous=gauss)
     if rank == 0:

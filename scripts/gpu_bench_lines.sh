@@ -3,7 +3,7 @@ set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 mkdir -p gpurun_out/lines
-for cfg in mnist frey synth; do
+for cfg in mnist frey fv synth; do
   timeout -k 10 300 python3 bench.py --config $cfg > gpurun_out/lines/$cfg.json 2> gpurun_out/lines/$cfg.err || { tail gpurun_out/lines/$cfg.err; exit 1; }
   python3 -c "
 import json; d=json.load(open('gpurun_out/lines/$cfg.json'))

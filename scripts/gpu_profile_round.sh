@@ -4,7 +4,7 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
-for cfg in mnist frey synth; do
+for cfg in mnist frey fv synth; do
   O=gpurun_out/round/$cfg
   mkdir -p $O
   if [ $cfg = synth ]; then S="--steps 30 --warmup 3"; P="--steps 10 --warmup 2"; else S="--steps 1000 --warmup 100"; P="--steps 200 --warmup 20"; fi

@@ -49,3 +49,10 @@ def test_configs_name_their_metric():
     for name, c in bench.CONFIGS.items():
         assert c["metric"] and c["workload"] and c["dtype"] in ("f32", "bf16")
     assert bench.CONFIGS["mnist"]["metric"] == "SGVB training images/sec + ELBO at MNIST 784-500-20, batch 100"
+
+
+def test_cpu_baseline_fv_leg_runs():
+    from oracle import vaeb_oracle as O
+    x = O.synthetic_mnist(n=40, D=56)
+    r = bench.cpu_baseline_fv(56, 20, 4, 10, x, budget_s=0.2, max_steps=3)
+    assert r["kind"] == "port" and r["value"] > 0

@@ -336,18 +336,37 @@ __global__ __launch_bounds__(256) void fv_kernel(float* mu, float* sg, float* am
     __shared__ double sh[256];
     double tp = 0;
     const int64_t stride = (int64_t)gridDim.x * 256;
-    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < P; i += stride) {
-        const float m = mu[i], s = sg[i];
-        tp += 0.5 * (1.0 + (double)logf(s * s) - (double)m * m - (double)s * s);
-        if (update) {
-            const float gm = -2.f * m;
-            const float gs = 1.f / s - 2.f * s;
-            const float a1 = am[i] + gm * gm;
-            const float a2 = as[i] + gs * gs;
-            am[i] = a1;
-            as[i] = a2;
-            mu[i] = m + lr * gm / (sqrtf(a1) + eps);
-            sg[i] = s + lr * gs / (sqrtf(a2) + eps);
+    const rsrc_t bm = mkbuf(mu, P * 4), bs = mkbuf(sg, P * 4), bam = mkbuf(am, P * 4), bas = mkbuf(as, P * 4);
+    // U grid-stride elements per round trip: all their loads go out before any store (a
+    // load -> store chain per element would serialise the stream), in the same element
+    // order as a plain grid-stride loop, so the fp64 thetaPrior partial is unchanged
+    constexpr int U = 4;
+    for (int64_t i0 = (int64_t)blockIdx.x * 256 + threadIdx.x; i0 < P; i0 += U * stride) {
+        uint32_t off[U];
+        float m[U], s[U], a1[U], a2[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t i = i0 + u * stride;
+            off[u] = i < P ? (uint32_t)i * 4u : kOOB;
+            m[u] = bld(bm, off[u]);
+            s[u] = bld(bs, off[u]);
+            a1[u] = bld(bam, update ? off[u] : kOOB);
+            a2[u] = bld(bas, update ? off[u] : kOOB);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if (off[u] == kOOB) continue;
+            tp += 0.5 * (1.0 + (double)logf(s[u] * s[u]) - (double)m[u] * m[u] - (double)s[u] * s[u]);
+            if (update) {
+                const float gm = -2.f * m[u];
+                const float gs = 1.f / s[u] - 2.f * s[u];
+                const float n1 = a1[u] + gm * gm;
+                const float n2 = a2[u] + gs * gs;
+                bst(bam, off[u], n1);
+                bst(bas, off[u], n2);
+                bst(bm, off[u], m[u] + lr * gm / (sqrtf(n1) + eps));
+                bst(bs, off[u], s[u] + lr * gs / (sqrtf(n2) + eps));
+            }
         }
     }
     tp = block_sum256(tp, sh);
