@@ -519,69 +519,77 @@ struct EpiDecOut {
     DEV void apply(int mw, int nw, f32x4 (&acc)[4][4], int, char* smem) const {
         const int lane = threadIdx.x & 63;
         const int lr0 = mw & (BM - 1), lc0 = nw & (W - 1);
-        float rs[4][4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) rs[i][r] = 0.f;
+        // fragment row i outermost: only its 4 row partials and the JN column partials stay
+        // live (the transcendental-heavy body then fits the register budget without spills)
         constexpr int JN = GAUSS ? 2 : 4;
+        int col[JN], d[JN];
+        bool cok[JN];
+        float bb2[JN], bb6[JN], cs2[JN], cs6[JN];
 #pragma unroll
         for (int j = 0; j < JN; ++j) {
-            const int col = ecol(nw, j, lane);                               // dA column
-            const int d = GAUSS ? (nw >> 1) + 16 * j + (lane & 15) : col;   // data column
-            const bool cok = d < D;
-            const float bb2 = cok ? b2[d] : 0.f;
-            const float bb6 = (GAUSS && cok) ? b6[d] : 0.f;
-            float cs2 = 0.f, cs6 = 0.f;
+            col[j] = ecol(nw, j, lane);                                   // dA column
+            d[j] = GAUSS ? (nw >> 1) + 16 * j + (lane & 15) : col[j];     // data column
+            cok[j] = d[j] < D;
+            bb2[j] = cok[j] ? b2[d[j]] : 0.f;
+            bb6[j] = (GAUSS && cok[j]) ? b6[d[j]] : 0.f;
+            cs2[j] = 0.f;
+            cs6[j] = 0.f;
+        }
 #pragma unroll
-            for (int i = 0; i < 4; ++i)
+        for (int i = 0; i < 4; ++i) {
+            float rs[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int j = 0; j < JN; ++j)
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     const int row = erow(mw, i, r, lane), lr = erow(lr0, i, r, lane);
-                    const bool ok = cok && row < M;
+                    const bool ok = cok[j] && row < M;
                     const float xv = lds_bf<W>(smem, lr, ecol(lc0, j, lane));
-                    const float a2 = acc[i][j][r] + bb2;
-                    const float y = sigmoidf(a2);
-                    float lpv, g2, g6 = 0.f;
+                    const float a2 = acc[i][j][r] + bb2[j];
+                    float y, lpv, g2, g6 = 0.f;
                     if constexpr (!GAUSS) {
-                        lpv = xv * a2 - softplusf(a2);
+                        float sp;
+                        sigmoid_softplus(a2, y, sp);
+                        lpv = xv * a2 - sp;
                         g2 = sl * (xv - y);
                     } else {
-                        const float a6 = acc[i][j + 2][r] + bb6;
+                        y = sigmoidf(a2);
+                        const float a6 = acc[i][j + 2][r] + bb6[j];
                         const float rr = xv - y, e6 = fexp(-a6);
                         lpv = -kHalfLog2Pi - 0.5f * a6 - 0.5f * rr * rr * e6;
                         g2 = sl * rr * e6 * y * (1.f - y);
                         g6 = sl * (-0.5f + 0.5f * rr * rr * e6);
                     }
-                    rs[i][r] += ok ? lpv : 0.f;
-                    if (yout && ok) yout[(int64_t)row * D + d] = y;
+                    rs[r] += ok ? lpv : 0.f;
+                    if (yout && ok) yout[(int64_t)row * D + d[j]] = y;
                     if (train) {
                         lds_st_bf<W>(smem, lr, ecol(lc0, j, lane), g2);
-                        cs2 += ok ? g2 : 0.f;
+                        cs2[j] += ok ? g2 : 0.f;
                         if constexpr (GAUSS) {
                             lds_st_bf<W>(smem, lr, ecol(lc0, j, lane) + 32, g6);
-                            cs6 += ok ? g6 : 0.f;
+                            cs6[j] += ok ? g6 : 0.f;
                         }
                     }
                 }
-            if (train) {
-                cs2 = colsum_lanes(cs2);
-                if (lane < 16 && cok) colpart[(int64_t)(mw >> 6) * N + col] = cs2;
-                if constexpr (GAUSS) {
-                    cs6 = colsum_lanes(cs6);
-                    if (lane < 16 && cok) colpart[(int64_t)(mw >> 6) * N + col + 32] = cs6;
+            if (nw < N) {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const float sr = sum16(rs[r]);
+                    const int row = erow(mw, i, r, lane);
+                    if ((lane & 15) == 0 && row < M) lp[(int64_t)row * nlp + (nw >> 6)] = sr;
                 }
             }
         }
-        if (nw < N) {
+        if (train) {
 #pragma unroll
-            for (int i = 0; i < 4; ++i)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const float s = sum16(rs[i][r]);
-                    const int row = erow(mw, i, r, lane);
-                    if ((lane & 15) == 0 && row < M) lp[(int64_t)row * nlp + (nw >> 6)] = s;
+            for (int j = 0; j < JN; ++j) {
+                const float c2 = colsum_lanes(cs2[j]);
+                if (lane < 16 && cok[j]) colpart[(int64_t)(mw >> 6) * N + col[j]] = c2;
+                if constexpr (GAUSS) {
+                    const float c6 = colsum_lanes(cs6[j]);
+                    if (lane < 16 && cok[j]) colpart[(int64_t)(mw >> 6) * N + col[j] + 32] = c6;
                 }
+            }
         }
     }
     template <int W>
