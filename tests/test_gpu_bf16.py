@@ -220,3 +220,30 @@ def test_bf16_full_size_row_linearity_and_determinism():
     assert rel(g_full, g_a + g_b) <= 1e-3, rel(g_full, g_a + g_b)
     s_again, g_again, p_again = run(x, eps)
     assert s_again == s_full and np.array_equal(g_again, g_full) and np.array_equal(p_again, p_full)
+
+
+def test_bf16_dp_path_world1_matches_fused_optimizer():
+    """The data-parallel path of the bf16 engine (gradients stored, RCCL all-reduce of
+    [grads | SGVB], replicated Adagrad + shadow rewrite in adagrad_bf16_kernel) at world
+    size 1 against the fused-optimizer path, over 6 graph-replayed steps."""
+    from vaeb_amd import _lib
+    cfg = O.Config(D=256, H=128, Z=32)
+    B = 256
+    x = data_for(cfg, 8 * B)
+    order = np.array([3, 1, 4, 1, 5, 7], np.int32)
+    outs = []
+    for use_comm in (False, True):
+        ctx = _lib.Context(cfg.D, cfg.H, cfg.Z, B, max_eval_rows=B, dtype=_lib.DTYPE_BF16)
+        if use_comm:
+            ctx.comm_init(_lib.Context.comm_unique_id(), 0, 1)
+        ctx.set_data(x)
+        ctx.set_params(O.flatten(O.init_params(cfg)))
+        ctx.set_eps_mode(_lib.EPS_PHILOX, 10)
+        ctx.set_step(0)
+        ctx.update_many(order)
+        s, n = ctx.epoch_elbo()
+        outs.append((s / n, ctx.get_params(), ctx.get_adagrad_state()))
+        ctx.close()
+    assert abs(outs[0][0] - outs[1][0]) <= 1e-5 * abs(outs[0][0]), (outs[0][0], outs[1][0])
+    assert np.abs(outs[0][1] - outs[1][1]).max() <= 1e-5
+    assert rel(outs[1][2], outs[0][2]) <= 1e-4
