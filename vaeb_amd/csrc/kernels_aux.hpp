@@ -313,10 +313,29 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WGradArgs p) {
 // added once (so every rank applies the identical update).
 __global__ __launch_bounds__(256) void adagrad_kernel(OptArgs o, int64_t P, ElboArgs e) {
     const int64_t stride = (int64_t)gridDim.x * 256;
-    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < P; i += stride) {
-        float a = o.acc[i];
-        o.theta_out[i] = opt_rule(o, o.theta_in[i], a, o.grad[i]);
-        o.acc[i] = a;
+    const rsrc_t bti = mkbuf(o.theta_in, P * 4), bto = mkbuf(o.theta_out, P * 4);
+    const rsrc_t bac = mkbuf(o.acc, P * 4), bgr = mkbuf(o.grad, P * 4);
+    // U grid-stride elements per memory round trip: every load is issued before any store
+    // (hipcc cannot reorder a per-element load -> store chain: the arrays may alias)
+    constexpr int U = 8;
+    for (int64_t i0 = (int64_t)blockIdx.x * 256 + threadIdx.x; i0 < P; i0 += U * stride) {
+        uint32_t off[U];
+        float th[U], ac[U], gr[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t i = i0 + u * stride;
+            off[u] = i < P ? (uint32_t)i * 4u : kOOB;
+            th[u] = bld(bti, off[u]);
+            ac[u] = bld(bac, off[u]);
+            gr[u] = bld(bgr, off[u]);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            float a = ac[u];
+            const float tn = opt_rule(o, th[u], a, gr[u]);
+            bst(bto, off[u], tn);
+            bst(bac, off[u], a);
+        }
     }
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         const double v = (double)o.grad[P] * e.inv_bglob;

@@ -344,10 +344,34 @@ __global__ __launch_bounds__(256) void bias_opt_kernel(BiasArgs b) {
 // whole arena, rewriting the bf16 shadow.
 __global__ __launch_bounds__(256) void adagrad_bf16_kernel(Opt o, int64_t P, ShadowMap m, ElboArgs e) {
     const int64_t stride = (int64_t)gridDim.x * 256;
-    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < P; i += stride) {
-        Opt q = o;
-        q.store_grad = 0;
-        q.apply(i, m.at(i), o.grad[i]);
+    const rsrc_t bti = mkbuf(o.th_in, P * 4), bto = mkbuf(o.th_out, P * 4);
+    const rsrc_t bac = mkbuf(o.accum, P * 4), bgr = mkbuf(o.grad, P * 4);
+    // U grid-stride elements per memory round trip (loads before stores), the rule of
+    // Opt::apply, then theta' and its bf16 shadow copy
+    constexpr int U = 8;
+    for (int64_t i0 = (int64_t)blockIdx.x * 256 + threadIdx.x; i0 < P; i0 += U * stride) {
+        uint32_t off[U];
+        float th[U], ac[U], gr[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t i = i0 + u * stride;
+            off[u] = i < P ? (uint32_t)i * 4u : kOOB;
+            th[u] = bld(bti, off[u]);
+            ac[u] = bld(bac, off[u]);
+            gr[u] = bld(bgr, off[u]);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if (off[u] == kOOB) continue;
+            const int64_t i = i0 + u * stride;
+            const float gg = gr[u] - o.prior * th[u];
+            const float a = ac[u] + gg * gg;
+            const float tn = th[u] + o.lr * gg / (__builtin_amdgcn_sqrtf(a) + o.eps) - o.decay * th[u] * th[u];
+            bst(bac, off[u], a);
+            bst(bto, off[u], tn);
+            const int64_t si = m.at(i);
+            if (si >= 0) o.shadow_out[si] = (bf16_t)f2bf(tn);
+        }
     }
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         const double v = (double)o.grad[P] * e.inv_bglob;
