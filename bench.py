@@ -11,10 +11,11 @@ Configs (BASELINE.json):
   --config mnist (default, the headline metric): 784-500-20 Bernoulli, B=100, fp32 MFMA
   --config frey  (Frey-shaped, BASELINE config 1 shapes): 560-200-2 Gaussian decoder, B=100, fp32
   --config fv    (config 4): literal --full_varational step, MNIST 784-500-20, B=100, fp32
+  --config fvs   (config 4, weight-posterior reparam extension): FV with theta~ = mu + |sigma| zeta
   --config synth (config 5, roofline stress): 4096-2048-128 Bernoulli, B=8192 per GPU,
                  bf16 MFMA operands / fp32 accumulation and master weights
 
-Usage:  python bench.py [--gpus N] [--steps K] [--warmup W] [--config mnist|frey|fv|synth]
+Usage:  python bench.py [--gpus N] [--steps K] [--warmup W] [--config mnist|frey|fv|fvs|synth]
                        [--scaling weak|strong]
         (N > 1: torch.distributed.run, one process per GPU)
 Prints ONE JSON line on rank 0.
@@ -149,8 +150,9 @@ def cpu_baseline(D, H, Z, B, x, budget_s=10.0, max_steps=20000, continuous=False
             "sample": f"{n} float32 NumPy oracle steps ({D}-{H}-{Z}, B={B}) in {dt:.1f} s, OpenBLAS {threads} threads"}
 
 
-def cpu_baseline_fv(D, H, Z, B, x, budget_s=10.0, max_steps=20000):
-    """The oracle's literal full-variational step (float32 NumPy) on the host cores."""
+def cpu_baseline_fv(D, H, Z, B, x, budget_s=10.0, max_steps=20000, sample=False):
+    """The oracle's full-variational step (literal, or with the weight sample: FVS) in
+    float32 NumPy on the host cores."""
     from oracle import vaeb_oracle as O
     try:
         from threadpoolctl import threadpool_limits
@@ -170,7 +172,11 @@ def cpu_baseline_fv(D, H, Z, B, x, budget_s=10.0, max_steps=20000):
     while True:
         b = n % nb
         eps = rng.standard_normal((1, B, Z)).astype(np.float32)
-        _, mu, sig, am, as_, _ = O.fv_step(theta, mu, sig, am, as_, x[b * B:(b + 1) * B], eps, cfg)
+        if sample:
+            zeta = [rng.standard_normal(t.shape).astype(np.float32) for t in theta]
+            _, mu, sig, am, as_, _ = O.fvs_step(mu, sig, am, as_, x[b * B:(b + 1) * B], eps, zeta, cfg)
+        else:
+            _, mu, sig, am, as_, _ = O.fv_step(theta, mu, sig, am, as_, x[b * B:(b + 1) * B], eps, cfg)
         n += 1
         dt = time.perf_counter() - t0
         if dt >= budget_s or n >= max_steps:
@@ -178,7 +184,8 @@ def cpu_baseline_fv(D, H, Z, B, x, budget_s=10.0, max_steps=20000):
     if ctx is not None and hasattr(ctx, "unregister"):
         ctx.unregister()
     return {"value": n * B / dt, "unit": "images/s", "cores": threads, "kind": "port",
-            "sample": f"{n} float32 NumPy oracle FV steps ({D}-{H}-{Z}, B={B}) in {dt:.1f} s, OpenBLAS {threads} threads"}
+            "sample": f"{n} float32 NumPy oracle {'FVS' if sample else 'FV'} steps ({D}-{H}-{Z}, B={B}) in {dt:.1f} s, "
+                      f"OpenBLAS {threads} threads"}
 
 
 CONFIGS = {
@@ -193,6 +200,12 @@ CONFIGS = {
                metric="Literal full-variational (--full_varational) SGVB step images/sec, MNIST 784-500-20, batch 100",
                workload="MNIST 784-500-20 Bernoulli decoder, FV estimator (fixed theta, Adagrad on mu_theta / "
                         "sigma_theta, sigma 1e-3), L=1, lr 0.01 (BASELINE config 4)"),
+    "fvs": dict(D=784, H=500, Z=20, B=100, N=50000, dtype="f32", steps=2000, warmup=200, estimator="FVS",
+                metric="Full-variational SGVB step with the weight-posterior sample theta~ = mu + |sigma| zeta, "
+                       "images/sec, MNIST 784-500-20, batch 100",
+                workload="MNIST 784-500-20 Bernoulli decoder, FVS estimator (extension: weights sampled from "
+                         "N(mu, sigma^2) each step, VAEB.py:127-129; Adagrad on mu / sigma), L=1, lr 0.01 "
+                         "(BASELINE config 4's weight-posterior reparam)"),
     "synth": dict(D=4096, H=2048, Z=128, B=8192, N=16 * 8192, dtype="bf16", steps=50, warmup=5,
                   metric="SGVB training images/sec, synthetic 4096-2048-128, batch 8192 per GPU, bf16 MFMA",
                   workload="synthetic 4096-2048-128 Bernoulli decoder, LB, L=1, Adagrad lr 0.01, bf16 operands / "
@@ -246,12 +259,12 @@ def main():
     else:
         x = O.synthetic_mnist(n=N, D=D)
     cfg = O.Config(D=D, H=H, Z=Z, continuous=gauss)
-    fv = C.get("estimator") == "FV"
+    fv = C.get("estimator") in ("FV", "FVS")
     if fv and world > 1:
-        raise SystemExit("the literal full-variational path is single-rank (vaeb_comm_init rejects it)")
+        raise SystemExit("the full-variational paths are single-rank (vaeb_comm_init rejects them)")
     ctx = _lib.Context(D, H, Z, B, B_global=Bg, row_offset=row_off, device=local,
                        decoder=_lib.DEC_GAUSSIAN if gauss else _lib.DEC_BERNOULLI,
-                       estimator=_lib.EST_FV if fv else _lib.EST_LB,
+                       estimator={"FV": _lib.EST_FV, "FVS": _lib.EST_FVS}.get(C.get("estimator"), _lib.EST_LB),
                        use_graph=not args.no_graph, max_eval_rows=B if bf16 else 1000,
                        dtype=_lib.DTYPE_BF16 if bf16 else _lib.DTYPE_F32)
     if world > 1:
@@ -299,17 +312,20 @@ def main():
     # per-kernel device time (HIP events on the context's stream), after the timed region
     prof = ctx.profile_steps(50 if not bf16 else 5)
     fl = phase_flops(D, H, Z, B, gaussian=gauss)
-    if fv:   # forward only: the backward launches do not exist on this path
-        fl["fv_update"] = 32 * ctx.P   # bytes: mu, sigma and their accumulators read + written
+    if fv:   # the (mu, sigma) updates stream 32 B per parameter (+ the gradient, FVS)
+        fl["fv_update"] = 32 * ctx.P
+        fl["fvs_update"] = 36 * ctx.P
+        fl["fvs_sample"] = 12 * ctx.P
     dom = max((k for k in prof if k[0] in fl), key=lambda k: k[1])
     traffic = committed_traffic(dom[0], PMC_FILES.get(args.config, ""))
-    if dom[0] == "fv_update":   # HBM-bound stream (config 4)
+    if dom[0] in ("fv_update", "fvs_update", "fvs_sample"):   # HBM-bound streams (config 4)
         achieved = fl[dom[0]] / (dom[1] * 1e-3) / 1e9
         peak, bound, unit = PEAK_HBM_GBS, "hbm", "GB/s"
     else:
         achieved = fl[dom[0]] / (dom[1] * 1e-3) / 1e12
         peak, bound, unit = (PEAK_BF16_TFLOPS if bf16 else PEAK_F32_TFLOPS), "mfma", "TFLOP/s"
-    sflops = step_flops(D, H, Z, B, gaussian=gauss) if not fv else fl["p1_enc_latent"] + fl["p4_decout_z"]
+    sflops = (fl["p1_enc_latent"] + fl["p4_decout_z"]) if C.get("estimator") == "FV" else \
+        step_flops(D, H, Z, B, gaussian=gauss)
 
     res = {
         "metric": C["metric"],
@@ -340,7 +356,8 @@ def main():
         if bf16:
             res["cpu_baseline"] = cpu_baseline(D, H, Z, B, x[:4 * B], budget_s=args.cpu_budget * 2, max_steps=8)
         elif fv:
-            res["cpu_baseline"] = cpu_baseline_fv(D, H, Z, B, x, budget_s=args.cpu_budget)
+            res["cpu_baseline"] = cpu_baseline_fv(D, H, Z, B, x, budget_s=args.cpu_budget,
+                                                  sample=C.get("estimator") == "FVS")
         else:
             res["cpu_baseline"] = cpu_baseline(D, H, Z, B, x, budget_s=args.cpu_budget, continuous=gauss)
     if rank == 0:

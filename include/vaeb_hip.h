@@ -26,7 +26,11 @@ extern "C" {
 #endif
 
 enum vaeb_decoder   { VAEB_DEC_BERNOULLI = 0, VAEB_DEC_GAUSSIAN = 1 };   /* --continuous, VAEB.py:256 */
-enum vaeb_estimator { VAEB_EST_LB = 0, VAEB_EST_LA = 1, VAEB_EST_FV = 2 };/* VAEB.py:378-383 */
+enum vaeb_estimator { VAEB_EST_LB = 0, VAEB_EST_LA = 1, VAEB_EST_FV = 2,  /* VAEB.py:378-383 */
+                      VAEB_EST_FVS = 3 };  /* extension (not in the reference code): full-variational
+                                              with the weight-posterior reparameterisation that
+                                              VAEB.sample_variational_params (VAEB.py:127-129)
+                                              defines but never calls: theta~ = mu + |sigma| zeta */
 enum vaeb_objective { VAEB_OBJ_SUM_PRIOR = 0,                             /* VAEB.py:386-390 */
                       VAEB_OBJ_MEAN_MAP = 1 };                            /* VAEBfullbayes.py:142,183 */
 enum vaeb_eps_mode  { VAEB_EPS_PHILOX = 0, VAEB_EPS_HOST = 1 };
@@ -89,6 +93,9 @@ int vaeb_get_fv_state(vaeb_ctx* ctx, float* mu, float* sigma,
  * pushes eps [L x rows x Z] before each update/validate chunk (parity mode). */
 int vaeb_set_eps_mode(vaeb_ctx* ctx, int32_t mode, uint64_t seed);
 int vaeb_push_eps(vaeb_ctx* ctx, const float* eps, int64_t rows, int32_t L);
+/* VAEB_EST_FVS in host eps mode: the standard normals zeta [P] (arena order) of the next
+ * step's weight sample theta~ = mu + |sigma| zeta (Philox mode draws them on device). */
+int vaeb_push_fv_noise(vaeb_ctx* ctx, const float* zeta, int64_t n);
 int vaeb_set_step(vaeb_ctx* ctx, int64_t step);   /* Philox step counter */
 
 /* One SGVB step on the contiguous minibatch `batch_index` (VAEB.py:413), synchronous

@@ -319,6 +319,30 @@ def fv_step(theta_fixed, vb_mu, vb_sig, acc_mu, acc_sig, x, eps, cfg: Config):
     return sgvb / B, new_mu, new_sig, new_am, new_as, sgvb
 
 
+def fvs_step(vb_mu, vb_sig, acc_mu, acc_sig, x, eps, zeta, cfg: Config):
+    """Weight-sampling full-variational step (extension, VAEB_EST_FVS): getFVBL
+    (VAEB.py:349-367) with the sample that VAEB.sample_variational_params (VAEB.py:127-129)
+    defines but the reference never calls, theta~ = mu + |sigma| * zeta, in the data term.
+    Criterion as the literal path (VAEB.py:386-399):
+        J = B (sum log p + sum KL)(theta~) + thetaPrior(mu, sigma) - 1/2 sum (mu^2 + sigma^2)
+        dJ/dmu    = B G - 2 mu,   dJ/dsigma = B G zeta sign(sigma) + 1/sigma - 2 sigma,
+    G = d(sum log p + sum KL)/d theta~ (the LB data gradient at theta~).
+    Returns (SGVB/B, mu', sig', acc_mu', acc_sig', sgvb_total)."""
+    cfg_lb = dataclasses.replace(cfg, estimator="LB")
+    theta = [m + np.abs(s) * z for m, s, z in zip(vb_mu, vb_sig, zeta)]
+    out = forward_backward(theta, x, eps, cfg_lb, need_grad=True)
+    B = x.shape[0]
+    data = float(out["logp_rows"].sum(dtype=np.float64)) / eps.shape[0] + float(out["kl_rows"].sum(dtype=np.float64))
+    tp = fv_theta_prior(vb_mu, vb_sig)
+    sgvb = B * data + tp
+    gm = [(B * G - 2 * m).astype(m.dtype) for G, m in zip(out["data_grads"], vb_mu)]
+    gs = [(B * G * z * np.sign(s) + 1 / s - 2 * s).astype(s.dtype)
+          for G, z, s in zip(out["data_grads"], zeta, vb_sig)]
+    new_mu, new_am = adagrad_update(vb_mu, acc_mu, gm, cfg)
+    new_sig, new_as = adagrad_update(vb_sig, acc_sig, gs, cfg)
+    return sgvb / B, new_mu, new_sig, new_am, new_as, sgvb
+
+
 # ---------------------------------------------------------------- logpdf (degenerate-vae)
 def logpdf_bernoulli(Y, P):
     """degenerate-vae/logpdf.py:85-86 (epsilon inside the log)."""

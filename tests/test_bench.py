@@ -56,3 +56,10 @@ def test_cpu_baseline_fv_leg_runs():
     x = O.synthetic_mnist(n=40, D=56)
     r = bench.cpu_baseline_fv(56, 20, 4, 10, x, budget_s=0.2, max_steps=3)
     assert r["kind"] == "port" and r["value"] > 0
+
+
+def test_cpu_baseline_fvs_leg_runs():
+    from oracle import vaeb_oracle as O
+    x = O.synthetic_mnist(n=40, D=56)
+    r = bench.cpu_baseline_fv(56, 20, 4, 10, x, budget_s=0.2, max_steps=3, sample=True)
+    assert r["kind"] == "port" and r["value"] > 0 and "FVS" in r["sample"]

@@ -82,3 +82,23 @@ def test_cli_main_synthetic(tmp_path):
     assert rows[0] == "num_samples,L,Lvalid" and len(rows) == 5
     lb = [float(x.split(",")[1]) for x in rows[1:]]
     assert lb[2] > lb[0]  # epoch 2 better than epoch 1
+
+
+def test_vaeb_class_fv_weight_sampling_extension():
+    """VAEB(..., fullVariational=True, fv_sample=True): theta~ = mu + |sigma| zeta each step
+    (VAEB.py:127-129); reproducible in the host-noise ('theano') mode, the loaded theta
+    untouched, the variational parameters moving."""
+    from vaeb_amd.model import VAEB
+    x = O.synthetic_frey(n=600)
+    theta = O.init_params(O.Config(D=560, H=200, Z=2, continuous=True))
+    runs = []
+    for _ in range(2):
+        m = VAEB(x, True, 200, 2, 100, 1, 0.01, False, True, params=theta, rng="theano", fv_sample=True)
+        e = [m.update(i % 6) for i in range(6)]
+        assert all(np.isfinite(e))
+        fvp = m.full_variational_params
+        runs.append((e, fvp[0].copy()))
+        assert all(np.array_equal(p.get_value(), t) for p, t in zip(m.params, theta))
+        assert not np.array_equal(fvp[0], theta[0])
+        m.close()
+    assert runs[0][0] == runs[1][0] and np.array_equal(runs[0][1], runs[1][1])

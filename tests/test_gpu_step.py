@@ -16,7 +16,7 @@ from oracle import vaeb_oracle as O
 
 pytestmark = pytest.mark.gpu
 
-EST = {"LB": 0, "LA": 1, "FV": 2}
+EST = {"LB": 0, "LA": 1, "FV": 2, "FVS": 3}
 OBJ = {"sum_prior": 0, "mean_map": 1}
 
 
@@ -231,6 +231,61 @@ def test_fv_literal_step():
     assert np.abs(gs - O.flatten(s64)).max() <= 1e-7
     # theta itself is never updated on the literal FV path (SURVEY 8(c) pin 2)
     assert np.array_equal(ctx.get_params(), O.flatten(theta))
+
+
+@pytest.mark.parametrize("continuous", [False, True])
+def test_fv_weight_sampling_step(continuous):
+    """VAEB_EST_FVS (extension): theta~ = mu + |sigma| zeta with host-injected zeta and eps,
+    3 steps against oracle.fvs_step (float64).  ELBO relative <= 1e-4; mu', sigma' within
+    1e-3 lr but for a 1e-3 fraction (the first Adagrad steps are ~lr sign(g)); the loaded
+    theta is never written."""
+    cfg = (O.Config(D=560, H=200, Z=2, continuous=True, estimator="FVS") if continuous
+           else O.Config(D=784, H=500, Z=20, estimator="FVS"))
+    B = 100
+    x = data_for(cfg, 500)
+    rng = np.random.default_rng(21)
+    theta = [(t + 0.05 * rng.standard_normal(t.shape)).astype(np.float32) for t in O.init_params(cfg)]
+    mu = [t.copy() for t in theta]
+    sig = [np.full_like(t, 1e-3) for t in theta]
+    am = [np.zeros_like(t) for t in theta]
+    as_ = [np.zeros_like(t) for t in theta]
+    ctx = make_ctx(cfg, B)
+    ctx.set_data(x)
+    ctx.set_params(O.flatten(theta))
+    ctx.set_fv_state(O.flatten(mu), O.flatten(sig), O.flatten(am), O.flatten(as_))
+    ctx.set_eps_mode(1)
+    m64, s64 = [q.astype(np.float64) for q in mu], [q.astype(np.float64) for q in sig]
+    am64, as64 = [q.astype(np.float64) for q in am], [q.astype(np.float64) for q in as_]
+    for t in range(3):
+        eps = rng.standard_normal((1, B, cfg.Z)).astype(np.float32)
+        zeta = [rng.standard_normal(q.shape).astype(np.float32) for q in theta]
+        ctx.push_eps(eps)
+        ctx.push_fv_noise(O.flatten(zeta))
+        e = ctx.update(t)
+        ref, m64, s64, am64, as64, _ = O.fvs_step(m64, s64, am64, as64, x[t * B:(t + 1) * B].astype(np.float64),
+                                                  eps.astype(np.float64), [z.astype(np.float64) for z in zeta], cfg)
+        assert abs(e - ref) <= 1e-4 * abs(ref), (t, e, ref)
+    gm, gs, gam, gas = ctx.get_fv_state()
+    # the B-scaled data gradient (B G) makes more elements sit near g = 0, where one
+    # fp32-rounding-sized difference flips a ~lr sign(g) Adagrad step: a 1e-3 fraction
+    # may differ by up to 2 lr; the updates as a whole agree norm-wise to 1e-2
+    for got, ref, start in ((gm, O.flatten(m64), O.flatten(mu)), (gs, O.flatten(s64), O.flatten(sig))):
+        d = np.abs(got - ref)
+        assert d.max() <= 2 * cfg.lr + 1e-7, d.max()
+        assert float((d > 1e-3 * cfg.lr).mean()) <= 1e-3
+        assert rel(got - start, ref - start) <= 1e-2
+    assert np.array_equal(ctx.get_params(), O.flatten(theta))
+    # validate evaluates the data term at mu_theta and adds thetaPrior (as the literal path)
+    xv = x[:200]
+    epsv = rng.standard_normal((1, 200, cfg.Z)).astype(np.float32)
+    ctx.push_eps(epsv)
+    v = ctx.validate(xv)
+    cfg_lb = O.Config(**{**cfg.__dict__, "estimator": "LB"})
+    mu_now = O.unflatten(gm.astype(np.float64), cfg)
+    data = O.forward_backward(mu_now, xv.astype(np.float64), epsv.astype(np.float64), cfg_lb, need_grad=False)["sgvb"]
+    ref_v = 200 * data + O.fv_theta_prior(mu_now, O.unflatten(gs.astype(np.float64), cfg))
+    assert abs(v - ref_v) <= 1e-4 * abs(ref_v), (v, ref_v)
+    ctx.close()
 
 
 def test_philox_eps_is_standard_normal_and_deterministic():

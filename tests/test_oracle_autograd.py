@@ -95,3 +95,39 @@ def test_oracle_reconstruct_branches():
     eps = np.random.default_rng(0).standard_normal((1, 7, 3))
     out = O.forward_backward(params, x, eps, cfg, need_grad=False)
     assert np.allclose(O.reconstruct(params, x, eps, cfg), out["y"], atol=1e-15)
+
+
+@pytest.mark.parametrize("continuous", [False, True])
+def test_fvs_gradients_match_autograd(continuous):
+    """Weight-sampling full-variational extension (oracle fvs_step): the Adagrad step it
+    takes equals the one from torch autograd of J(mu, sigma) = B (sum log p + sum KL)
+    (mu + |sigma| zeta) + thetaPrior(mu, sigma) - 1/2 sum(mu^2 + sigma^2) (VAEB.py:127-129,
+    349-367, 386-399)."""
+    cfg = O.Config(D=12, H=6, Z=2, continuous=continuous, estimator="FV")
+    rng = np.random.default_rng(11)
+    B = 5
+    mu = [0.3 * rng.standard_normal(s) for _, s in O.param_shapes(cfg)]
+    sig = [np.full(s, 0.05) + 0.01 * rng.random(s) for _, s in O.param_shapes(cfg)]
+    zeta = [rng.standard_normal(s) for _, s in O.param_shapes(cfg)]
+    am = [np.zeros(s) for _, s in O.param_shapes(cfg)]
+    as_ = [np.zeros(s) for _, s in O.param_shapes(cfg)]
+    x = rng.random((B, cfg.D))
+    if not continuous:
+        x = (x < 0.5).astype(np.float64)
+    eps = rng.standard_normal((1, B, cfg.Z))
+    _, new_mu, new_sig, new_am, new_as, sgvb = O.fvs_step(mu, sig, am, as_, x, eps, zeta, cfg)
+
+    tm = [torch.tensor(m, requires_grad=True) for m in mu]
+    ts = [torch.tensor(s, requires_grad=True) for s in sig]
+    theta = [m + torch.abs(s) * torch.tensor(z) for m, s, z in zip(tm, ts, zeta)]
+    data, _ = torch_objective(theta, torch.tensor(x), torch.tensor(eps), O.Config(**{**cfg.__dict__, "estimator": "LB"}))
+    tp = sum(0.5 * (1 + torch.log(s ** 2) - m ** 2 - s ** 2).sum() for m, s in zip(tm, ts))
+    J = B * data + tp - 0.5 * sum((m ** 2).sum() + (s ** 2).sum() for m, s in zip(tm, ts))
+    J.backward()
+    assert abs(sgvb - float((B * data + tp).detach())) <= 1e-9 * abs(sgvb)
+    for m, s, nm, ns, na, nb in zip(tm, ts, new_mu, new_sig, new_am, new_as):
+        gm, gs = m.grad.numpy(), s.grad.numpy()
+        assert np.allclose(na, gm * gm, rtol=1e-9, atol=1e-12)
+        assert np.allclose(nb, gs * gs, rtol=1e-9, atol=1e-12)
+        assert np.allclose(nm, m.detach().numpy() + cfg.lr * gm / (np.abs(gm) + cfg.eps), rtol=1e-9, atol=1e-12)
+        assert np.allclose(ns, s.detach().numpy() + cfg.lr * gs / (np.abs(gs) + cfg.eps), rtol=1e-9, atol=1e-12)

@@ -15,7 +15,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libvaeb_hip.so")
 
 DEC_BERNOULLI, DEC_GAUSSIAN = 0, 1
-EST_LB, EST_LA, EST_FV = 0, 1, 2
+EST_LB, EST_LA, EST_FV, EST_FVS = 0, 1, 2, 3   # FVS: weight-sampling extension (include/vaeb_hip.h)
 OBJ_SUM_PRIOR, OBJ_MEAN_MAP = 0, 1
 EPS_PHILOX, EPS_HOST = 0, 1
 DTYPE_F32, DTYPE_BF16 = 0, 1
@@ -28,7 +28,7 @@ EXPORTS = [
     "vaeb_push_eps", "vaeb_set_step", "vaeb_update", "vaeb_update_async", "vaeb_update_many",
     "vaeb_epoch_elbo", "vaeb_synchronize", "vaeb_validate", "vaeb_reconstruct", "vaeb_reconstruct_sampled",
     "vaeb_comm_unique_id", "vaeb_comm_init", "vaeb_get_grads", "vaeb_get_activation",
-    "vaeb_profile_steps", "vaeb_kernel_name", "vaeb_debug_timeline", "vaeb_test_gemm_bf16", "vaeb_bench_gemm_bf16",
+    "vaeb_profile_steps", "vaeb_kernel_name", "vaeb_debug_timeline", "vaeb_test_gemm_bf16", "vaeb_bench_gemm_bf16", "vaeb_push_fv_noise",
     "vaeb_ae_create", "vaeb_ae_destroy", "vaeb_ae_num_params", "vaeb_ae_set_data", "vaeb_ae_set_params",
     "vaeb_ae_get_params", "vaeb_ae_set_adagrad_state", "vaeb_ae_get_adagrad_state", "vaeb_ae_train",
     "vaeb_ae_train_many", "vaeb_ae_reconstruct", "vaeb_ae_encode", "vaeb_ae_decode",
@@ -112,6 +112,7 @@ def load():
                                  ctypes.POINTER(ctypes.c_int32)], ctypes.c_int),
         "vaeb_test_gemm_bf16": ([_P] + [ctypes.c_int32] * 5 + [_F, _F, _F, ctypes.c_int32], ctypes.c_int),
         "vaeb_bench_gemm_bf16": ([_P] + [ctypes.c_int32] * 7 + [_F], ctypes.c_int),
+        "vaeb_push_fv_noise": ([_P, _F, _I64], ctypes.c_int),
         "vaeb_ae_create": ([ctypes.POINTER(AEConfigC), ctypes.POINTER(_P)], ctypes.c_int),
         "vaeb_ae_destroy": ([_P], ctypes.c_int),
         "vaeb_ae_num_params": ([_P, ctypes.POINTER(_I64)], ctypes.c_int),
@@ -224,6 +225,11 @@ class Context:
     # ---- noise
     def set_eps_mode(self, mode, seed=10):
         check(self.lib.vaeb_set_eps_mode(self.h, mode, seed))
+
+    def push_fv_noise(self, zeta):
+        """VAEB_EST_FVS, host eps mode: zeta [P] for the next step's theta~ = mu + |sigma| zeta."""
+        zeta = np.ascontiguousarray(zeta, np.float32).ravel()
+        check(self.lib.vaeb_push_fv_noise(self.h, fptr(zeta), zeta.size))
 
     def push_eps(self, eps):
         eps = np.ascontiguousarray(eps, np.float32)

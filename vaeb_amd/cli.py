@@ -34,7 +34,9 @@ command_line_args = {'seed': (15485863, int),
                      'rng': ('philox', str),        # philox (device) | theano (host RandomStreams emulation)
                      'objective': ('sum_prior', str),  # sum_prior (VAEB.py) | mean_map (VAEBfullbayes.py)
                      'max_eval_rows': (10000, int),
-                     'trace_dedup': (0, int)}       # 1: write each trace row once
+                     'trace_dedup': (0, int),       # 1: write each trace row once
+                     'fv_sample': (0, int)}         # 1 (with --full_varational): weight-posterior sample
+                                                    # theta~ = mu + |sigma| zeta (VAEB.py:127-129; extension)
 #   to add a new flag, add its name (VAEB.py:37-38)
 command_line_flags = ['continuous', 'generic_estimator', 'full_varational',
                       'synthetic']                 # added: synthetic data when the pickles are absent
@@ -133,7 +135,8 @@ def train_model(args):
     save_file = args['save_file']
     vb_param_file = args['vb_param_file']
     kw = dict(device=args.get('device', 0), rng=args.get('rng', 'philox'),
-              objective=args.get('objective', 'sum_prior'), max_eval_rows=args.get('max_eval_rows', 10000))
+              objective=args.get('objective', 'sum_prior'), max_eval_rows=args.get('max_eval_rows', 10000),
+              fv_sample=bool(args.get('fv_sample', 0)))
 
     print("loading data")
     if hidden_unit < 0:

@@ -347,6 +347,90 @@ __global__ __launch_bounds__(256) void adagrad_kernel(OptArgs o, int64_t P, Elbo
     }
 }
 
+// ------------------------------------------------ full variational, weight sampling
+// VAEB_EST_FVS (extension): the weight-posterior reparameterisation of
+// VAEB.sample_variational_params (VAEB.py:127-129), theta~ = mu + |sigma| zeta, used by the
+// data term of getFVBL (VAEB.py:349-367); criterion as the literal path (VAEB.py:386-399).
+// zeta: host buffer, or Philox keyed by (seed, step, parameter index) on a counter range
+// disjoint from the latent noise (c1 bit 30).
+DEV float fvs_zeta(int64_t i, const float* zin, uint64_t seed, int64_t step) {
+    if (zin) return zin[i];
+    return philox_normal(seed, (uint32_t)i, 0x40000000u | (uint32_t)(i >> 32), philox_c23(step, 0));
+}
+__global__ __launch_bounds__(256) void fvs_sample_kernel(const float* mu, const float* sg, float* theta, int64_t P,
+                                                        uint64_t seed, const int64_t* step, const float* zin) {
+    const int64_t stride = (int64_t)gridDim.x * 256;
+    const int64_t stp = *step;
+    const rsrc_t bm = mkbuf(mu, P * 4), bs = mkbuf(sg, P * 4), bt = mkbuf(theta, P * 4);
+    const rsrc_t bz = mkbuf(zin, zin ? P * 4 : 0);
+    constexpr int U = 4;   // grid-stride elements per round trip (loads before stores)
+    for (int64_t i0 = (int64_t)blockIdx.x * 256 + threadIdx.x; i0 < P; i0 += U * stride) {
+        uint32_t off[U];
+        float m[U], s[U], z[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t i = i0 + u * stride;
+            off[u] = i < P ? (uint32_t)i * 4u : kOOB;
+            m[u] = bld(bm, off[u]);
+            s[u] = bld(bs, off[u]);
+            z[u] = bld(bz, zin ? off[u] : kOOB);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if (off[u] == kOOB) continue;
+            const float zz = zin ? z[u] : fvs_zeta(i0 + u * stride, nullptr, seed, stp);
+            bst(bt, off[u], m[u] + fabsf(s[u]) * zz);
+        }
+    }
+}
+// Given the data gradient G = d(sum log p + sum KL)/d theta~ at the sample (grad arena):
+//   d/dmu    = B G - 2 mu                                  (thetaPrior -mu, L2 -mu)
+//   d/dsigma = B G zeta sign(sigma) + 1/sigma - 2 sigma    (thetaPrior 1/sigma - sigma, L2 -sigma)
+// then Adagrad on both (VAEB.py:426-444); thetaPrior partials from the pre-update values,
+// accumulated in the plain grid-stride element order.
+__global__ __launch_bounds__(256) void fvs_update_kernel(float* mu, float* sg, float* am, float* as, const float* grad,
+                                                        int64_t P, float B, float lr, float eps, uint64_t seed,
+                                                        const int64_t* step, const float* zin, float* part) {
+    __shared__ double sh[256];
+    double tp = 0;
+    const int64_t stride = (int64_t)gridDim.x * 256;
+    const int64_t stp = *step;
+    const rsrc_t bm = mkbuf(mu, P * 4), bs = mkbuf(sg, P * 4), bam = mkbuf(am, P * 4), bas = mkbuf(as, P * 4);
+    const rsrc_t bg = mkbuf(grad, P * 4), bz = mkbuf(zin, zin ? P * 4 : 0);
+    constexpr int U = 4;
+    for (int64_t i0 = (int64_t)blockIdx.x * 256 + threadIdx.x; i0 < P; i0 += U * stride) {
+        uint32_t off[U];
+        float m[U], s[U], a1[U], a2[U], G[U], z[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t i = i0 + u * stride;
+            off[u] = i < P ? (uint32_t)i * 4u : kOOB;
+            m[u] = bld(bm, off[u]);
+            s[u] = bld(bs, off[u]);
+            a1[u] = bld(bam, off[u]);
+            a2[u] = bld(bas, off[u]);
+            G[u] = bld(bg, off[u]);
+            z[u] = bld(bz, zin ? off[u] : kOOB);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if (off[u] == kOOB) continue;
+            const float zz = zin ? z[u] : fvs_zeta(i0 + u * stride, nullptr, seed, stp);
+            tp += 0.5 * (1.0 + (double)logf(s[u] * s[u]) - (double)m[u] * m[u] - (double)s[u] * s[u]);
+            const float gm = B * G[u] - 2.f * m[u];
+            const float gs = B * G[u] * zz * (s[u] >= 0.f ? 1.f : -1.f) + 1.f / s[u] - 2.f * s[u];
+            const float n1 = a1[u] + gm * gm;
+            const float n2 = a2[u] + gs * gs;
+            bst(bam, off[u], n1);
+            bst(bas, off[u], n2);
+            bst(bm, off[u], m[u] + lr * gm / (sqrtf(n1) + eps));
+            bst(bs, off[u], s[u] + lr * gs / (sqrtf(n2) + eps));
+        }
+    }
+    tp = block_sum256(tp, sh);
+    if (threadIdx.x == 0) part[blockIdx.x] = (float)tp;
+}
+
 // ----------------------------------------------------------------- full variational
 // Literal --full_varational update (VAEB.py:117-125, 349-367, 392-393, 426-444):
 // g_mu = -2 mu, g_sigma = 1/sigma - 2 sigma; thetaPrior partials from pre-update values.

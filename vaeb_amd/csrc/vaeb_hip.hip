@@ -80,7 +80,9 @@ const char* kKernelNames[] = {"p1_enc", "p2_heads", "p3_dechid", "p4_decout", "p
                               // bf16 engine (step_bf16.hpp), ids 18..34
                               "bf_enc", "bf_heads", "bf_latent", "bf_dechid", "bf_decout", "bf_dhd", "bf_dW26",
                               "bf_dz", "bf_dW1", "bf_dW1_opt", "bf_latent_bwd", "bf_dh", "bf_dW45", "bf_dW45_opt",
-                              "bf_dW3", "bf_bias_elbo", "bf_adagrad_dp"};
+                              "bf_dW3", "bf_bias_elbo", "bf_adagrad_dp",
+                              // weight-sampling full-variational extension, ids 35..38
+                              "unused35", "unused36", "fvs_sample", "fvs_update"};
 
 }  // namespace
 
@@ -95,6 +97,7 @@ struct vaeb_ctx {
     int par = 0;                              // arena holding the current parameters
     float *acc = nullptr, *grad = nullptr;
     float *fvmu = nullptr, *fvsg = nullptr, *fvam = nullptr, *fvas = nullptr, *fv_part = nullptr;
+    float* fvzeta = nullptr;   // VAEB_EST_FVS host-mode weight noise [P]
     // data
     float* data = nullptr;
     int64_t nrows = 0;
@@ -151,7 +154,7 @@ StepArgs make_args(vaeb_ctx* c, int par, int Mb, int mode, const float* xbase, b
     const vaeb_config& g = c->c;
     a.D = g.D; a.H = g.H; a.Z = g.Z; a.L = g.L;
     a.Mb = Mb; a.Mbp = r16(Mb); a.Me = g.L * a.Mbp;
-    a.dec = g.decoder; a.est = g.estimator; a.mode = mode;
+    a.dec = g.decoder; a.est = g.estimator == VAEB_EST_FVS ? VAEB_EST_LB : g.estimator; a.mode = mode;
     a.sc = (g.objective == VAEB_OBJ_MEAN_MAP) ? 1.0f / (float)g.B_global : 1.0f;
     const float* t = c->theta2[par];
     const bool gs = gaussian(c);
@@ -394,6 +397,17 @@ int enqueue_train_step(vaeb_ctx* c, int par, bool prof) {
     if (prof) pr.reps = c->prof_reps;
     const vaeb_config& g = c->c;
     hipStream_t s = c->s;
+    // VAEB_EST_FVS: the step reads the weight sample theta~ written into the spare arena
+    // par ^ 1 (the loaded theta in arena par is never updated, as on the literal path)
+    const bool fvs = g.estimator == VAEB_EST_FVS;
+    const float* zin = (fvs && c->eps_mode == VAEB_EPS_HOST) ? c->fvzeta : nullptr;
+    if (fvs) {
+        pr.mark(37);
+        REP(pr) hipLaunchKernelGGL(fvs_sample_kernel, dim3(kFvParts), dim3(256), 0, s, c->fvmu, c->fvsg,
+                                   c->theta2[par ^ 1], c->P, c->seed, c->step, zin);
+        CHECK_LAUNCH();
+        par ^= 1;
+    }
     StepArgs a = make_args(c, par, g.B, g.estimator == VAEB_EST_FV ? MODE_EVAL : MODE_TRAIN, c->data, true);
     if (int rc = enqueue_forward(c, a, pr)) return rc;
     ElboArgs e = base_elbo(c, a);
@@ -414,7 +428,8 @@ int enqueue_train_step(vaeb_ctx* c, int par, bool prof) {
         return 0;
     }
     const bool dp = c->comm != nullptr;  // any communicator (also world 1) takes the all-reduce path
-    const OptArgs opt = make_opt(c, par, !dp, dp || g.keep_grads != 0);
+    // FVS: the weight-gradient launches only store the data gradient at theta~
+    const OptArgs opt = make_opt(c, par, !dp && !fvs, dp || fvs || g.keep_grads != 0);
     const int bo = gaussian(c) ? 6 : 5;
     const bool gs = gaussian(c);
 
@@ -478,10 +493,23 @@ int enqueue_train_step(vaeb_ctx* c, int par, bool prof) {
             make_group(c, c->h, a.H, a.Mbp, 0, a.H, c->dMuLv, 2 * a.Z, a.Z, c->dMuLv + a.Z, 2 * a.Z, a.Z, a.Mbp, 1,
                        bo + 1, 2, bo + 2)};
         ElboArgs e1 = e;
-        if (dp) { e1.dp_slot = c->grad + c->P; e1.elbo_out = nullptr; e1.cursor = nullptr; e1.step = nullptr; }
+        if (dp || fvs) { e1.dp_slot = c->grad + c->P; e1.elbo_out = nullptr; e1.cursor = nullptr; e1.step = nullptr; }
         a.dbg = next_dbg(c);
         pr.mark(7);
         REP(pr) if (int rc = launch_wgrad(c, s, g12, 2, opt, &e1, a)) return rc;
+    }
+    if (fvs) {   // Adagrad on (mu_theta, sigma_theta), then the step's SGVB / B and cursor++
+        pr.mark(38);
+        REP(pr) hipLaunchKernelGGL(fvs_update_kernel, dim3(kFvParts), dim3(256), 0, s, c->fvmu, c->fvsg, c->fvam,
+                                   c->fvas, (const float*)c->grad, c->P, (float)g.B, g.lr, g.adagrad_eps, c->seed,
+                                   (const int64_t*)c->step, zin, c->fv_part);
+        CHECK_LAUNCH();
+        pr.mark(11);
+        e.fv_part = c->fv_part; e.n_fv = kFvParts;
+        e.data_mul = (double)g.B;
+        e.est = VAEB_EST_FV;   // SGVB = B (sum log p + sum KL) + thetaPrior (VAEB.py:364)
+        hipLaunchKernelGGL(elbo_kernel, dim3(1), dim3(256), 0, s, e);
+        CHECK_LAUNCH();
     }
     if (dp) {
         pr.mark(8);
@@ -499,7 +527,7 @@ int enqueue_train_step(vaeb_ctx* c, int par, bool prof) {
     return 0;
 }
 
-bool flips(const vaeb_ctx* c) { return c->c.estimator != VAEB_EST_FV; }
+bool flips(const vaeb_ctx* c) { return c->c.estimator != VAEB_EST_FV && c->c.estimator != VAEB_EST_FVS; }
 
 void free_graphs(vaeb_ctx* c) {
     for (auto& g1 : c->g1) if (g1) hipGraphExecDestroy(g1);
@@ -598,17 +626,18 @@ int vaeb_create(const vaeb_config* cfg, vaeb_ctx** out) {
     const vaeb_config& g = *cfg;
     if (g.D <= 0 || g.H <= 0 || g.Z <= 0 || g.B <= 0 || g.L <= 0)
         return fail(VAEB_ERR_ARG, "dimensions must be positive (D=%d H=%d Z=%d B=%d L=%d)", g.D, g.H, g.Z, g.B, g.L);
-    if (g.decoder < 0 || g.decoder > 1 || g.estimator < 0 || g.estimator > 2 || g.objective < 0 || g.objective > 1)
+    if (g.decoder < 0 || g.decoder > 1 || g.estimator < 0 || g.estimator > 3 || g.objective < 0 || g.objective > 1)
         return fail(VAEB_ERR_ARG, "bad decoder/estimator/objective enum");
-    if (g.estimator == VAEB_EST_FV && g.L != 1)
-        return fail(VAEB_ERR_ARG, "the literal full-variational estimator supports L == 1 only (VAEB.py:361)");
+    const bool fvx = g.estimator == VAEB_EST_FV || g.estimator == VAEB_EST_FVS;
+    if (fvx && g.L != 1)
+        return fail(VAEB_ERR_ARG, "the full-variational estimators support L == 1 only (VAEB.py:361)");
     if (g.dtype != VAEB_DTYPE_F32 && g.dtype != VAEB_DTYPE_BF16) return fail(VAEB_ERR_ARG, "bad dtype %d", g.dtype);
     if (g.dtype == VAEB_DTYPE_BF16) {
         if (g.D % 8 || g.H % 8 || g.Z % 8)
             return fail(VAEB_ERR_ARG, "bf16 engine: D, H, Z must be multiples of 8 (got %d, %d, %d)", g.D, g.H, g.Z);
         if (g.decoder == VAEB_DEC_GAUSSIAN && g.D % 32)
             return fail(VAEB_ERR_ARG, "bf16 engine: the Gaussian decoder needs D %% 32 == 0 (got %d)", g.D);
-        if (g.estimator == VAEB_EST_FV) return fail(VAEB_ERR_ARG, "bf16 engine: the FV estimator runs on the fp32 path");
+        if (fvx) return fail(VAEB_ERR_ARG, "bf16 engine: the FV estimators run on the fp32 path");
         if (g.estimator == VAEB_EST_LA && g.L > 8) return fail(VAEB_ERR_ARG, "bf16 engine: LA supports L <= 8");
     }
     auto* c = new vaeb_ctx();
@@ -636,7 +665,7 @@ int vaeb_create(const vaeb_config* cfg, vaeb_ctx** out) {
     rc = rc ? rc : dalloc(&c->theta2[1], c->P);
     rc = rc ? rc : dalloc(&c->acc, c->P);
     rc = rc ? rc : dalloc(&c->grad, c->P + 1);
-    if (g.estimator == VAEB_EST_FV) {
+    if (g.estimator == VAEB_EST_FV || g.estimator == VAEB_EST_FVS) {
         rc = rc ? rc : dalloc(&c->fvmu, c->P);
         rc = rc ? rc : dalloc(&c->fvsg, c->P);
         rc = rc ? rc : dalloc(&c->fvam, c->P);
@@ -695,7 +724,8 @@ int vaeb_destroy(vaeb_ctx* c) {
     if (c->comm) ncclCommDestroy(c->comm);
     float* fp[] = {c->theta2[0], c->theta2[1], c->acc, c->grad, c->fvmu, c->fvsg, c->fvam, c->fvas, c->fv_part, c->data, c->xeval,
                    c->elbo_out, c->eps_in, c->h, c->mu, c->lv, c->eps, c->z, c->hd, c->y, c->dA2, c->dA6, c->dA1,
-                   c->dZ, c->dMuLv, c->dA3, c->kl_part, c->lp_part, c->slab_ml, c->slab_dz, c->yacc};
+                   c->dZ, c->dMuLv, c->dA3, c->kl_part, c->lp_part, c->slab_ml, c->slab_dz, c->yacc,
+                   c->fvzeta};
     for (float* p : fp) if (p) hipFree(p);
     if (c->cnt_ml) hipFree(c->cnt_ml);
     if (c->cnt_dz) hipFree(c->cnt_dz);
@@ -810,6 +840,20 @@ int vaeb_push_eps(vaeb_ctx* c, const float* eps, int64_t rows, int32_t L) {
     return 0;
 }
 
+int vaeb_push_fv_noise(vaeb_ctx* c, const float* zeta, int64_t n) {
+    if (!c || !zeta) return fail(VAEB_ERR_ARG, "null argument");
+    if (c->c.estimator != VAEB_EST_FVS) return fail(VAEB_ERR_STATE, "weight noise is for the VAEB_EST_FVS estimator");
+    if (n != c->P) return fail(VAEB_ERR_ARG, "weight noise needs %lld values (got %lld)", (long long)c->P, (long long)n);
+    HIP_TRY(hipStreamSynchronize(c->s));
+    if (!c->fvzeta) {
+        if (int rc = dalloc(&c->fvzeta, (size_t)c->P)) return rc;
+        free_graphs(c);   // captured steps hold the noise pointer
+        c->graph_failed = false;
+    }
+    HIP_TRY(hipMemcpy(c->fvzeta, zeta, sizeof(float) * (size_t)n, hipMemcpyHostToDevice));
+    return 0;
+}
+
 int vaeb_set_step(vaeb_ctx* c, int64_t step) {
     if (!c) return fail(VAEB_ERR_ARG, "null ctx");
     HIP_TRY(hipStreamSynchronize(c->s));
@@ -884,7 +928,12 @@ static int eval_rows(vaeb_ctx* c, const float* x, int64_t n, int mode, float* ou
             continue;
         }
         HIP_TRY(hipMemcpyAsync(c->xeval, x + r0 * g.D, sizeof(float) * (size_t)rows * g.D, hipMemcpyHostToDevice, c->s));
-        StepArgs a = make_args(c, c->par, rows, mode, c->xeval, false);
+        int epar = c->par;
+        if (g.estimator == VAEB_EST_FVS) {   // the data term at the posterior mean mu_theta
+            epar = c->par ^ 1;
+            HIP_TRY(hipMemcpyAsync(c->theta2[epar], c->fvmu, sizeof(float) * (size_t)c->P, hipMemcpyDeviceToDevice, c->s));
+        }
+        StepArgs a = make_args(c, epar, rows, mode, c->xeval, false);
         a.row_base_add = r0;
         a.eps_in = c->eps_in ? c->eps_in + r0 * g.Z : nullptr;
         a.eps_in_ld = c->eps_rows;
@@ -902,7 +951,7 @@ static int eval_rows(vaeb_ctx* c, const float* x, int64_t n, int mode, float* ou
     }
     if (mode == MODE_EVAL) {
         double tp = 0.0;
-        if (g.estimator == VAEB_EST_FV) {
+        if (g.estimator == VAEB_EST_FV || g.estimator == VAEB_EST_FVS) {
             hipLaunchKernelGGL(fv_kernel, dim3(kFvParts), dim3(256), 0, c->s, c->fvmu, c->fvsg, c->fvam, c->fvas, c->P,
                                g.lr, g.adagrad_eps, 0, c->fv_part);
             CHECK_LAUNCH();
@@ -914,7 +963,7 @@ static int eval_rows(vaeb_ctx* c, const float* x, int64_t n, int mode, float* ou
         HIP_TRY(hipMemcpy(c->h_d2, c->eval_acc, 2 * sizeof(double), hipMemcpyDeviceToHost));
         const double data = c->h_d2[0];
         // FV validate: x.shape[0] * (sum logp + sum KL) + thetaPrior (VAEB.py:364)
-        *out_sum = (g.estimator == VAEB_EST_FV) ? (double)n * data + tp : data;
+        *out_sum = (g.estimator == VAEB_EST_FV || g.estimator == VAEB_EST_FVS) ? (double)n * data + tp : data;
     }
     return 0;
 }
@@ -997,8 +1046,8 @@ int vaeb_comm_unique_id(uint8_t out_id[128]) {
 
 int vaeb_comm_init(vaeb_ctx* c, const uint8_t id_bytes[128], int32_t rank, int32_t world) {
     if (!c || !id_bytes || world <= 0 || rank < 0 || rank >= world) return fail(VAEB_ERR_ARG, "bad comm arguments");
-    if (c->c.estimator == VAEB_EST_FV && world > 1)
-        return fail(VAEB_ERR_ARG, "the literal full-variational path is single-rank");
+    if ((c->c.estimator == VAEB_EST_FV || c->c.estimator == VAEB_EST_FVS) && world > 1)
+        return fail(VAEB_ERR_ARG, "the full-variational paths are single-rank");
     HIP_TRY(hipSetDevice(c->c.device));
     ncclUniqueId id;
     memcpy(&id, id_bytes, 128);

@@ -96,7 +96,7 @@ class VAEB:
     def __init__(self, x_train, continuous, hidden_units, latent_size, batch_size, L, learning_rate,
                  genericEstimator, fullVariational, params=None, prng=None, sigmaInit=None, *,
                  device=0, rng="philox", seed=10, objective="sum_prior", use_graph=True, max_eval_rows=10000,
-                 B_global=None, row_offset=0):
+                 B_global=None, row_offset=0, fv_sample=False):
         x_train = np.asarray(x_train, np.float32)
         self.N, self.input_size = x_train.shape
         self.n_hidden_units = hidden_units
@@ -116,7 +116,11 @@ class VAEB:
         self.objective = objective
         if self.fullVariational:
             assert params is not None
-        est = _lib.EST_LA if self.genericEstimator else (_lib.EST_FV if self.fullVariational else _lib.EST_LB)
+        # fv_sample (extension): full-variational with the weight-posterior sample of
+        # sample_variational_params (VAEB.py:127-129) in the data term
+        self.fv_sample = bool(fv_sample) and self.fullVariational
+        est = _lib.EST_LA if self.genericEstimator else (
+            (_lib.EST_FVS if self.fv_sample else _lib.EST_FV) if self.fullVariational else _lib.EST_LB)
         self._ctx = _lib.Context(self.input_size, hidden_units, latent_size, batch_size, L=L,
                                  decoder=_lib.DEC_GAUSSIAN if self.continuous else _lib.DEC_BERNOULLI,
                                  estimator=est,
@@ -140,6 +144,7 @@ class VAEB:
         if rng == "theano":
             self._stream = TheanoStreamEmulation(L, seed)
             self._ctx.set_eps_mode(_lib.EPS_HOST, seed)
+            self._zeta_rs = np.random.RandomState(seed + 1)   # host weight noise (fv_sample)
         else:
             self._stream = None
             self._ctx.set_eps_mode(_lib.EPS_PHILOX, seed)
@@ -184,6 +189,8 @@ class VAEB:
         [index*B, (index+1)*B); returns SGVB / batch_size."""
         if self._stream is not None:
             self._ctx.push_eps(self._stream.draw(self.batch_size, self.n_latent))
+            if self.fv_sample:
+                self._ctx.push_fv_noise(self._zeta_rs.standard_normal(self._ctx.P).astype(np.float32))
         return self._ctx.update(int(index))
 
     def update_epoch(self, batch_order):
