@@ -48,14 +48,20 @@ def test_vaeb_class_theano_rng_mode_is_reproducible():
     assert r[0] == r[1]
 
 
-def test_dp_path_world1_matches_fused_path():
+@pytest.mark.parametrize("continuous,use_graph", [(False, True), (True, True), (False, False)])
+def test_dp_path_world1_matches_fused_path(continuous, use_graph):
+    """The data-parallel path (gradients stored; bucket A = W2 [| W6] all-reduced and
+    updated on the second stream while the backward continues, bucket B + SGVB after it)
+    at world size 1 against the fused-optimizer path: Bernoulli / Gaussian decoder,
+    graph-replayed and eager."""
     from vaeb_amd import _lib
-    cfg = O.Config(D=784, H=500, Z=20)
-    x = O.synthetic_mnist(n=2000)
+    cfg = O.Config(D=560, H=200, Z=2, continuous=True) if continuous else O.Config(D=784, H=500, Z=20)
+    x = O.synthetic_frey(n=2000) if continuous else O.synthetic_mnist(n=2000)
     order = np.random.default_rng(1).permutation(20).astype(np.int32)
     outs = []
     for use_comm in (False, True):
-        ctx = _lib.Context(cfg.D, cfg.H, cfg.Z, 100, max_eval_rows=500)
+        ctx = _lib.Context(cfg.D, cfg.H, cfg.Z, 100, max_eval_rows=500, use_graph=use_graph,
+                           decoder=_lib.DEC_GAUSSIAN if continuous else _lib.DEC_BERNOULLI)
         if use_comm:
             ctx.comm_init(_lib.Context.comm_unique_id(), 0, 1)
         ctx.set_data(x)

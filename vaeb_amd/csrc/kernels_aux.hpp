@@ -310,21 +310,30 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WGradArgs p) {
 
 // ----------------------------------------------------------------- DP optimizer
 // After the RCCL all-reduce of [grad arena | SGVB]: replicated Adagrad with the prior
-// added once (so every rank applies the identical update).
-__global__ __launch_bounds__(256) void adagrad_kernel(OptArgs o, int64_t P, ElboArgs e) {
+// added once (so every rank applies the identical update).  The arena is reduced in two
+// buckets (vaeb_hip.hip: dp_bucket_*): a DpRange names the arena elements one launch
+// updates, as up to two index runs [lo0, lo0 + n0) and [lo1, lo1 + n1); `book` = this
+// launch also publishes the step's SGVB and advances the cursor / step counter.
+struct DpRange {
+    int64_t lo0, n0, lo1, n1;
+    int book;
+    DEV int64_t at(int64_t v) const { return v < n0 ? lo0 + v : lo1 + (v - n0); }
+};
+__global__ __launch_bounds__(256) void adagrad_kernel(OptArgs o, int64_t P, DpRange r, ElboArgs e) {
     const int64_t stride = (int64_t)gridDim.x * 256;
+    const int64_t n = r.n0 + r.n1;
     const rsrc_t bti = mkbuf(o.theta_in, P * 4), bto = mkbuf(o.theta_out, P * 4);
     const rsrc_t bac = mkbuf(o.acc, P * 4), bgr = mkbuf(o.grad, P * 4);
     // U grid-stride elements per memory round trip: every load is issued before any store
     // (hipcc cannot reorder a per-element load -> store chain: the arrays may alias)
     constexpr int U = 8;
-    for (int64_t i0 = (int64_t)blockIdx.x * 256 + threadIdx.x; i0 < P; i0 += U * stride) {
+    for (int64_t v0 = (int64_t)blockIdx.x * 256 + threadIdx.x; v0 < n; v0 += U * stride) {
         uint32_t off[U];
         float th[U], ac[U], gr[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            const int64_t i = i0 + u * stride;
-            off[u] = i < P ? (uint32_t)i * 4u : kOOB;
+            const int64_t v = v0 + u * stride;
+            off[u] = v < n ? (uint32_t)r.at(v) * 4u : kOOB;
             th[u] = bld(bti, off[u]);
             ac[u] = bld(bac, off[u]);
             gr[u] = bld(bgr, off[u]);
@@ -337,7 +346,7 @@ __global__ __launch_bounds__(256) void adagrad_kernel(OptArgs o, int64_t P, Elbo
             bst(bac, off[u], a);
         }
     }
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
+    if (r.book && blockIdx.x == 0 && threadIdx.x == 0) {
         const double v = (double)o.grad[P] * e.inv_bglob;
         *e.elbo_out = (float)v;
         e.epoch[0] += v;

@@ -342,20 +342,21 @@ __global__ __launch_bounds__(256) void bias_opt_kernel(BiasArgs b) {
 
 // DP: after the all-reduce of [grad arena | SGVB], the replicated optimizer over the
 // whole arena, rewriting the bf16 shadow.
-__global__ __launch_bounds__(256) void adagrad_bf16_kernel(Opt o, int64_t P, ShadowMap m, ElboArgs e) {
+__global__ __launch_bounds__(256) void adagrad_bf16_kernel(Opt o, int64_t P, DpRange r, ShadowMap m, ElboArgs e) {
     const int64_t stride = (int64_t)gridDim.x * 256;
+    const int64_t n = r.n0 + r.n1;
     const rsrc_t bti = mkbuf(o.th_in, P * 4), bto = mkbuf(o.th_out, P * 4);
     const rsrc_t bac = mkbuf(o.accum, P * 4), bgr = mkbuf(o.grad, P * 4);
     // U grid-stride elements per memory round trip (loads before stores), the rule of
     // Opt::apply, then theta' and its bf16 shadow copy
     constexpr int U = 8;
-    for (int64_t i0 = (int64_t)blockIdx.x * 256 + threadIdx.x; i0 < P; i0 += U * stride) {
+    for (int64_t v0 = (int64_t)blockIdx.x * 256 + threadIdx.x; v0 < n; v0 += U * stride) {
         uint32_t off[U];
         float th[U], ac[U], gr[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            const int64_t i = i0 + u * stride;
-            off[u] = i < P ? (uint32_t)i * 4u : kOOB;
+            const int64_t v = v0 + u * stride;
+            off[u] = v < n ? (uint32_t)r.at(v) * 4u : kOOB;
             th[u] = bld(bti, off[u]);
             ac[u] = bld(bac, off[u]);
             gr[u] = bld(bgr, off[u]);
@@ -363,7 +364,7 @@ __global__ __launch_bounds__(256) void adagrad_bf16_kernel(Opt o, int64_t P, Sha
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             if (off[u] == kOOB) continue;
-            const int64_t i = i0 + u * stride;
+            const int64_t i = off[u] >> 2;
             const float gg = gr[u] - o.prior * th[u];
             const float a = ac[u] + gg * gg;
             const float tn = th[u] + o.lr * gg / (__builtin_amdgcn_sqrtf(a) + o.eps) - o.decay * th[u] * th[u];
@@ -373,7 +374,7 @@ __global__ __launch_bounds__(256) void adagrad_bf16_kernel(Opt o, int64_t P, Sha
             if (si >= 0) o.shadow_out[si] = (bf16_t)f2bf(tn);
         }
     }
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
+    if (r.book && blockIdx.x == 0 && threadIdx.x == 0) {
         const double v = (double)o.grad[P] * e.inv_bglob;
         *e.elbo_out = (float)v;
         e.epoch[0] += v;

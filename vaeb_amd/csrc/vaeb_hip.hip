@@ -11,6 +11,7 @@
 
 #include <algorithm>
 #include <cstdarg>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -132,6 +133,9 @@ struct vaeb_ctx {
     // comm
     ncclComm_t comm = nullptr;
     int rank = 0, world = 1;
+    hipStream_t s2 = nullptr;     // DP: the gradient buckets' all-reduces and their Adagrad
+    hipEvent_t dp_ev[3] = {};     // fork after dW2, bucket A reduced, bucket A updated
+    bool dp_overlap = false;      // bucket A on s2 (bf16 engine; VAEB_DP_OVERLAP=0/1 overrides)
     // profiling
     hipEvent_t pev[kMaxProfKernels + 1] = {};
     int prof_n = 0, prof_reps = 1;
@@ -385,6 +389,74 @@ WGroup make_group(vaeb_ctx* c, const float* at, int ld_at, int klim, int at_is_x
     return G;
 }
 
+// ------------------------------------------------------------------ DP gradient buckets
+// Arena order W3 W4 W5 W1 W2 [W6] b3 b4 b5 b1 b2 [b6] | SGVB.  Bucket A = W2 [| W6] is final
+// once the dW2 (| dW6) launch has run, early in the backward; bucket B = the rest plus the
+// SGVB slot, final after the last weight-gradient launch.  Unprofiled steps fork bucket A's
+// all-reduce and Adagrad onto s2, where they overlap the remaining backward launches; s
+// then waits for bucket A's all-reduce (RCCL calls on one communicator stay serialised, in
+// the same order on every rank), reduces bucket B itself, runs its Adagrad and waits for
+// bucket A's Adagrad.  Only the fork sits on s2's queue: the critical path on s keeps its
+// own queue, and both waits are normally satisfied by the time s reaches them.  Profiled
+// steps run one all-reduce and one optimizer launch on s (per-kernel timing).
+// The fork costs ~18 us per step on the fp32 engine's 58-us MNIST step at world 1 (hipGraph
+// with a second branch; 78 vs 60 us) -- more than a 1.6-MB bucket's all-reduce can hide --
+// so it is the bf16 engine's default only, where bucket A is 34 MB (config 5) and its
+// Adagrad alone (37 us) pays for the fork already at world 1 (933 vs ~940 us).
+DpRange dp_range_a(const vaeb_ctx* c) {
+    const int bo = gaussian(c) ? 6 : 5;
+    return DpRange{c->off[4], c->off[bo] - c->off[4], 0, 0, 0};
+}
+DpRange dp_range_b(const vaeb_ctx* c) {
+    const int bo = gaussian(c) ? 6 : 5;
+    return DpRange{0, c->off[4], c->off[bo], c->P - c->off[bo], 1};
+}
+DpRange dp_range_all(const vaeb_ctx* c) { return DpRange{0, c->P, 0, 0, 1}; }
+
+int nccl_sum(vaeb_ctx* c, float* p, int64_t n, hipStream_t st) {
+    ncclResult_t r = ncclAllReduce(p, p, (size_t)n, ncclFloat, ncclSum, c->comm, st);
+    if (r != ncclSuccess) return fail(VAEB_ERR_COMM, "ncclAllReduce: %s", ncclGetErrorString(r));
+    return 0;
+}
+
+// after the dW2 (| dW6) launch: opt(stream, range) enqueues the optimizer over a range
+template <class Opt>
+int dp_bucket_a(vaeb_ctx* c, const Prof& pr, Opt opt) {
+    if (pr.on || !c->dp_overlap) return 0;
+    const DpRange r = dp_range_a(c);
+    HIP_TRY(hipEventRecord(c->dp_ev[0], c->s));
+    HIP_TRY(hipStreamWaitEvent(c->s2, c->dp_ev[0], 0));
+    if (int rc = nccl_sum(c, c->grad + r.lo0, r.n0, c->s2)) return rc;
+    HIP_TRY(hipEventRecord(c->dp_ev[1], c->s2));
+    if (int rc = opt(c->s2, r)) return rc;
+    HIP_TRY(hipEventRecord(c->dp_ev[2], c->s2));
+    return 0;
+}
+
+// after the last weight-gradient launch (the SGVB slot written)
+template <class Opt>
+int dp_bucket_b(vaeb_ctx* c, Prof& pr, int opt_mark, Opt opt) {
+    if (pr.on || !c->dp_overlap) {
+        pr.mark(8);
+        REP(pr) if (int rc = nccl_sum(c, c->grad, c->P + 1, c->s)) return rc;
+        pr.mark(opt_mark);
+        REP(pr) if (int rc = opt(c->s, dp_range_all(c))) return rc;
+        return 0;
+    }
+    const DpRange r = dp_range_b(c);
+    HIP_TRY(hipStreamWaitEvent(c->s, c->dp_ev[1], 0));
+    ncclResult_t g0 = ncclGroupStart();
+    if (g0 != ncclSuccess) return fail(VAEB_ERR_COMM, "ncclGroupStart: %s", ncclGetErrorString(g0));
+    int rc = nccl_sum(c, c->grad + r.lo0, r.n0, c->s);
+    rc = rc ? rc : nccl_sum(c, c->grad + r.lo1, r.n1 + 1, c->s);   // + the SGVB slot grad[P]
+    ncclResult_t g1 = ncclGroupEnd();
+    if (rc) return rc;
+    if (g1 != ncclSuccess) return fail(VAEB_ERR_COMM, "ncclGroupEnd: %s", ncclGetErrorString(g1));
+    if (int rc2 = opt(c->s, r)) return rc2;
+    HIP_TRY(hipStreamWaitEvent(c->s, c->dp_ev[2], 0));
+    return 0;
+}
+
 #include "engine_bf16.inc"
 
 // One training step reading parameter arena `par` and writing arena par ^ 1.
@@ -432,6 +504,12 @@ int enqueue_train_step(vaeb_ctx* c, int par, bool prof) {
     const OptArgs opt = make_opt(c, par, !dp && !fvs, dp || fvs || g.keep_grads != 0);
     const int bo = gaussian(c) ? 6 : 5;
     const bool gs = gaussian(c);
+    const OptArgs dopt = make_opt(c, par, true, false);
+    auto dp_opt = [&](hipStream_t st, const DpRange& r) -> int {
+        hipLaunchKernelGGL(adagrad_kernel, dim3(r.book ? 512 : 256), dim3(256), 0, st, dopt, c->P, r, e);
+        CHECK_LAUNCH();
+        return 0;
+    };
 
     // P5 + dW2 (| dW6) = [hd|1]^T [dA2 (| dA6)] in one grid: both need only P4's outputs
     a.dbg = next_dbg(c);
@@ -454,6 +532,7 @@ int enqueue_train_step(vaeb_ctx* c, int par, bool prof) {
         }
         CHECK_LAUNCH();
     }
+    if (dp) if (int rc = dp_bucket_a(c, pr, dp_opt)) return rc;
     // P67 (+ dW1 = [z|1]^T dA1 on the fused path): both need only P5's output
     a.dbg = next_dbg(c);
     {
@@ -511,17 +590,7 @@ int enqueue_train_step(vaeb_ctx* c, int par, bool prof) {
         hipLaunchKernelGGL(elbo_kernel, dim3(1), dim3(256), 0, s, e);
         CHECK_LAUNCH();
     }
-    if (dp) {
-        pr.mark(8);
-        REP(pr) {
-            ncclResult_t r = ncclAllReduce(c->grad, c->grad, (size_t)c->P + 1, ncclFloat, ncclSum, c->comm, s);
-            if (r != ncclSuccess) return fail(VAEB_ERR_COMM, "ncclAllReduce: %s", ncclGetErrorString(r));
-        }
-        pr.mark(9);
-        const OptArgs o = make_opt(c, par, true, false);
-        REP(pr) hipLaunchKernelGGL(adagrad_kernel, dim3(512), dim3(256), 0, s, o, c->P, e);
-        CHECK_LAUNCH();
-    }
+    if (dp) if (int rc = dp_bucket_b(c, pr, 9, dp_opt)) return rc;
     pr.mark(-1);
     c->prof_n = pr.k;
     return 0;
@@ -719,6 +788,7 @@ int vaeb_create(const vaeb_config* cfg, vaeb_ctx** out) {
 int vaeb_destroy(vaeb_ctx* c) {
     if (!c) return 0;
     if (c->s) hipStreamSynchronize(c->s);
+    if (c->s2) hipStreamSynchronize(c->s2);
     free_graphs(c);
     bf_free(c);
     if (c->comm) ncclCommDestroy(c->comm);
@@ -738,6 +808,8 @@ int vaeb_destroy(vaeb_ctx* c) {
     if (c->h_d2) hipHostFree(c->h_d2);
     if (c->ctl_ev) hipEventDestroy(c->ctl_ev);
     for (auto& ev : c->pev) if (ev) hipEventDestroy(ev);
+    for (auto& ev : c->dp_ev) if (ev) hipEventDestroy(ev);
+    if (c->s2) hipStreamDestroy(c->s2);
     if (c->s) hipStreamDestroy(c->s);
     delete c;
     return 0;
@@ -1046,9 +1118,16 @@ int vaeb_comm_unique_id(uint8_t out_id[128]) {
 
 int vaeb_comm_init(vaeb_ctx* c, const uint8_t id_bytes[128], int32_t rank, int32_t world) {
     if (!c || !id_bytes || world <= 0 || rank < 0 || rank >= world) return fail(VAEB_ERR_ARG, "bad comm arguments");
-    if ((c->c.estimator == VAEB_EST_FV || c->c.estimator == VAEB_EST_FVS) && world > 1)
+    if ((c->c.estimator == VAEB_EST_FV && world > 1) || c->c.estimator == VAEB_EST_FVS)
         return fail(VAEB_ERR_ARG, "the full-variational paths are single-rank");
+    if (c->comm) return fail(VAEB_ERR_STATE, "communicator already initialised");
     HIP_TRY(hipSetDevice(c->c.device));
+    c->dp_overlap = is_bf16(c);
+    if (const char* ov = getenv("VAEB_DP_OVERLAP")) c->dp_overlap = atoi(ov) != 0;
+    if (!c->s2) {
+        HIP_TRY(hipStreamCreateWithFlags(&c->s2, hipStreamNonBlocking));
+        for (auto& ev : c->dp_ev) HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    }
     ncclUniqueId id;
     memcpy(&id, id_bytes, 128);
     ncclResult_t r = ncclCommInitRank(&c->comm, world, id, rank);
