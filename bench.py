@@ -83,7 +83,8 @@ def step_flops(D, H, Z, B, L=1, gaussian=False):
 
 KERNEL_SYMBOLS = {"p1_enc": "PEnc", "p23_heads_dechid": "heads_dechid_kernel", "p4_decout": "PDecOut",
                   "p5_dhd_w2": "vaeb::tile_wgrad_kernel", "p67_dz_dh_w1": "vaeb::dz_dh_wgrad_kernel",
-                  "fv_update": "vaeb::fv_kernel",
+                  "fv_update": "vaeb::fv_kernel", "fvs_update": "vaeb::fvs_update_kernel",
+                  "fvs_sample": "vaeb::fvs_sample_kernel",
                   "p8_wgrad_w3w45": "vaeb::wgrad_kernel", "p1_enc_latent": "vaeb::enc_latent_kernel",
                   "p4_decout_z": "vaeb::decout_z_kernel",
                   # bf16 GEMMs are one template: the epilogue / layout pair names the launch
@@ -94,6 +95,7 @@ KERNEL_SYMBOLS = {"p1_enc": "PEnc", "p23_heads_dechid": "heads_dechid_kernel", "
 PMC_FILES = {"mnist": os.path.join(ROOT, "profiles", "r1", "pmc_per_launch.json"),
              "frey": os.path.join(ROOT, "profiles", "r1", "pmc_frey_per_launch.json"),
              "fv": os.path.join(ROOT, "profiles", "r1", "pmc_fv_per_launch.json"),
+             "fvs": os.path.join(ROOT, "profiles", "r1", "pmc_fvs_per_launch.json"),
              "synth": os.path.join(ROOT, "profiles", "r1", "pmc_synth_per_launch.json")}
 
 
