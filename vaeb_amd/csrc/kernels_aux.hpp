@@ -65,6 +65,15 @@ DEV double wave_sum64(double v) {
     return v;
 }
 
+// Fixed-order workgroup sum for 256 threads: a butterfly per wave, then the wave sums in
+// order (one barrier instead of block_sum256's eight).  Valid on thread 0.
+DEV double block_sum256w(double v, double* sh) {
+    v = wave_sum64(v);
+    if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = v;
+    __syncthreads();
+    return ((sh[0] + sh[1]) + sh[2]) + sh[3];
+}
+
 // Deterministic (fixed-order) reduction by one 256-thread workgroup: strided per-thread
 // sums, a butterfly within each wave, then the four wave sums in wave order.
 DEV void elbo_reduce(const ElboArgs& e, double* sh) {
@@ -399,122 +408,175 @@ DEV float fvs_zeta(int64_t i, const float* zin, uint64_t seed, int64_t step) {
     if (zin) return zin[i];
     return philox_normal(seed, (uint32_t)i, 0x40000000u | (uint32_t)(i >> 32), philox_c23(step, 0));
 }
+// The (mu, sigma) streams below move 16-byte groups: thread t of the grid takes groups
+// t, t + T, ... (U per round trip, every load before any store), the P % 4 tail elements
+// go to threads 0..2 of block 0.  kFvGrid x 256 threads x U x 4 elements cover MNIST's
+// 0.8 M parameters in one round trip.
+DEV void fv_group(int64_t g, int64_t n4, uint32_t& off) { off = g < n4 ? (uint32_t)(g * 16) : kOOB; }
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+DEV void bst4(rsrc_t b, uint32_t off, f32x4 v) {
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, v), b, off, 0, 0);
+}
+
 __global__ __launch_bounds__(256) void fvs_sample_kernel(const float* mu, const float* sg, float* theta, int64_t P,
                                                         uint64_t seed, const int64_t* step, const float* zin) {
-    const int64_t stride = (int64_t)gridDim.x * 256;
+    const int64_t T = (int64_t)gridDim.x * 256, n4 = P >> 2;
     const int64_t stp = *step;
     const rsrc_t bm = mkbuf(mu, P * 4), bs = mkbuf(sg, P * 4), bt = mkbuf(theta, P * 4);
     const rsrc_t bz = mkbuf(zin, zin ? P * 4 : 0);
-    constexpr int U = 4;   // grid-stride elements per round trip (loads before stores)
-    for (int64_t i0 = (int64_t)blockIdx.x * 256 + threadIdx.x; i0 < P; i0 += U * stride) {
+    constexpr int U = 2;
+    for (int64_t g0 = (int64_t)blockIdx.x * 256 + threadIdx.x; g0 < n4; g0 += U * T) {
         uint32_t off[U];
-        float m[U], s[U], z[U];
+        f32x4 m[U], s[U], z[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            const int64_t i = i0 + u * stride;
-            off[u] = i < P ? (uint32_t)i * 4u : kOOB;
-            m[u] = bld(bm, off[u]);
-            s[u] = bld(bs, off[u]);
-            z[u] = bld(bz, zin ? off[u] : kOOB);
+            fv_group(g0 + u * T, n4, off[u]);
+            m[u] = bld4(bm, off[u]);
+            s[u] = bld4(bs, off[u]);
+            z[u] = bld4(bz, zin ? off[u] : kOOB);
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             if (off[u] == kOOB) continue;
-            const float zz = zin ? z[u] : fvs_zeta(i0 + u * stride, nullptr, seed, stp);
-            bst(bt, off[u], m[u] + fabsf(s[u]) * zz);
+            f32x4 t;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const float zz = zin ? z[u][k] : fvs_zeta((g0 + u * T) * 4 + k, nullptr, seed, stp);
+                t[k] = m[u][k] + fabsf(s[u][k]) * zz;
+            }
+            bst4(bt, off[u], t);
         }
     }
+    if (blockIdx.x == 0 && threadIdx.x < (P & 3)) {
+        const int64_t i = n4 * 4 + threadIdx.x;
+        theta[i] = mu[i] + fabsf(sg[i]) * fvs_zeta(i, zin, seed, stp);
+    }
 }
+
 // Given the data gradient G = d(sum log p + sum KL)/d theta~ at the sample (grad arena):
 //   d/dmu    = B G - 2 mu                                  (thetaPrior -mu, L2 -mu)
 //   d/dsigma = B G zeta sign(sigma) + 1/sigma - 2 sigma    (thetaPrior 1/sigma - sigma, L2 -sigma)
-// then Adagrad on both (VAEB.py:426-444); thetaPrior partials from the pre-update values,
-// accumulated in the plain grid-stride element order.
+// then Adagrad on both (VAEB.py:426-444); thetaPrior partials from the pre-update values.
+struct FvsElem {
+    float B, lr, eps;
+    DEV void operator()(float& m, float& s, float& a1, float& a2, float G, float zz, double& tp) const {
+        tp += 0.5 * (1.0 + (double)logf(s * s) - (double)m * m - (double)s * s);
+        const float gm = B * G - 2.f * m;
+        const float gs = B * G * zz * (s >= 0.f ? 1.f : -1.f) + 1.f / s - 2.f * s;
+        a1 += gm * gm;
+        a2 += gs * gs;
+        m += lr * gm / (sqrtf(a1) + eps);
+        s += lr * gs / (sqrtf(a2) + eps);
+    }
+};
 __global__ __launch_bounds__(256) void fvs_update_kernel(float* mu, float* sg, float* am, float* as, const float* grad,
                                                         int64_t P, float B, float lr, float eps, uint64_t seed,
                                                         const int64_t* step, const float* zin, float* part) {
     __shared__ double sh[256];
     double tp = 0;
-    const int64_t stride = (int64_t)gridDim.x * 256;
+    const FvsElem f{B, lr, eps};
+    const int64_t T = (int64_t)gridDim.x * 256, n4 = P >> 2;
     const int64_t stp = *step;
     const rsrc_t bm = mkbuf(mu, P * 4), bs = mkbuf(sg, P * 4), bam = mkbuf(am, P * 4), bas = mkbuf(as, P * 4);
     const rsrc_t bg = mkbuf(grad, P * 4), bz = mkbuf(zin, zin ? P * 4 : 0);
-    constexpr int U = 4;
-    for (int64_t i0 = (int64_t)blockIdx.x * 256 + threadIdx.x; i0 < P; i0 += U * stride) {
+    constexpr int U = 2;
+    for (int64_t g0 = (int64_t)blockIdx.x * 256 + threadIdx.x; g0 < n4; g0 += U * T) {
         uint32_t off[U];
-        float m[U], s[U], a1[U], a2[U], G[U], z[U];
+        f32x4 m[U], s[U], a1[U], a2[U], G[U], z[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            const int64_t i = i0 + u * stride;
-            off[u] = i < P ? (uint32_t)i * 4u : kOOB;
-            m[u] = bld(bm, off[u]);
-            s[u] = bld(bs, off[u]);
-            a1[u] = bld(bam, off[u]);
-            a2[u] = bld(bas, off[u]);
-            G[u] = bld(bg, off[u]);
-            z[u] = bld(bz, zin ? off[u] : kOOB);
+            fv_group(g0 + u * T, n4, off[u]);
+            m[u] = bld4(bm, off[u]);
+            s[u] = bld4(bs, off[u]);
+            a1[u] = bld4(bam, off[u]);
+            a2[u] = bld4(bas, off[u]);
+            G[u] = bld4(bg, off[u]);
+            z[u] = bld4(bz, zin ? off[u] : kOOB);
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             if (off[u] == kOOB) continue;
-            const float zz = zin ? z[u] : fvs_zeta(i0 + u * stride, nullptr, seed, stp);
-            tp += 0.5 * (1.0 + (double)logf(s[u] * s[u]) - (double)m[u] * m[u] - (double)s[u] * s[u]);
-            const float gm = B * G[u] - 2.f * m[u];
-            const float gs = B * G[u] * zz * (s[u] >= 0.f ? 1.f : -1.f) + 1.f / s[u] - 2.f * s[u];
-            const float n1 = a1[u] + gm * gm;
-            const float n2 = a2[u] + gs * gs;
-            bst(bam, off[u], n1);
-            bst(bas, off[u], n2);
-            bst(bm, off[u], m[u] + lr * gm / (sqrtf(n1) + eps));
-            bst(bs, off[u], s[u] + lr * gs / (sqrtf(n2) + eps));
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const float zz = zin ? z[u][k] : fvs_zeta((g0 + u * T) * 4 + k, nullptr, seed, stp);
+                float mm = m[u][k], ss = s[u][k], x1 = a1[u][k], x2 = a2[u][k];
+                f(mm, ss, x1, x2, G[u][k], zz, tp);
+                m[u][k] = mm; s[u][k] = ss; a1[u][k] = x1; a2[u][k] = x2;
+            }
+            bst4(bam, off[u], a1[u]);
+            bst4(bas, off[u], a2[u]);
+            bst4(bm, off[u], m[u]);
+            bst4(bs, off[u], s[u]);
         }
     }
-    tp = block_sum256(tp, sh);
+    if (blockIdx.x == 0 && threadIdx.x < (P & 3)) {
+        const int64_t i = n4 * 4 + threadIdx.x;
+        f(mu[i], sg[i], am[i], as[i], grad[i], fvs_zeta(i, zin, seed, stp), tp);
+    }
+    tp = block_sum256w(tp, sh);
     if (threadIdx.x == 0) part[blockIdx.x] = (float)tp;
 }
 
 // ----------------------------------------------------------------- full variational
 // Literal --full_varational update (VAEB.py:117-125, 349-367, 392-393, 426-444):
 // g_mu = -2 mu, g_sigma = 1/sigma - 2 sigma; thetaPrior partials from pre-update values.
+struct FvElem {
+    float lr, eps;
+    int update;
+    DEV void operator()(float& m, float& s, float& a1, float& a2, double& tp) const {
+        tp += 0.5 * (1.0 + (double)logf(s * s) - (double)m * m - (double)s * s);
+        if (!update) return;
+        const float gm = -2.f * m;
+        const float gs = 1.f / s - 2.f * s;
+        a1 += gm * gm;
+        a2 += gs * gs;
+        m += lr * gm / (sqrtf(a1) + eps);
+        s += lr * gs / (sqrtf(a2) + eps);
+    }
+};
 __global__ __launch_bounds__(256) void fv_kernel(float* mu, float* sg, float* am, float* as, int64_t P,
                                                  float lr, float eps, int update, float* part) {
     __shared__ double sh[256];
     double tp = 0;
-    const int64_t stride = (int64_t)gridDim.x * 256;
+    const FvElem f{lr, eps, update};
+    const int64_t T = (int64_t)gridDim.x * 256, n4 = P >> 2;
     const rsrc_t bm = mkbuf(mu, P * 4), bs = mkbuf(sg, P * 4), bam = mkbuf(am, P * 4), bas = mkbuf(as, P * 4);
-    // U grid-stride elements per round trip: all their loads go out before any store (a
-    // load -> store chain per element would serialise the stream), in the same element
-    // order as a plain grid-stride loop, so the fp64 thetaPrior partial is unchanged
-    constexpr int U = 4;
-    for (int64_t i0 = (int64_t)blockIdx.x * 256 + threadIdx.x; i0 < P; i0 += U * stride) {
+    constexpr int U = 2;   // 16-byte groups per round trip (fvs_sample_kernel's scheme)
+    for (int64_t g0 = (int64_t)blockIdx.x * 256 + threadIdx.x; g0 < n4; g0 += U * T) {
         uint32_t off[U];
-        float m[U], s[U], a1[U], a2[U];
+        f32x4 m[U], s[U], a1[U], a2[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            const int64_t i = i0 + u * stride;
-            off[u] = i < P ? (uint32_t)i * 4u : kOOB;
-            m[u] = bld(bm, off[u]);
-            s[u] = bld(bs, off[u]);
-            a1[u] = bld(bam, update ? off[u] : kOOB);
-            a2[u] = bld(bas, update ? off[u] : kOOB);
+            fv_group(g0 + u * T, n4, off[u]);
+            m[u] = bld4(bm, off[u]);
+            s[u] = bld4(bs, off[u]);
+            a1[u] = bld4(bam, update ? off[u] : kOOB);
+            a2[u] = bld4(bas, update ? off[u] : kOOB);
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             if (off[u] == kOOB) continue;
-            tp += 0.5 * (1.0 + (double)logf(s[u] * s[u]) - (double)m[u] * m[u] - (double)s[u] * s[u]);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                float mm = m[u][k], ss = s[u][k], x1 = a1[u][k], x2 = a2[u][k];
+                f(mm, ss, x1, x2, tp);
+                m[u][k] = mm; s[u][k] = ss; a1[u][k] = x1; a2[u][k] = x2;
+            }
             if (update) {
-                const float gm = -2.f * m[u];
-                const float gs = 1.f / s[u] - 2.f * s[u];
-                const float n1 = a1[u] + gm * gm;
-                const float n2 = a2[u] + gs * gs;
-                bst(bam, off[u], n1);
-                bst(bas, off[u], n2);
-                bst(bm, off[u], m[u] + lr * gm / (sqrtf(n1) + eps));
-                bst(bs, off[u], s[u] + lr * gs / (sqrtf(n2) + eps));
+                bst4(bam, off[u], a1[u]);
+                bst4(bas, off[u], a2[u]);
+                bst4(bm, off[u], m[u]);
+                bst4(bs, off[u], s[u]);
             }
         }
     }
-    tp = block_sum256(tp, sh);
+    if (blockIdx.x == 0 && threadIdx.x < (P & 3)) {
+        const int64_t i = n4 * 4 + threadIdx.x;
+        float m = mu[i], s = sg[i], a1 = update ? am[i] : 0.f, a2 = update ? as[i] : 0.f;
+        f(m, s, a1, a2, tp);
+        if (update) { mu[i] = m; sg[i] = s; am[i] = a1; as[i] = a2; }
+    }
+    tp = block_sum256w(tp, sh);
     if (threadIdx.x == 0) part[blockIdx.x] = (float)tp;
 }
 

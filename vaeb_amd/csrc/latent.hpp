@@ -61,18 +61,78 @@ DEV bool arrive_last(int* cnt, int target, int* sflag) {
 // Grid (Mbp/16, ceil(H/16)), 512 threads: 8 waves split K = D.  Tile (bx, by) stores its
 // partial [mu | lv] slab column-major: slab[((bx * nctH + by) * 2Z + c) * 16 + m]
 // (c < Z: mu column c, c >= Z: lv column c - Z).
-template <int NCT, int GCH>
-__global__ __launch_bounds__(512) void enc_latent_kernel(StepArgs a) {
+// Literal-FV steps append a.fv_rows grid rows of blocks that run fv_kernel's update over
+// (mu, sigma) (kernels_aux.hpp: FvElem, same 16-byte group scheme), one thetaPrior partial
+// per block: the update needs none of the step's data, so it fills the CUs the 16x16
+// tiles leave idle instead of taking a launch of its own.
+DEV void fv_stream_block(const FvFold& a, int fb, int nfb, double* sh) {
+    const FvElem f{a.lr, a.eps, 1};
+    const int64_t P = a.P, T = (int64_t)nfb * 512, n4 = P >> 2;
+    const rsrc_t bm = mkbuf(a.mu, P * 4), bs = mkbuf(a.sg, P * 4);
+    const rsrc_t bam = mkbuf(a.am, P * 4), bas = mkbuf(a.as, P * 4);
+    double tp = 0;
+    constexpr int U = 2;
+    for (int64_t g0 = (int64_t)fb * 512 + threadIdx.x; g0 < n4; g0 += U * T) {
+        uint32_t off[U];
+        f32x4 m[U], s[U], a1[U], a2[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            fv_group(g0 + u * T, n4, off[u]);
+            m[u] = bld4(bm, off[u]);
+            s[u] = bld4(bs, off[u]);
+            a1[u] = bld4(bam, off[u]);
+            a2[u] = bld4(bas, off[u]);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if (off[u] == kOOB) continue;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                float mm = m[u][k], ss = s[u][k], x1 = a1[u][k], x2 = a2[u][k];
+                f(mm, ss, x1, x2, tp);
+                m[u][k] = mm; s[u][k] = ss; a1[u][k] = x1; a2[u][k] = x2;
+            }
+            bst4(bam, off[u], a1[u]);
+            bst4(bas, off[u], a2[u]);
+            bst4(bm, off[u], m[u]);
+            bst4(bs, off[u], s[u]);
+        }
+    }
+    if (fb == 0 && threadIdx.x < (P & 3)) {
+        const int64_t i = n4 * 4 + threadIdx.x;
+        float m = a.mu[i], s = a.sg[i], x1 = a.am[i], x2 = a.as[i];
+        f(m, s, x1, x2, tp);
+        a.mu[i] = m; a.sg[i] = s; a.am[i] = x1; a.as[i] = x2;
+    }
+    tp = wave_sum64(tp);
+    if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = tp;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double r = sh[0];
+#pragma unroll
+        for (int w = 1; w < 8; ++w) r += sh[w];
+        a.part[fb] = (float)r;
+    }
+}
+
+template <int NCT, int GCH, bool FV>
+DEV void enc_latent_body(const StepArgs& a, const FvFold& fvf) {
     __shared__ f32x4 red[512];
     __shared__ float hs[16][20];
     __shared__ int sflag;
+    const int nctH = FV ? (a.H + 15) >> 4 : (int)gridDim.y;   // FV: rows beyond run the stream
+    if (FV && (int)blockIdx.y >= nctH) {
+        fv_stream_block(fvf, (blockIdx.y - nctH) * gridDim.x + blockIdx.x, (gridDim.y - nctH) * gridDim.x,
+                        reinterpret_cast<double*>(red));
+        return;
+    }
     VAEB_STAMP(a, 0);
     PEnc p{a, nullptr, a.Mbp, a.H, a.D};
     p.prepare();
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int li = lane & 15, q = lane >> 4;
-    const int lin = xcd_remap(blockIdx.x + blockIdx.y * gridDim.x, gridDim.x * gridDim.y);
-    const int bx = lin % gridDim.x, by = lin / gridDim.x, nctH = gridDim.y;
+    const int lin = xcd_remap(blockIdx.x + blockIdx.y * gridDim.x, gridDim.x * nctH);
+    const int bx = lin % gridDim.x, by = lin / gridDim.x;
     const int m0 = bx * 16, n0 = by * 16;
     const int Z = a.Z, H = a.H;
     const rsrc_t bs = mkbuf(a.slab_ml, (int64_t)gridDim.x * nctH * 2 * Z * 16 * 4);
@@ -202,6 +262,14 @@ __global__ __launch_bounds__(512) void enc_latent_kernel(StepArgs a) {
         if (n < a.nctZ) a.kl_part[(int64_t)m * a.nctZ + n] = (n == 0) ? kl : 0.f;
     }
     VAEB_STAMP(a, 5);
+}
+template <int NCT, int GCH>
+__global__ __launch_bounds__(512) void enc_latent_kernel(StepArgs a) {
+    enc_latent_body<NCT, GCH, false>(a, FvFold{});
+}
+template <int NCT, int GCH>
+__global__ __launch_bounds__(512) void enc_latent_fv_kernel(StepArgs a, FvFold f) {
+    enc_latent_body<NCT, GCH, true>(a, f);
 }
 
 // ----------------------------------------------------------------------------- P4'

@@ -60,6 +60,16 @@ struct StepArgs {
     uint64_t* dbg;         // diagnostics: per-workgroup s_memrealtime stamps (null = off)
 };
 
+// Literal FV training step: the (mu, sigma) Adagrad stream of fv_kernel rides
+// enc_latent_fv_kernel's `rows` extra grid rows beyond ceil(H/16) (latent.hpp).  A kernel
+// argument of its own, so StepArgs (every phase's kernarg) keeps its size.
+struct FvFold {
+    float *mu, *sg, *am, *as, *part;
+    int64_t P;
+    float lr, eps;
+    int rows;
+};
+
 
 
 // P1 resolves the minibatch index from the device-side batch order; every later phase

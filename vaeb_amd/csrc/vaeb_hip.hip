@@ -69,7 +69,7 @@ int dalloc(T** p, size_t n) {
 
 // Control block layout (ints): [0] cursor, [1] resolved batch, [2..] batch order.
 constexpr int kOrderCap = 1 << 20;
-constexpr int kFvParts = 512;
+constexpr int kFvParts = 1024;   // FV stream grid (one thetaPrior partial per block)
 constexpr int kGraphSteps = 32;
 constexpr int kMaxProfKernels = 24;
 constexpr int kDbgWG = 1024;      // diagnostics: stamp slots per launch (workgroups)
@@ -261,16 +261,24 @@ bool folded_latent(const vaeb_ctx* c, const StepArgs& a) {
 }
 
 // Forward phases P1..P4 for any mode.
-int enqueue_forward(vaeb_ctx* c, const StepArgs& a0, Prof& pr) {
+int enqueue_forward(vaeb_ctx* c, const StepArgs& a0, Prof& pr, const FvFold& fvf = FvFold{}) {
     hipStream_t s = c->s;
     StepArgs a = a0;
     a.dbg = next_dbg(c);
     if (folded_latent(c, a)) {
-        const dim3 g1(a.Mbp / 16, cdiv(a.H, 16));
+        const dim3 g1(a.Mbp / 16, cdiv(a.H, 16) + fvf.rows);
         const bool deep = cdiv(cdiv(a.D, 16), 8) > 4;
         pr.mark(16);
         REP(pr) {
-            if (a.Z <= 16) {
+            if (fvf.rows > 0) {
+                if (a.Z <= 16) {
+                    if (deep) hipLaunchKernelGGL((enc_latent_fv_kernel<1, 8>), g1, dim3(512), 0, s, a, fvf);
+                    else hipLaunchKernelGGL((enc_latent_fv_kernel<1, 4>), g1, dim3(512), 0, s, a, fvf);
+                } else {
+                    if (deep) hipLaunchKernelGGL((enc_latent_fv_kernel<2, 8>), g1, dim3(512), 0, s, a, fvf);
+                    else hipLaunchKernelGGL((enc_latent_fv_kernel<2, 4>), g1, dim3(512), 0, s, a, fvf);
+                }
+            } else if (a.Z <= 16) {
                 if (deep) hipLaunchKernelGGL((enc_latent_kernel<1, 8>), g1, dim3(512), 0, s, a);
                 else hipLaunchKernelGGL((enc_latent_kernel<1, 4>), g1, dim3(512), 0, s, a);
             } else {
@@ -481,17 +489,30 @@ int enqueue_train_step(vaeb_ctx* c, int par, bool prof) {
         par ^= 1;
     }
     StepArgs a = make_args(c, par, g.B, g.estimator == VAEB_EST_FV ? MODE_EVAL : MODE_TRAIN, c->data, true);
-    if (int rc = enqueue_forward(c, a, pr)) return rc;
+    // literal FV: the (mu, sigma) update needs none of the step's data; with the folded
+    // latent block it rides enc_latent_kernel's extra grid rows (~256 blocks), else it is
+    // fv_kernel's launch
+    const bool fv_fold = g.estimator == VAEB_EST_FV && folded_latent(c, a);
+    int n_fv = kFvParts;
+    FvFold fvf{};
+    if (fv_fold) {
+        fvf = FvFold{c->fvmu, c->fvsg, c->fvam, c->fvas, c->fv_part, c->P, g.lr, g.adagrad_eps, cdiv(256, a.Mbp / 16)};
+        n_fv = fvf.rows * (a.Mbp / 16);
+        if (n_fv > kFvParts) return fail(VAEB_ERR_ARG, "internal: %d FV partials > %d", n_fv, kFvParts);
+    }
+    if (int rc = enqueue_forward(c, a, pr, fvf)) return rc;
     ElboArgs e = base_elbo(c, a);
     e.elbo_out = c->elbo_out; e.epoch = c->epoch; e.cursor = c->ictl; e.step = c->step;
 
     if (g.estimator == VAEB_EST_FV) {
-        pr.mark(10);
-        REP(pr) hipLaunchKernelGGL(fv_kernel, dim3(kFvParts), dim3(256), 0, s, c->fvmu, c->fvsg, c->fvam, c->fvas,
-                           c->P, g.lr, g.adagrad_eps, 1, c->fv_part);
-        CHECK_LAUNCH();
+        if (!fv_fold) {
+            pr.mark(10);
+            REP(pr) hipLaunchKernelGGL(fv_kernel, dim3(kFvParts), dim3(256), 0, s, c->fvmu, c->fvsg, c->fvam,
+                                       c->fvas, c->P, g.lr, g.adagrad_eps, 1, c->fv_part);
+            CHECK_LAUNCH();
+        }
         pr.mark(11);
-        e.fv_part = c->fv_part; e.n_fv = kFvParts;
+        e.fv_part = c->fv_part; e.n_fv = n_fv;
         e.data_mul = (double)g.B;
         hipLaunchKernelGGL(elbo_kernel, dim3(1), dim3(256), 0, s, e);
         CHECK_LAUNCH();
