@@ -13,6 +13,9 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libvaeb_hip.so")
+# diagnostics A/B only: an alternative in-tree build of the same library (scripts/)
+if os.environ.get("VAEB_LIB_VARIANT"):
+    LIB_PATH = os.path.join(HERE, f"libvaeb_hip_{os.environ['VAEB_LIB_VARIANT']}.so")
 
 DEC_BERNOULLI, DEC_GAUSSIAN = 0, 1
 EST_LB, EST_LA, EST_FV, EST_FVS = 0, 1, 2, 3   # FVS: weight-sampling extension (include/vaeb_hip.h)
