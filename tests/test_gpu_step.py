@@ -288,6 +288,33 @@ def test_fv_weight_sampling_step(continuous):
     ctx.close()
 
 
+def test_fv_weight_sampling_philox_graph_matches_eager():
+    """VAEB_EST_FVS in Philox mode: a graph-replayed sequence draws the weight sample once
+    and then reads the one each fvs_update wrote for the next step (zeta(step + 1)); eager
+    steps draw it every step.  The two must agree bit for bit over 40 steps (one 32-step
+    replay plus single-step graphs), and the literal FV path likewise."""
+    for est in ("FVS", "FV"):
+        cfg = O.Config(D=784, H=500, Z=20, estimator=est)
+        x = data_for(cfg, 1000)
+        theta = O.init_params(cfg)
+        order = np.random.default_rng(4).integers(0, 10, 40).astype(np.int32)
+        outs = []
+        for use_graph in (True, False):
+            ctx = make_ctx(cfg, 100, keep_grads=False, use_graph=use_graph)
+            ctx.set_data(x)
+            ctx.set_params(O.flatten(theta))
+            t = O.flatten(theta)
+            ctx.set_fv_state(t, np.full_like(t, 1e-3), np.zeros_like(t), np.zeros_like(t))
+            ctx.set_eps_mode(0, 10)
+            ctx.set_step(0)
+            ctx.update_many(order)
+            outs.append((ctx.epoch_elbo(), ctx.get_fv_state()))
+            ctx.close()
+        assert outs[0][0] == outs[1][0], (est, outs[0][0], outs[1][0])
+        for a, b in zip(outs[0][1], outs[1][1]):
+            assert np.array_equal(a, b), est
+
+
 def test_philox_eps_is_standard_normal_and_deterministic():
     cfg = O.Config(D=784, H=500, Z=20)
     x = data_for(cfg, 1000)

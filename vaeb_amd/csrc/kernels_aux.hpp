@@ -404,9 +404,28 @@ __global__ __launch_bounds__(256) void adagrad_kernel(OptArgs o, int64_t P, DpRa
 // data term of getFVBL (VAEB.py:349-367); criterion as the literal path (VAEB.py:386-399).
 // zeta: host buffer, or Philox keyed by (seed, step, parameter index) on a counter range
 // disjoint from the latent noise (c1 bit 30).
+// One Philox block per 16-byte group g of parameters: both Box-Muller pairs of its four
+// outputs give the group's four normals.
+DEV f32x4 fvs_zeta4(int64_t g, uint64_t seed, int64_t step) {
+    uint32_t ctr[4] = {(uint32_t)g, 0x40000000u | (uint32_t)(g >> 32), 0u, 0u};
+    const uint64_t c23 = philox_c23(step, 0);
+    ctr[2] = (uint32_t)c23;
+    ctr[3] = (uint32_t)(c23 >> 32);
+    philox4x32(ctr, (uint32_t)seed, (uint32_t)(seed >> 32));
+    const float r0 = __builtin_amdgcn_sqrtf(-2.0f * flog(((float)(ctr[0] >> 8) + 1.0f) * (1.0f / 16777216.0f)));
+    const float r1 = __builtin_amdgcn_sqrtf(-2.0f * flog(((float)(ctr[2] >> 8) + 1.0f) * (1.0f / 16777216.0f)));
+    const float t0 = (float)(ctr[1] >> 8) * (1.0f / 16777216.0f);   // revolutions
+    const float t1 = (float)(ctr[3] >> 8) * (1.0f / 16777216.0f);
+    f32x4 z;
+    z[0] = r0 * __builtin_amdgcn_cosf(t0);
+    z[1] = r0 * __builtin_amdgcn_sinf(t0);
+    z[2] = r1 * __builtin_amdgcn_cosf(t1);
+    z[3] = r1 * __builtin_amdgcn_sinf(t1);
+    return z;
+}
 DEV float fvs_zeta(int64_t i, const float* zin, uint64_t seed, int64_t step) {
     if (zin) return zin[i];
-    return philox_normal(seed, (uint32_t)i, 0x40000000u | (uint32_t)(i >> 32), philox_c23(step, 0));
+    return fvs_zeta4(i >> 2, seed, step)[i & 3];
 }
 // The (mu, sigma) streams below move 16-byte groups: thread t of the grid takes groups
 // t, t + T, ... (U per round trip, every load before any store), the P % 4 tail elements
@@ -438,12 +457,10 @@ __global__ __launch_bounds__(256) void fvs_sample_kernel(const float* mu, const 
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             if (off[u] == kOOB) continue;
+            const f32x4 zz = zin ? z[u] : fvs_zeta4(g0 + u * T, seed, stp);
             f32x4 t;
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const float zz = zin ? z[u][k] : fvs_zeta((g0 + u * T) * 4 + k, nullptr, seed, stp);
-                t[k] = m[u][k] + fabsf(s[u][k]) * zz;
-            }
+            for (int k = 0; k < 4; ++k) t[k] = m[u][k] + fabsf(s[u][k]) * zz[k];
             bst4(bt, off[u], t);
         }
     }
@@ -457,6 +474,8 @@ __global__ __launch_bounds__(256) void fvs_sample_kernel(const float* mu, const 
 //   d/dmu    = B G - 2 mu                                  (thetaPrior -mu, L2 -mu)
 //   d/dsigma = B G zeta sign(sigma) + 1/sigma - 2 sigma    (thetaPrior 1/sigma - sigma, L2 -sigma)
 // then Adagrad on both (VAEB.py:426-444); thetaPrior partials from the pre-update values.
+// next_theta (Philox mode): also writes the next step's sample mu' + |sigma'| zeta(step + 1),
+// so a graph-replayed sequence draws it once, at its first step.
 struct FvsElem {
     float B, lr, eps;
     DEV void operator()(float& m, float& s, float& a1, float& a2, float G, float zz, double& tp) const {
@@ -471,10 +490,12 @@ struct FvsElem {
 };
 __global__ __launch_bounds__(256) void fvs_update_kernel(float* mu, float* sg, float* am, float* as, const float* grad,
                                                         int64_t P, float B, float lr, float eps, uint64_t seed,
-                                                        const int64_t* step, const float* zin, float* part) {
+                                                        const int64_t* step, const float* zin, float* part,
+                                                        float* next_theta) {
     __shared__ double sh[256];
     double tp = 0;
     const FvsElem f{B, lr, eps};
+    const rsrc_t bn = mkbuf(next_theta, next_theta ? P * 4 : 0);
     const int64_t T = (int64_t)gridDim.x * 256, n4 = P >> 2;
     const int64_t stp = *step;
     const rsrc_t bm = mkbuf(mu, P * 4), bs = mkbuf(sg, P * 4), bam = mkbuf(am, P * 4), bas = mkbuf(as, P * 4);
@@ -496,22 +517,30 @@ __global__ __launch_bounds__(256) void fvs_update_kernel(float* mu, float* sg, f
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             if (off[u] == kOOB) continue;
+            const f32x4 zz = zin ? z[u] : fvs_zeta4(g0 + u * T, seed, stp);
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
-                const float zz = zin ? z[u][k] : fvs_zeta((g0 + u * T) * 4 + k, nullptr, seed, stp);
                 float mm = m[u][k], ss = s[u][k], x1 = a1[u][k], x2 = a2[u][k];
-                f(mm, ss, x1, x2, G[u][k], zz, tp);
+                f(mm, ss, x1, x2, G[u][k], zz[k], tp);
                 m[u][k] = mm; s[u][k] = ss; a1[u][k] = x1; a2[u][k] = x2;
             }
             bst4(bam, off[u], a1[u]);
             bst4(bas, off[u], a2[u]);
             bst4(bm, off[u], m[u]);
             bst4(bs, off[u], s[u]);
+            if (next_theta) {   // the next step's sample (Philox mode; fvs_sample_kernel's rule)
+                const f32x4 zn = fvs_zeta4(g0 + u * T, seed, stp + 1);
+                f32x4 t;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) t[k] = m[u][k] + fabsf(s[u][k]) * zn[k];
+                bst4(bn, off[u], t);
+            }
         }
     }
     if (blockIdx.x == 0 && threadIdx.x < (P & 3)) {
         const int64_t i = n4 * 4 + threadIdx.x;
         f(mu[i], sg[i], am[i], as[i], grad[i], fvs_zeta(i, zin, seed, stp), tp);
+        if (next_theta) next_theta[i] = mu[i] + fabsf(sg[i]) * fvs_zeta(i, nullptr, seed, stp + 1);
     }
     tp = block_sum256w(tp, sh);
     if (threadIdx.x == 0) part[blockIdx.x] = (float)tp;

@@ -471,7 +471,9 @@ int dp_bucket_b(vaeb_ctx* c, Prof& pr, int opt_mark, Opt opt) {
 // One stream: P1 -> P23 -> P4 -> [P5 | dW2 (| dW6)] -> [P67 | dW1] -> [dW3 | dW45 + ELBO]
 // (bracketed groups share one grid, see hfuse.hpp); DP adds all-reduce -> Adagrad.
 // `prof` brackets every launch with timing events.
-int enqueue_train_step(vaeb_ctx* c, int par, bool prof) {
+// fresh: first step of an enqueued sequence (VAEB_EST_FVS in Philox mode draws the weight
+// sample here; later steps of the sequence read the one their predecessor's update wrote).
+int enqueue_train_step(vaeb_ctx* c, int par, bool prof, bool fresh = true) {
     if (is_bf16(c)) return bf_train_step(c, par, prof);
     Prof pr{c, prof};
     if (prof) pr.reps = c->prof_reps;
@@ -481,13 +483,13 @@ int enqueue_train_step(vaeb_ctx* c, int par, bool prof) {
     // par ^ 1 (the loaded theta in arena par is never updated, as on the literal path)
     const bool fvs = g.estimator == VAEB_EST_FVS;
     const float* zin = (fvs && c->eps_mode == VAEB_EPS_HOST) ? c->fvzeta : nullptr;
-    if (fvs) {
+    if (fvs && (fresh || zin)) {
         pr.mark(37);
         REP(pr) hipLaunchKernelGGL(fvs_sample_kernel, dim3(kFvParts), dim3(256), 0, s, c->fvmu, c->fvsg,
                                    c->theta2[par ^ 1], c->P, c->seed, c->step, zin);
         CHECK_LAUNCH();
-        par ^= 1;
     }
+    if (fvs) par ^= 1;
     StepArgs a = make_args(c, par, g.B, g.estimator == VAEB_EST_FV ? MODE_EVAL : MODE_TRAIN, c->data, true);
     // literal FV: the (mu, sigma) update needs none of the step's data; with the folded
     // latent block it rides enc_latent_kernel's extra grid rows (~256 blocks), else it is
@@ -602,7 +604,7 @@ int enqueue_train_step(vaeb_ctx* c, int par, bool prof) {
         pr.mark(38);
         REP(pr) hipLaunchKernelGGL(fvs_update_kernel, dim3(kFvParts), dim3(256), 0, s, c->fvmu, c->fvsg, c->fvam,
                                    c->fvas, (const float*)c->grad, c->P, (float)g.B, g.lr, g.adagrad_eps, c->seed,
-                                   (const int64_t*)c->step, zin, c->fv_part);
+                                   (const int64_t*)c->step, zin, c->fv_part, zin ? nullptr : c->theta2[par]);
         CHECK_LAUNCH();
         pr.mark(11);
         e.fv_part = c->fv_part; e.n_fv = kFvParts;
@@ -631,7 +633,7 @@ int capture(vaeb_ctx* c, int nsteps, int par, hipGraphExec_t* out) {
     HIP_TRY(hipStreamBeginCapture(c->s, hipStreamCaptureModeThreadLocal));
     int rc = 0;
     for (int i = 0; i < nsteps && rc == 0; ++i) {
-        rc = enqueue_train_step(c, par, false);
+        rc = enqueue_train_step(c, par, false, i == 0);
         if (flips(c)) par ^= 1;
     }
     hipError_t e = hipStreamEndCapture(c->s, &gr);
