@@ -85,7 +85,8 @@ KERNEL_SYMBOLS = {"p1_enc": "PEnc", "p23_heads_dechid": "heads_dechid_kernel", "
                   "p5_dhd_w2": "vaeb::tile_wgrad_kernel", "p67_dz_dh_w1": "vaeb::dz_dh_wgrad_kernel",
                   "fv_update": "vaeb::fv_kernel", "fvs_update": "vaeb::fvs_update_kernel",
                   "fvs_sample": "vaeb::fvs_sample_kernel",
-                  "p8_wgrad_w3w45": "vaeb::wgrad_kernel", "p1_enc_latent": "vaeb::enc_latent_kernel",
+                  "p8_wgrad_w3w45": "vaeb::wgrad_kernel",
+                  "p1_enc_latent": ("vaeb::enc_latent",),   # enc_latent_kernel | enc_latent_fv_kernel
                   "p4_decout_z": "vaeb::decout_z_kernel",
                   # bf16 GEMMs are one template: the epilogue / layout pair names the launch
                   # (all listed substrings must appear: the tile width is a template argument)
@@ -314,9 +315,9 @@ def main():
     # per-kernel device time (HIP events on the context's stream), after the timed region
     prof = ctx.profile_steps(50 if not bf16 else 5)
     fl = phase_flops(D, H, Z, B, gaussian=gauss)
-    if fv:   # the (mu, sigma) updates stream 32 B per parameter (+ the gradient, FVS)
-        fl["fv_update"] = 32 * ctx.P
-        fl["fvs_update"] = 36 * ctx.P
+    if fv:   # the (mu, sigma) updates stream 32 B per parameter (FVS: + the gradient read and
+        fl["fv_update"] = 32 * ctx.P   # the next step's sample written, Philox mode)
+        fl["fvs_update"] = 40 * ctx.P
         fl["fvs_sample"] = 12 * ctx.P
     dom = max((k for k in prof if k[0] in fl), key=lambda k: k[1])
     traffic = committed_traffic(dom[0], PMC_FILES.get(args.config, ""))
