@@ -56,6 +56,10 @@ CASES = [
     ("wide_latent_generic", dict(D=64, H=40, Z=40, L=2), 20),
     ("wide_latent_LA", dict(D=66, H=48, Z=36, estimator="LA"), 30),
     ("gauss_odd_D", dict(D=45, H=30, Z=6, continuous=True), 17),
+    ("batch1", dict(D=784, H=500, Z=20), 1),                 # a single-row minibatch
+    ("latent1_LA_L2", dict(D=30, H=17, Z=1, estimator="LA", L=2), 5),
+    ("mnist_B1024", dict(D=784, H=500, Z=20), 1024),         # fp32 engine at a large batch
+    ("gauss_B333", dict(D=560, H=200, Z=2, continuous=True), 333),
 ]
 
 
