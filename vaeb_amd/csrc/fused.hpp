@@ -195,8 +195,13 @@ __global__ __launch_bounds__(512) void heads_dechid_kernel(StepArgs a) {
 }
 
 // ---------------------------------------------------------------------------- P67
+// Column split: nsp workgroups share row block i0; each recomputes stages 1-2 (dZ and
+// [dMu | dLv] need the whole K = H reduction, ~100 KB of operands) and runs stage 3 for
+// its 1/nsp of the H columns only, so the per-CU operand stream on this critical-path
+// phase falls from ~250 KB (stage-3 [W4|W5] and h for all H columns) to ~130 KB at nsp = 4.
+// Split 0 alone stores dZ and [dMu | dLv].
 template <int NCT>
-DEV void dz_dh_body(const StepArgs& a, int i0) {
+DEV void dz_dh_body(const StepArgs& a, int i0, int sp, int nsp) {
     __shared__ f32x4 red[8][NCT][64];
     __shared__ float dml[16][kKP];     // [dMu | dLv] tile (A operand of the dA3 GEMM)
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -227,6 +232,7 @@ DEV void dz_dh_body(const StepArgs& a, int i0) {
     const rsrc_t bw5 = mkbuf(a.W5, (int64_t)H * Z * 4);
     const rsrc_t bhh = mkbuf(a.h, (int64_t)a.Mbp * H * 4);
     const int nctH = (H + 15) >> 4;
+    const int tper = (nctH + nsp - 1) / nsp, t_lo = sp * tper, t_hi = min(nctH, t_lo + tper);
     const bool vz = (Z & 3) == 0 && aligned16(a.W4) && aligned16(a.W5);
     auto ldw45 = [&](int nn, int k) {
         if (vz) return (k < Z) ? kc4(bw4, Z, nn, k, H, Z, true) : kc4(bw5, Z, nn, k - Z, H, Z, true);
@@ -252,7 +258,8 @@ DEV void dz_dh_body(const StepArgs& a, int i0) {
     f32x4 w45pre[4][2 * NCT], hpre[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-        const int nn = (wave + 8 * u) * 16 + li;
+        const int t = t_lo + wave + 8 * u;
+        const int nn = t < t_hi ? t * 16 + li : H;   // H: out of range, no fetch
 #pragma unroll
         for (int c = 0; c < 2 * NCT; ++c) w45pre[u][c] = ldw45(nn, c * 16 + 4 * q);
         hpre[u] = ldh(nn);
@@ -299,7 +306,7 @@ DEV void dz_dh_body(const StepArgs& a, int i0) {
             const float e = (l < kLP) ? epre[l] : (valid ? a.eps[((int64_t)l * a.Mbp + m) * Z + j] : 0.f);
             dzsum += dz;
             dzes += dz * e;
-            if (j < Z) a.dZ[((int64_t)l * a.Mbp + m) * Z + j] = dz;
+            if (j < Z && sp == 0) a.dZ[((int64_t)l * a.Mbp + m) * Z + j] = dz;
         }
         __syncthreads();
     }
@@ -329,8 +336,10 @@ DEV void dz_dh_body(const StepArgs& a, int i0) {
         }
         dml[ml][j] = dmu;
         dml[ml][Z + j] = dlv;
-        a.dMuLv[(int64_t)m * 2 * Z + j] = dmu;
-        a.dMuLv[(int64_t)m * 2 * Z + Z + j] = dlv;
+        if (sp == 0) {
+            a.dMuLv[(int64_t)m * 2 * Z + j] = dmu;
+            a.dMuLv[(int64_t)m * 2 * Z + Z + j] = dlv;
+        }
     }
     VAEB_STAMP(a, 2);
     __syncthreads();
@@ -355,10 +364,10 @@ DEV void dz_dh_body(const StepArgs& a, int i0) {
     };
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-        const int t = wave + 8 * u;
-        if (t < nctH) tile3(t, w45pre[u], hpre[u]);
+        const int t = t_lo + wave + 8 * u;
+        if (t < t_hi) tile3(t, w45pre[u], hpre[u]);
     }
-    for (int t = wave + 32; t < nctH; t += 8) {
+    for (int t = t_lo + wave + 32; t < t_hi; t += 8) {
         f32x4 bw[2 * NCT];
 #pragma unroll
         for (int c = 0; c < 2 * NCT; ++c) bw[c] = ldw45(t * 16 + li, c * 16 + 4 * q);
@@ -370,7 +379,7 @@ DEV void dz_dh_body(const StepArgs& a, int i0) {
 template <int NCT>
 __global__ __launch_bounds__(512) void dz_dh_kernel(StepArgs a) {
     VAEB_STAMP(a, 0);
-    dz_dh_body<NCT>(a, blockIdx.x * 16);
+    dz_dh_body<NCT>(a, blockIdx.x * 16, 0, 1);
 }
 
 }  // namespace vaeb

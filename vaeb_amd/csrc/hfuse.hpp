@@ -4,7 +4,7 @@
 // side stream inside a hipGraph measured ~12 us/step slower than one stream).
 //
 //   P5  (dhd, 224 tiles at MNIST-20) + dW2|dW6 (104 tiles)   -- both need only P4's output
-//   P67 (dz/dh, 7 row blocks)         + dW1 (8 tiles)         -- both need only P5's output
+//   P67 (dz/dh, 7 row blocks x 4 column splits) + dW1 (8 tiles) -- both need only P5's output
 //
 // Phase blocks come first in the grid (they gate the next launch); all blocks are 512
 // threads, so the weight-gradient tiles use the 8-wave K-split form.
@@ -39,9 +39,10 @@ __global__ __launch_bounds__(512) void dz_dh_wgrad_kernel(StepArgs a, WGradArgs 
     __shared__ float sb[kWKB][kWP];
     const int b0 = blockIdx.x;
     const int bid = b0 < nrow ? b0 : nrow + xcd_remap(b0 - nrow, (int)gridDim.x - nrow);
-    if (bid < nrow) {
+    if (bid < nrow) {   // nrow = row blocks x column splits, split-major
         VAEB_STAMP(a, 0);
-        dz_dh_body<NCT>(a, bid * 16);
+        const int nrb = a.Mbp >> 4;
+        dz_dh_body<NCT>(a, (bid % nrb) * 16, bid / nrb, nrow / nrb);
         return;
     }
     if (w.dbg && threadIdx.x == 0) w.dbg[bid * 8 + 0] = __builtin_amdgcn_s_memrealtime();

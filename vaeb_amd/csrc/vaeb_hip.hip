@@ -136,6 +136,7 @@ struct vaeb_ctx {
     hipStream_t s2 = nullptr;     // DP: the gradient buckets' all-reduces and their Adagrad
     hipEvent_t dp_ev[3] = {};     // fork after dW2, bucket A reduced, bucket A updated
     bool dp_overlap = false;      // bucket A on s2 (bf16 engine; VAEB_DP_OVERLAP=0/1 overrides)
+    int dz_split = 4;             // P67 column splits per row block (fused.hpp dz_dh_body; VAEB_DZ_SPLIT)
     // profiling
     hipEvent_t pev[kMaxProfKernels + 1] = {};
     int prof_n = 0, prof_reps = 1;
@@ -561,7 +562,7 @@ int enqueue_train_step(vaeb_ctx* c, int par, bool prof, bool fresh = true) {
     {
         WGroup g3 = make_group(c, c->z, a.Z, a.Me, 0, a.Z, c->dA1, a.H, a.H, nullptr, 0, 0, a.Me, 3, bo + 3, -1, -1);
         if (fused_latent(c)) {
-            const int nrow = a.Mbp / 16;
+            const int nrow = a.Mbp / 16 * std::max(1, std::min(c->dz_split, cdiv(a.H, 16)));
             WGradArgs w;
             bool vec;
             if (int rc = prep_wgrad(c, &g3, 1, opt, nullptr, a, nrow, w, vec)) return rc;
@@ -740,6 +741,7 @@ int vaeb_create(const vaeb_config* cfg, vaeb_ctx** out) {
     hipError_t e = hipSetDevice(g.device);
     if (e != hipSuccess) { delete c; return fail(VAEB_ERR_HIP, "hipSetDevice(%d): %s", g.device, hipGetErrorString(e)); }
     e = hipStreamCreateWithFlags(&c->s, hipStreamNonBlocking);
+    if (const char* ds = getenv("VAEB_DZ_SPLIT")) c->dz_split = atoi(ds);
     if (e != hipSuccess) { delete c; return fail(VAEB_ERR_HIP, "stream/event create: %s", hipGetErrorString(e)); }
     const int64_t D = g.D, H = g.H, Z = g.Z;
     std::vector<int64_t> sz = {D * H, H * Z, H * Z, Z * H, H * D};
