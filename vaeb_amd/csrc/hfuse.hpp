@@ -14,7 +14,7 @@
 
 namespace vaeb {
 
-template <int WM, int WN, int KS, int NB, int GCH, class P, bool VEC>
+template <int WM, int WN, int KS, int NB, int GCH, class P, bool VEC, int TS>
 __global__ __launch_bounds__(512) void tile_wgrad_kernel(P p0, WGradArgs w, int ntile, int gx) {
     static_assert(WM * WN * KS == 8, "fused launches are 512 threads");
     __shared__ float sa[kWKB][kWP];
@@ -30,10 +30,10 @@ __global__ __launch_bounds__(512) void tile_wgrad_kernel(P p0, WGradArgs w, int 
         return;
     }
     if (w.dbg && threadIdx.x == 0) w.dbg[bid * 8 + 0] = __builtin_amdgcn_s_memrealtime();
-    wgrad_body<VEC, 8>(w, w.g[0], bid, sa, sb);
+    wgrad_body<VEC, 8, TS>(w, w.g[0], bid, sa, sb);
 }
 
-template <int NCT, bool VEC>
+template <int NCT, bool VEC, int TS>
 __global__ __launch_bounds__(512) void dz_dh_wgrad_kernel(StepArgs a, WGradArgs w, int nrow) {
     __shared__ float sa[kWKB][kWP];
     __shared__ float sb[kWKB][kWP];
@@ -46,7 +46,7 @@ __global__ __launch_bounds__(512) void dz_dh_wgrad_kernel(StepArgs a, WGradArgs 
         return;
     }
     if (w.dbg && threadIdx.x == 0) w.dbg[bid * 8 + 0] = __builtin_amdgcn_s_memrealtime();
-    wgrad_body<VEC, 8>(w, w.g[0], bid, sa, sb);
+    wgrad_body<VEC, 8, TS>(w, w.g[0], bid, sa, sb);
 }
 
 }  // namespace vaeb

@@ -166,7 +166,7 @@ DEV float opt_rule(const OptArgs& o, float th, float& acc, float dsg) {
 // reads over the banks), then wave w computes rows 16w..16w+15 x 64 columns
 // (4 accumulators sharing one A fragment).  The epilogue applies prior + Adagrad
 // (theta / acc prefetched before the panels) or stores the gradient (DP / introspection).
-constexpr int kWT = 64;
+constexpr int kWT = 64;   // weight rows (i) per tile; the columns per tile are 16 * TS (wgrad_body)
 constexpr int kWKB = 128;
 constexpr int kWP = 68;
 
@@ -191,19 +191,21 @@ struct WGradArgs {
     uint64_t* dbg;
 };
 
-// One 64 x 64 tile of group g (passed with a compile-time index, so its fields are
+// One 64 x (16 TS) tile of group g (passed with a compile-time index, so its fields are
 // scalar kernel-argument loads; a dynamic index made hipcc fetch them with serialized
 // per-lane vector loads).  NWV = 4 waves (standalone launch) or 8 (a 512-thread fused
 // launch): waves w and w + 4 then take alternate K chunks and are summed through LDS.
-template <bool VEC, int NWV>
+template <bool VEC, int NWV, int TS>
 DEV void wgrad_body(const WGradArgs& p, const WGroup& g, int bid, float (*sa)[kWP], float (*sb)[kWP]) {
     static_assert(NWV == 4 || NWV == 8, "wgrad: 4 or 8 waves");
+    static_assert(TS == 1 || TS == 2 || TS == 4, "wgrad: 16, 32 or 64 columns per tile");
+    constexpr int kWTS = TS, kWTJ = 16 * TS;
     constexpr int NTH = 64 * NWV;
     // resolve the batch pointer first: its load must not queue behind the prefetches below
     const float* at = g.at_is_x ? p.xbase + (int64_t)__builtin_amdgcn_readfirstlane(*p.cur_batch) * p.batch_stride : g.at;
     const rsrc_t ba = mkbuf(at, (int64_t)g.klim_at * g.ld_at * 4);
     const int lt = bid - g.wg_begin;
-    const int i0 = (lt / g.tiles_j) * kWT, j0 = (lt % g.tiles_j) * kWT;
+    const int i0 = (lt / g.tiles_j) * kWT, j0 = (lt % g.tiles_j) * kWTJ;
     const int lane = threadIdx.x & 63, wave = (threadIdx.x >> 6) & 3, kh = threadIdx.x >> 8;
     const int li = lane & 15, q = lane >> 4;
     const int NT = g.N0 + g.N1;
@@ -211,10 +213,10 @@ DEV void wgrad_body(const WGradArgs& p, const WGroup& g, int bid, float (*sa)[kW
     // ---- prefetch theta / acc of this lane's 16 outputs (rows i0+16w+4q+r, cols j0+16t+li)
     const bool upd = p.opt.update != 0;
     const rsrc_t bth = mkbuf(p.opt.theta_in, p.P * 4), bac = mkbuf(p.opt.acc, p.P * 4);
-    uint32_t off[4][4];
-    float th[4][4], ac[4][4];
+    uint32_t off[kWTS][4];
+    float th[kWTS][4], ac[kWTS][4];
 #pragma unroll
-    for (int t = 0; t < 4; ++t) {
+    for (int t = 0; t < kWTS; ++t) {
         const int j = j0 + 16 * t + li;
         const bool s1 = j >= g.N0;
         const int jj = s1 ? j - g.N0 : j;
@@ -239,9 +241,9 @@ DEV void wgrad_body(const WGradArgs& p, const WGroup& g, int bid, float (*sa)[kW
     const rsrc_t bb1 = mkbuf(g.b1 ? g.b1 : g.b0, (int64_t)g.K * (g.b1 ? g.ld1 : g.ld0) * 4);
     // VEC (chosen on the host): every panel row is 16-byte aligned with widths % 4 == 0
     constexpr bool va = VEC, vb = VEC;
-    f32x4 acc[4];
+    f32x4 acc[kWTS];
 #pragma unroll
-    for (int t = 0; t < 4; ++t) acc[t] = zero4();
+    for (int t = 0; t < kWTS; ++t) acc[t] = zero4();
     int kb = 0;
     do {  // K >= 1 always; a do-loop keeps the pre-loop loads off the exit path
         // stage the panels: element e = (row kr, float4 column c4).  All 16 loads of a
@@ -254,6 +256,7 @@ DEV void wgrad_body(const WGradArgs& p, const WGroup& g, int bid, float (*sa)[kW
             const int kr = e >> 4, c4 = e & 15;
             const int k = kb + kr;
             const int i = i0 + 4 * c4, j = j0 + 4 * c4;
+            const bool jt = 4 * c4 < kWTJ;   // B columns beyond a narrow tile: no fetch
             if (va) {
                 ra[u] = bld4(ba, (k < g.klim_at && i < g.rowsW) ? (uint32_t)(k * g.ld_at + i) * 4u : kOOB);
             } else {
@@ -263,16 +266,16 @@ DEV void wgrad_body(const WGradArgs& p, const WGroup& g, int bid, float (*sa)[kW
             }
             if (vb) {
                 const bool in0 = j < g.N0;
-                const uint32_t o0 = (k < g.K && in0) ? (uint32_t)(k * g.ld0 + j) * 4u : kOOB;
-                const uint32_t o1 = (k < g.K && !in0 && j - g.N0 < g.N1) ? (uint32_t)(k * g.ld1 + j - g.N0) * 4u : kOOB;
+                const uint32_t o0 = (jt && k < g.K && in0) ? (uint32_t)(k * g.ld0 + j) * 4u : kOOB;
+                const uint32_t o1 = (jt && k < g.K && !in0 && j - g.N0 < g.N1) ? (uint32_t)(k * g.ld1 + j - g.N0) * 4u : kOOB;
                 rb[u] = in0 ? bld4(bb0, o0) : bld4(bb1, o1);
             } else {
 #pragma unroll
                 for (int s = 0; s < 4; ++s) {
                     const int jj = j + s;
                     const bool in0 = jj < g.N0;
-                    rb[u][s] = in0 ? bld(bb0, (k < g.K) ? (uint32_t)(k * g.ld0 + jj) * 4u : kOOB)
-                                   : bld(bb1, (k < g.K && jj - g.N0 < g.N1) ? (uint32_t)(k * g.ld1 + jj - g.N0) * 4u : kOOB);
+                    rb[u][s] = in0 ? bld(bb0, (jt && k < g.K) ? (uint32_t)(k * g.ld0 + jj) * 4u : kOOB)
+                                   : bld(bb1, (jt && k < g.K && jj - g.N0 < g.N1) ? (uint32_t)(k * g.ld1 + jj - g.N0) * 4u : kOOB);
                 }
             }
         }
@@ -296,7 +299,7 @@ DEV void wgrad_body(const WGradArgs& p, const WGroup& g, int bid, float (*sa)[kW
 #pragma unroll
             for (int s = 0; s < 4; ++s) a4[s] = sa[kk + s][16 * wave + li];
 #pragma unroll
-            for (int t = 0; t < 4; ++t) {
+            for (int t = 0; t < kWTS; ++t) {
                 f32x4 b4;
 #pragma unroll
                 for (int s = 0; s < 4; ++s) b4[s] = sb[kk + s][16 * t + li];
@@ -310,18 +313,18 @@ DEV void wgrad_body(const WGradArgs& p, const WGroup& g, int bid, float (*sa)[kW
         f32x4* red = reinterpret_cast<f32x4*>(&sa[0][0]);
         if (kh == 1)
 #pragma unroll
-            for (int t = 0; t < 4; ++t) red[(wave * 4 + t) * 64 + lane] = acc[t];
+            for (int t = 0; t < kWTS; ++t) red[(wave * 4 + t) * 64 + lane] = acc[t];
         __syncthreads();
         if (kh == 1) return;
 #pragma unroll
-        for (int t = 0; t < 4; ++t) acc[t] += red[(wave * 4 + t) * 64 + lane];
+        for (int t = 0; t < kWTS; ++t) acc[t] += red[(wave * 4 + t) * 64 + lane];
     }
     if (p.dbg && threadIdx.x == 0) p.dbg[bid * 8 + 1] = __builtin_amdgcn_s_memrealtime();
 
     // ---- epilogue: out-of-range byte offsets make masked buffer stores no-ops
     const rsrc_t bto = mkbuf(p.opt.theta_out, p.P * 4), bgr = mkbuf(p.opt.grad, p.P * 4);
 #pragma unroll
-    for (int t = 0; t < 4; ++t)
+    for (int t = 0; t < kWTS; ++t)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const float dsg = acc[t][r];
@@ -336,7 +339,7 @@ DEV void wgrad_body(const WGradArgs& p, const WGroup& g, int bid, float (*sa)[kW
     if (p.dbg && threadIdx.x == 0) p.dbg[bid * 8 + 3] = __builtin_amdgcn_s_memrealtime();
 }
 
-template <bool VEC>
+template <bool VEC, int TS>
 __global__ __launch_bounds__(256) void wgrad_kernel(WGradArgs p) {
     __shared__ float sa[kWKB][kWP];
     __shared__ float sb[kWKB][kWP];
@@ -346,8 +349,8 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WGradArgs p) {
         elbo_reduce(p.elbo, reinterpret_cast<double*>(&sa[0][0]));
         return;
     }
-    if (p.ngroups > 1 && bid >= p.g[1].wg_begin) wgrad_body<VEC, 4>(p, p.g[1], bid, sa, sb);
-    else wgrad_body<VEC, 4>(p, p.g[0], bid, sa, sb);
+    if (p.ngroups > 1 && bid >= p.g[1].wg_begin) wgrad_body<VEC, 4, TS>(p, p.g[1], bid, sa, sb);
+    else wgrad_body<VEC, 4, TS>(p, p.g[0], bid, sa, sb);
 }
 
 // ----------------------------------------------------------------- DP optimizer

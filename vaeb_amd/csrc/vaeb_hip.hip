@@ -341,17 +341,26 @@ OptArgs make_opt(vaeb_ctx* c, int par, bool update, bool store) {
     return o;
 }
 
+// Weight-gradient tile widths (columns; rows are kWT = 64).  Narrower tiles mean more
+// workgroups, each streaming fewer theta / accumulator / panel bytes through its CU: at
+// MNIST-20, 64 -> 32 wide took the dW2 launch 11.7 -> 9.5 us and the dW3 | dW45 launch
+// 10.9 -> 8.1 us; 16 wide takes the latter to 7.5 us but the dW2 launch (beside 224 dhd
+// tiles) back up to 11.1 us.
+constexpr int kWTJ_P5 = 32;    // dW2 (| dW6), beside the dhd tiles
+constexpr int kWTJ_P67 = 16;   // dW1, beside the dz / dh phase
+constexpr int kWTJ_W = 16;     // standalone launches: dW3 | dW45 (+ ELBO), non-fused dW1
+
 // Weight-gradient arguments over `n` groups whose tiles start at block `base` of the
 // launch (+ the ELBO workgroup when e != nullptr).  *vec: 16-byte panel loads are legal.
 int prep_wgrad(vaeb_ctx* c, const WGroup* groups, int n, const OptArgs& opt, const ElboArgs* e, const StepArgs& a,
-               int base, WGradArgs& w, bool& vec) {
+               int base, WGradArgs& w, bool& vec, int tw) {
     w = WGradArgs{};
     int begin = base;
     if (n < 1 || n > 2) return fail(VAEB_ERR_ARG, "internal: 1 or 2 weight-gradient groups per launch");
     for (int gi = 0; gi < n; ++gi) {
         w.g[gi] = groups[gi];
         WGroup& G = w.g[gi];
-        G.tiles_j = cdiv(G.N0 + G.N1, kWT);
+        G.tiles_j = cdiv(G.N0 + G.N1, tw);
         G.wg_begin = begin;
         G.wg_end = begin + cdiv(G.rowsW + 1, kWT) * G.tiles_j;
         begin = G.wg_end;
@@ -381,9 +390,9 @@ int launch_wgrad(vaeb_ctx* c, hipStream_t s, const WGroup* groups, int n, const 
                  const StepArgs& a) {
     WGradArgs w;
     bool vec;
-    if (int rc = prep_wgrad(c, groups, n, opt, e, a, 0, w, vec)) return rc;
-    if (vec) hipLaunchKernelGGL(wgrad_kernel<true>, dim3(w.total_wgs + (e ? 1 : 0)), dim3(256), 0, s, w);
-    else hipLaunchKernelGGL(wgrad_kernel<false>, dim3(w.total_wgs + (e ? 1 : 0)), dim3(256), 0, s, w);
+    if (int rc = prep_wgrad(c, groups, n, opt, e, a, 0, w, vec, kWTJ_W)) return rc;
+    if (vec) hipLaunchKernelGGL((wgrad_kernel<true, kWTJ_W / 16>), dim3(w.total_wgs + (e ? 1 : 0)), dim3(256), 0, s, w);
+    else hipLaunchKernelGGL((wgrad_kernel<false, kWTJ_W / 16>), dim3(w.total_wgs + (e ? 1 : 0)), dim3(256), 0, s, w);
     CHECK_LAUNCH();
     return 0;
 }
@@ -544,15 +553,15 @@ int enqueue_train_step(vaeb_ctx* c, int par, bool prof, bool fresh = true) {
         const int gx = cdiv(p5.M, 16), ntile = gx * cdiv(p5.N, 16);
         WGradArgs w;
         bool vec;
-        if (int rc = prep_wgrad(c, &g4, 1, opt, nullptr, a, ntile, w, vec)) return rc;
+        if (int rc = prep_wgrad(c, &g4, 1, opt, nullptr, a, ntile, w, vec, kWTJ_P5)) return rc;
         const dim3 grid(w.total_wgs);
         pr.mark(4);
         REP(pr) if (cdiv(cdiv(p5.K, 16), 8) <= 4) {
-            if (vec) hipLaunchKernelGGL((tile_wgrad_kernel<1, 1, 8, 1, 4, PDhd, true>), grid, dim3(512), 0, s, p5, w, ntile, gx);
-            else hipLaunchKernelGGL((tile_wgrad_kernel<1, 1, 8, 1, 4, PDhd, false>), grid, dim3(512), 0, s, p5, w, ntile, gx);
+            if (vec) hipLaunchKernelGGL((tile_wgrad_kernel<1, 1, 8, 1, 4, PDhd, true, kWTJ_P5 / 16>), grid, dim3(512), 0, s, p5, w, ntile, gx);
+            else hipLaunchKernelGGL((tile_wgrad_kernel<1, 1, 8, 1, 4, PDhd, false, kWTJ_P5 / 16>), grid, dim3(512), 0, s, p5, w, ntile, gx);
         } else {
-            if (vec) hipLaunchKernelGGL((tile_wgrad_kernel<1, 1, 8, 1, 8, PDhd, true>), grid, dim3(512), 0, s, p5, w, ntile, gx);
-            else hipLaunchKernelGGL((tile_wgrad_kernel<1, 1, 8, 1, 8, PDhd, false>), grid, dim3(512), 0, s, p5, w, ntile, gx);
+            if (vec) hipLaunchKernelGGL((tile_wgrad_kernel<1, 1, 8, 1, 8, PDhd, true, kWTJ_P5 / 16>), grid, dim3(512), 0, s, p5, w, ntile, gx);
+            else hipLaunchKernelGGL((tile_wgrad_kernel<1, 1, 8, 1, 8, PDhd, false, kWTJ_P5 / 16>), grid, dim3(512), 0, s, p5, w, ntile, gx);
         }
         CHECK_LAUNCH();
     }
@@ -565,15 +574,15 @@ int enqueue_train_step(vaeb_ctx* c, int par, bool prof, bool fresh = true) {
             const int nrow = a.Mbp / 16 * std::max(1, std::min(c->dz_split, cdiv(a.H, 16)));
             WGradArgs w;
             bool vec;
-            if (int rc = prep_wgrad(c, &g3, 1, opt, nullptr, a, nrow, w, vec)) return rc;
+            if (int rc = prep_wgrad(c, &g3, 1, opt, nullptr, a, nrow, w, vec, kWTJ_P67)) return rc;
             const dim3 grid(w.total_wgs);
             pr.mark(13);
             REP(pr) if (a.Z <= 16) {
-                if (vec) hipLaunchKernelGGL((dz_dh_wgrad_kernel<1, true>), grid, dim3(512), 0, s, a, w, nrow);
-                else hipLaunchKernelGGL((dz_dh_wgrad_kernel<1, false>), grid, dim3(512), 0, s, a, w, nrow);
+                if (vec) hipLaunchKernelGGL((dz_dh_wgrad_kernel<1, true, kWTJ_P67 / 16>), grid, dim3(512), 0, s, a, w, nrow);
+                else hipLaunchKernelGGL((dz_dh_wgrad_kernel<1, false, kWTJ_P67 / 16>), grid, dim3(512), 0, s, a, w, nrow);
             } else {
-                if (vec) hipLaunchKernelGGL((dz_dh_wgrad_kernel<2, true>), grid, dim3(512), 0, s, a, w, nrow);
-                else hipLaunchKernelGGL((dz_dh_wgrad_kernel<2, false>), grid, dim3(512), 0, s, a, w, nrow);
+                if (vec) hipLaunchKernelGGL((dz_dh_wgrad_kernel<2, true, kWTJ_P67 / 16>), grid, dim3(512), 0, s, a, w, nrow);
+                else hipLaunchKernelGGL((dz_dh_wgrad_kernel<2, false, kWTJ_P67 / 16>), grid, dim3(512), 0, s, a, w, nrow);
             }
             CHECK_LAUNCH();
         } else {
