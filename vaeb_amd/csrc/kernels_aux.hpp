@@ -76,6 +76,13 @@ DEV double block_sum256w(double v, double* sh) {
 
 // Deterministic (fixed-order) reduction by one 256-thread workgroup: strided per-thread
 // sums, a butterfly within each wave, then the four wave sums in wave order.
+// cursor += 1 and next = order[cursor] (tile_engine.hpp, kCtlNext)
+DEV void advance_cursor(int* cursor) {
+    const int c1 = *cursor + 1;
+    *cursor = c1;
+    cursor[kCtlNext] = cursor[2 + c1];
+}
+
 DEV void elbo_reduce(const ElboArgs& e, double* sh) {
     double v[3] = {strided_sum<16>(e.lp_part, e.n_lp), strided_sum<4>(e.kl_part, e.n_kl),
                    strided_sum<4>(e.fv_part, e.n_fv)};
@@ -108,7 +115,7 @@ DEV void elbo_emit(const ElboArgs& e, double lp, double kl, double fv) {
         e.epoch[0] += v;
         e.epoch[1] += 1.0;
     }
-    if (e.cursor) *e.cursor += 1;
+    if (e.cursor) advance_cursor(e.cursor);
     if (e.step) *e.step += 1;
 }
 
@@ -396,7 +403,7 @@ __global__ __launch_bounds__(256) void adagrad_kernel(OptArgs o, int64_t P, DpRa
         *e.elbo_out = (float)v;
         e.epoch[0] += v;
         e.epoch[1] += 1.0;
-        *e.cursor += 1;
+        advance_cursor(e.cursor);
         *e.step += 1;
     }
 }

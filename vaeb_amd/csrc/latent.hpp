@@ -156,7 +156,7 @@ DEV void enc_latent_body(const StepArgs& a, const FvFold& fvf) {
     if (wave == 0) {
 #pragma unroll
         for (int s = 1; s < 8; ++s) acc[0] += red[s * 64 + lane];
-        if (a.order && bx == 0 && by == 0 && lane == 0) *a.cur_batch = a.order[*a.cursor];
+        if (a.order && bx == 0 && by == 0 && lane == 0) *a.cur_batch = a.cursor[kCtlNext];
         const int n = n0 + li;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
@@ -195,9 +195,9 @@ DEV void enc_latent_body(const StepArgs& a, const FvFold& fvf) {
         for (int l = 0; l < kLP; ++l)
             epre[l] = bld(be, (a.eps_mode == 1 && l < a.L && valid) ? (uint32_t)((l * a.eps_in_ld + m) * Z + n) * 4u : kOOB);
     }
-    // the row base comes from the order itself: cur_batch is written by tile (0,0) of
+    // the row base comes from `next` (kCtlNext): cur_batch is written by tile (0,0) of
     // this same launch, which need not have run yet
-    const int64_t grow0 = (a.order ? (int64_t)a.order[*a.cursor] * a.row_base_mul : 0) + a.row_base_add;
+    const int64_t grow0 = (a.order ? (int64_t)a.cursor[kCtlNext] * a.row_base_mul : 0) + a.row_base_add;
     const int64_t stp = a.step ? *a.step : 0;
     const int NF4 = 8 * Z;                  // float4 per slab (2Z columns x 16 rows)
     const int NP = 512 / NF4;               // slab partitions (threads >= NP * NF4 idle)

@@ -75,7 +75,7 @@ struct FvFold {
 // P1 resolves the minibatch index from the device-side batch order; every later phase
 // of the step reads the resolved copy (the cursor advances inside P8 / the optimizer).
 DEV const float* x_rows_p1(const StepArgs& a) {
-    return a.order ? a.xbase + (int64_t)a.order[*a.cursor] * a.batch_stride : a.xbase;
+    return a.order ? a.xbase + (int64_t)a.cursor[kCtlNext] * a.batch_stride : a.xbase;
 }
 DEV const float* x_rows(const StepArgs& a) {
     return a.order ? a.xbase + (int64_t)(*a.cur_batch) * a.batch_stride : a.xbase;
@@ -109,7 +109,7 @@ struct PEnc {
     template <int NB>
     DEV void epilogue(int m0, int n0, const f32x4 (&acc)[NB], const Pre& pre) const {
         const int lane = threadIdx.x & 63;
-        if (a.order && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) *a.cur_batch = a.order[*a.cursor];
+        if (a.order && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) *a.cur_batch = a.cursor[kCtlNext];
         const int n = n0 + (lane & 15);
         if (n >= a.H) return;
         const float b = pre.b;

@@ -379,7 +379,7 @@ __global__ __launch_bounds__(256) void adagrad_bf16_kernel(Opt o, int64_t P, DpR
         *e.elbo_out = (float)v;
         e.epoch[0] += v;
         e.epoch[1] += 1.0;
-        *e.cursor += 1;
+        advance_cursor(e.cursor);
         *e.step += 1;
     }
 }

@@ -49,6 +49,13 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 namespace vaeb {
 
+// Device control block (vaeb_hip.hip: ictl): [cursor, cur_batch, order[kOrderCap], next].
+// `next` = order[cursor] is kept by whoever advances the cursor (the step's last launch;
+// upload_order for a fresh order), so the next step's encoder resolves its input rows
+// with ONE dependent load instead of the cursor -> order[cursor] chain.
+constexpr int kOrderCap = 1 << 20;
+constexpr int kCtlNext = kOrderCap + 2;   // offset of `next` from the cursor
+
 DEV f32x4 zero4() { f32x4 z = {0.f, 0.f, 0.f, 0.f}; return z; }
 
 // XCD-aware block order (guide T1): the dispatcher deals linear workgroup ids round-robin

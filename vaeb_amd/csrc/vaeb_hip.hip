@@ -68,7 +68,6 @@ int dalloc(T** p, size_t n) {
 }
 
 // Control block layout (ints): [0] cursor, [1] resolved batch, [2..] batch order.
-constexpr int kOrderCap = 1 << 20;
 constexpr int kFvParts = 1024;   // FV stream grid (one thetaPrior partial per block)
 constexpr int kGraphSteps = 32;
 constexpr int kMaxProfKernels = 24;
@@ -104,7 +103,7 @@ struct vaeb_ctx {
     int64_t nrows = 0;
     float* xeval = nullptr;
     // control
-    int* ictl = nullptr;          // cursor, cur_batch, order[kOrderCap]
+    int* ictl = nullptr;          // cursor, cur_batch, order[kOrderCap], next (tile_engine.hpp)
     int64_t* step = nullptr;
     float* elbo_out = nullptr;
     double* epoch = nullptr;      // [2]
@@ -695,7 +694,9 @@ int upload_order(vaeb_ctx* c, const int32_t* idx, int n) {
     c->h_ctl[0] = 0;
     c->h_ctl[1] = 0;
     memcpy(c->h_ctl + 2, idx, sizeof(int) * (size_t)n);
+    c->h_ctl[kCtlNext] = n > 0 ? idx[0] : 0;
     HIP_TRY(hipMemcpyAsync(c->ictl, c->h_ctl, sizeof(int) * (size_t)(n + 2), hipMemcpyHostToDevice, c->s));
+    HIP_TRY(hipMemcpyAsync(c->ictl + kCtlNext, c->h_ctl + kCtlNext, sizeof(int), hipMemcpyHostToDevice, c->s));
     HIP_TRY(hipEventRecord(c->ctl_ev, c->s));
     return 0;
 }
@@ -776,7 +777,7 @@ int vaeb_create(const vaeb_config* cfg, vaeb_ctx** out) {
     }
     rc = rc ? rc : dalloc(&c->fv_part, kFvParts);
     rc = rc ? rc : dalloc(&c->xeval, (size_t)R * D);
-    rc = rc ? rc : dalloc(&c->ictl, kOrderCap + 2);
+    rc = rc ? rc : dalloc(&c->ictl, kCtlNext + 1);
     rc = rc ? rc : dalloc(&c->step, 1);
     rc = rc ? rc : dalloc(&c->elbo_out, 1);
     rc = rc ? rc : dalloc(&c->epoch, 2);
@@ -805,7 +806,7 @@ int vaeb_create(const vaeb_config* cfg, vaeb_ctx** out) {
     }
     if (!rc && is_bf16(c)) rc = bf_alloc(c);
     if (rc) { vaeb_destroy(c); return rc; }
-    if (hipHostMalloc((void**)&c->h_ctl, sizeof(int) * (kOrderCap + 2), 0) != hipSuccess ||
+    if (hipHostMalloc((void**)&c->h_ctl, sizeof(int) * (kCtlNext + 1), 0) != hipSuccess ||
         hipHostMalloc((void**)&c->h_elbo, sizeof(float) * 4, 0) != hipSuccess ||
         hipHostMalloc((void**)&c->h_d2, sizeof(double) * 4, 0) != hipSuccess) {
         vaeb_destroy(c);
