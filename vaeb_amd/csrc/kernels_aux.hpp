@@ -209,7 +209,7 @@ DEV void wgrad_body(const WGradArgs& p, const WGroup& g, int bid, float (*sa)[kW
     constexpr int kWTS = TS, kWTJ = 16 * TS;
     constexpr int NTH = 64 * NWV;
     // resolve the batch pointer first: its load must not queue behind the prefetches below
-    const float* at = g.at_is_x ? p.xbase + (int64_t)__builtin_amdgcn_readfirstlane(*p.cur_batch) * p.batch_stride : g.at;
+    const float* at = g.at_is_x ? p.xbase + (int64_t)ld_launch_const(p.cur_batch) * p.batch_stride : g.at;
     const rsrc_t ba = mkbuf(at, (int64_t)g.klim_at * g.ld_at * 4);
     const int lt = bid - g.wg_begin;
     const int i0 = (lt / g.tiles_j) * kWT, j0 = (lt % g.tiles_j) * kWTJ;

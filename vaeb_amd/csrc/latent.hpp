@@ -197,7 +197,7 @@ DEV void enc_latent_body(const StepArgs& a, const FvFold& fvf) {
     }
     // the row base comes from `next` (kCtlNext): cur_batch is written by tile (0,0) of
     // this same launch, which need not have run yet
-    const int64_t grow0 = (a.order ? (int64_t)a.cursor[kCtlNext] * a.row_base_mul : 0) + a.row_base_add;
+    const int64_t grow0 = (a.order ? (int64_t)ld_launch_const(a.cursor + kCtlNext) * a.row_base_mul : 0) + a.row_base_add;
     const int64_t stp = a.step ? *a.step : 0;
     const int NF4 = 8 * Z;                  // float4 per slab (2Z columns x 16 rows)
     const int NP = 512 / NF4;               // slab partitions (threads >= NP * NF4 idle)
@@ -279,11 +279,16 @@ __global__ __launch_bounds__(512) void enc_latent_fv_kernel(StepArgs a, FvFold f
 // and lane (m, q) ends with hd[m][kb + 16 q + 4 r + u] -- the decoder GEMM's A operand
 // at MFMA step r, matched by W2 row kb + 16 q + 4 r + u on the B side.
 // ZS = ceil(Z / 4): the hd^T product runs ZS MFMA k-steps (latent 4t + q at step t).
-template <int NB, int ZS>
+// V1 (host-chosen: H % 4 == 0, W1 / b1 16-byte aligned) selects the 16-byte W1 / b1
+// loads at compile time: with a runtime choice the loads sat in branches and hipcc drained
+// vmcnt at each, serialising the z, W1 / b1 and W2 round trips.  The x rows for the
+// likelihood are resolved (scalar load of cur_batch) only after wave 0 has issued its
+// first block's operand loads.
+template <int NB, int ZS, bool V1>
 __global__ __launch_bounds__(512, 4) void decout_z_kernel(StepArgs a) {
     VAEB_STAMP(a, 0);
     PDecOut p{a, nullptr, a.Me, a.D, a.H};
-    p.prepare();
+    p.prepare_at(nullptr);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int li = lane & 15, q = lane >> 4;
     const int lin = xcd_remap(blockIdx.x + blockIdx.y * gridDim.x, gridDim.x * gridDim.y);
@@ -294,7 +299,7 @@ __global__ __launch_bounds__(512, 4) void decout_z_kernel(StepArgs a) {
     const bool rowok = ((m0 + li) % a.Mbp) < a.Mb;
     const rsrc_t bw1 = mkbuf(a.W1, (int64_t)Z * H * 4);
     const rsrc_t bb1 = mkbuf(a.b1, (int64_t)H * 4);
-    const bool v1 = (H & 3) == 0 && aligned16(a.W1) && aligned16(a.b1);
+    constexpr bool v1 = V1;
     float zb[ZS];
     {
         const rsrc_t bz = mkbuf(a.z, (int64_t)a.Me * Z * 4);
@@ -302,7 +307,6 @@ __global__ __launch_bounds__(512, 4) void decout_z_kernel(StepArgs a) {
         for (int t = 0; t < ZS; ++t) zb[t] = bld(bz, (4 * t + q < Z) ? (uint32_t)((m0 + li) * Z + 4 * t + q) * 4u : kOOB);
     }
     PDecOut::Pre pre{};
-    if (wave == 0) pre = p.prefetch(m0, n0);
     f32x4 acc[NB];
 #pragma unroll
     for (int w = 0; w < NB; ++w) acc[w] = zero4();
@@ -326,6 +330,10 @@ __global__ __launch_bounds__(512, 4) void decout_z_kernel(StepArgs a) {
                     const int k = kb + 16 * q + 4 * r + u;
                     w2b[u][r][w] = p.b1(n0 + li, k, w);
                 }
+        if (kb == 0) {   // wave 0, first block: its loads are in flight
+            p.x = x_rows(a);
+            pre = p.prefetch(m0, n0);
+        }
         f32x4 hv[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u) {

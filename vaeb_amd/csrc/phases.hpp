@@ -75,13 +75,13 @@ struct FvFold {
 // P1 resolves the minibatch index from the device-side batch order; every later phase
 // of the step reads the resolved copy (the cursor advances inside P8 / the optimizer).
 DEV const float* x_rows_p1(const StepArgs& a) {
-    return a.order ? a.xbase + (int64_t)a.cursor[kCtlNext] * a.batch_stride : a.xbase;
+    return a.order ? a.xbase + (int64_t)ld_launch_const(a.cursor + kCtlNext) * a.batch_stride : a.xbase;
 }
 DEV const float* x_rows(const StepArgs& a) {
-    return a.order ? a.xbase + (int64_t)(*a.cur_batch) * a.batch_stride : a.xbase;
+    return a.order ? a.xbase + (int64_t)ld_launch_const(a.cur_batch) * a.batch_stride : a.xbase;
 }
 DEV int64_t global_row0(const StepArgs& a) {
-    return (a.order ? (int64_t)(*a.cur_batch) * a.row_base_mul : 0) + a.row_base_add;
+    return (a.order ? (int64_t)ld_launch_const(a.cur_batch) * a.row_base_mul : 0) + a.row_base_add;
 }
 
 struct NoPre {};

@@ -56,6 +56,16 @@ namespace vaeb {
 constexpr int kOrderCap = 1 << 20;
 constexpr int kCtlNext = kOrderCap + 2;   // offset of `next` from the cursor
 
+// A control word that no workgroup of this launch writes (cursor / next / cur_batch, all
+// written by earlier launches): read through the constant address space, i.e. a scalar
+// load counted by lgkmcnt, so the wait for it does not drain the vector loads issued
+// around it (a vector load + readfirstlane made hipcc wait vmcnt(0) before the first
+// operand load of the launch could even be issued).
+DEV int ld_launch_const(const int* p) {
+    typedef const __attribute__((address_space(4))) int cint;
+    return *(cint*)(uintptr_t)p;
+}
+
 DEV f32x4 zero4() { f32x4 z = {0.f, 0.f, 0.f, 0.f}; return z; }
 
 // XCD-aware block order (guide T1): the dispatcher deals linear workgroup ids round-robin

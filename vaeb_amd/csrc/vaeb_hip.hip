@@ -243,15 +243,21 @@ ElboArgs base_elbo(vaeb_ctx* c, const StepArgs& a) {
     return e;
 }
 
+template <int NB, bool V1>
+void launch_decout_zv(hipStream_t s, dim3 grid, const StepArgs& a) {
+    switch ((a.Z + 3) / 4) {
+        case 1: hipLaunchKernelGGL((decout_z_kernel<NB, 1, V1>), grid, dim3(512), 0, s, a); break;
+        case 2: hipLaunchKernelGGL((decout_z_kernel<NB, 2, V1>), grid, dim3(512), 0, s, a); break;
+        case 3: case 4: hipLaunchKernelGGL((decout_z_kernel<NB, 4, V1>), grid, dim3(512), 0, s, a); break;
+        case 5: hipLaunchKernelGGL((decout_z_kernel<NB, 5, V1>), grid, dim3(512), 0, s, a); break;
+        default: hipLaunchKernelGGL((decout_z_kernel<NB, 8, V1>), grid, dim3(512), 0, s, a); break;
+    }
+}
 template <int NB>
 void launch_decout_z(hipStream_t s, dim3 grid, const StepArgs& a) {
-    switch ((a.Z + 3) / 4) {
-        case 1: hipLaunchKernelGGL((decout_z_kernel<NB, 1>), grid, dim3(512), 0, s, a); break;
-        case 2: hipLaunchKernelGGL((decout_z_kernel<NB, 2>), grid, dim3(512), 0, s, a); break;
-        case 3: case 4: hipLaunchKernelGGL((decout_z_kernel<NB, 4>), grid, dim3(512), 0, s, a); break;
-        case 5: hipLaunchKernelGGL((decout_z_kernel<NB, 5>), grid, dim3(512), 0, s, a); break;
-        default: hipLaunchKernelGGL((decout_z_kernel<NB, 8>), grid, dim3(512), 0, s, a); break;
-    }
+    auto al = [](const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
+    if ((a.H & 3) == 0 && al(a.W1) && al(a.b1)) launch_decout_zv<NB, true>(s, grid, a);
+    else launch_decout_zv<NB, false>(s, grid, a);
 }
 
 // Training minibatches with Z <= 32 fold the latent block into the wide phases
