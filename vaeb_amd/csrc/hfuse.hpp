@@ -4,7 +4,7 @@
 // side stream inside a hipGraph measured ~12 us/step slower than one stream).
 //
 //   P5  (dhd, 224 tiles at MNIST-20) + dW2|dW6 (104 tiles)   -- both need only P4's output
-//   P67 (dz/dh, 7 row blocks x 4 column splits) + dW1 (8 tiles) -- both need only P5's output
+//   P67 (dz/dh, 7 row blocks x 8 column splits) + dW1 (8 tiles) -- both need only P5's output
 //
 // Phase blocks come first in the grid (they gate the next launch); all blocks are 512
 // threads, so the weight-gradient tiles use the 8-wave K-split form.

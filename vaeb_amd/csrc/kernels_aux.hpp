@@ -350,7 +350,16 @@ template <bool VEC, int TS>
 __global__ __launch_bounds__(256) void wgrad_kernel(WGradArgs p) {
     __shared__ float sa[kWKB][kWP];
     __shared__ float sb[kWKB][kWP];
-    const int bid = (int)blockIdx.x < p.total_wgs ? xcd_remap(blockIdx.x, p.total_wgs) : (int)blockIdx.x;
+#ifndef VAEB_ELBO_FIRST
+#define VAEB_ELBO_FIRST 1
+#endif
+    // the ELBO workgroup (with_elbo) is block 0, dispatched first, so its reduction runs
+    // beside the weight-gradient tiles instead of after the last of them was placed
+    int bid;
+    if (VAEB_ELBO_FIRST && p.with_elbo)
+        bid = blockIdx.x == 0 ? p.total_wgs : xcd_remap((int)blockIdx.x - 1, p.total_wgs);
+    else
+        bid = (int)blockIdx.x < p.total_wgs ? xcd_remap(blockIdx.x, p.total_wgs) : (int)blockIdx.x;
     if (p.dbg && threadIdx.x == 0) p.dbg[bid * 8 + 0] = __builtin_amdgcn_s_memrealtime();
     if (bid >= p.total_wgs) {  // the extra workgroup: ELBO of this step
         elbo_reduce(p.elbo, reinterpret_cast<double*>(&sa[0][0]));

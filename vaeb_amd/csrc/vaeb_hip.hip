@@ -135,7 +135,7 @@ struct vaeb_ctx {
     hipStream_t s2 = nullptr;     // DP: the gradient buckets' all-reduces and their Adagrad
     hipEvent_t dp_ev[3] = {};     // fork after dW2, bucket A reduced, bucket A updated
     bool dp_overlap = false;      // bucket A on s2 (bf16 engine; VAEB_DP_OVERLAP=0/1 overrides)
-    int dz_split = 4;             // P67 column splits per row block (fused.hpp dz_dh_body; VAEB_DZ_SPLIT)
+    int dz_split = 8;             // P67 column splits per row block (fused.hpp dz_dh_body; VAEB_DZ_SPLIT)
     // profiling
     hipEvent_t pev[kMaxProfKernels + 1] = {};
     int prof_n = 0, prof_reps = 1;
