@@ -118,50 +118,96 @@ def committed_traffic(kernel, path=PMC_FILES["mnist"], symbols=KERNEL_SYMBOLS):
     return None
 
 
-def cpu_baseline(D, H, Z, B, x, budget_s=10.0, max_steps=20000, continuous=False):
-    """The oracle's float32 NumPy restatement of the same step, on the host cores."""
-    from oracle import vaeb_oracle as O
+def host_cpu_info():
+    """(threads to use, nproc, CPU model).  The GPU box shares its host among the GPUs and
+    pins OMP_NUM_THREADS to this job's share (16 per GPU): os.cpu_count() reports the
+    whole machine, so the baseline uses the share (OMP_NUM_THREADS, else the affinity
+    mask) and records nproc beside it."""
+    nproc = os.cpu_count() or 1
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except Exception:  # pragma: no cover
+        aff = nproc
+    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    threads = max(1, min(aff, share) if share > 0 else aff)
+    model = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:  # pragma: no cover
+        pass
+    return threads, nproc, model
+
+
+def _threads_ctx(n):
     try:
         from threadpoolctl import threadpool_limits
+        return threadpool_limits(limits=n)
     except Exception:  # pragma: no cover
-        threadpool_limits = None
-    threads = min(16, os.cpu_count() or 1)
+        return None
+
+
+def cpu_baseline_pair(fn, budget_s, single_kw=None, **kw):
+    """Time `fn` (a bounded oracle run returning (steps, seconds, images)) on the job's host
+    thread share, then single-threaded on a shorter budget; one cpu_baseline object."""
+    threads, nproc, model = host_cpu_info()
+    ctx = _threads_ctx(threads)
+    try:
+        n, dt, imgs, what = fn(budget_s, **kw)
+    finally:
+        if ctx is not None and hasattr(ctx, "unregister"):
+            ctx.unregister()
+    ctx1 = _threads_ctx(1)
+    try:
+        n1, dt1, imgs1, _ = fn(max(2.0, budget_s / 2), **{**kw, **(single_kw or {})})
+    finally:
+        if ctx1 is not None and hasattr(ctx1, "unregister"):
+            ctx1.unregister()
+    return {"value": imgs / dt, "unit": "images/s", "cores": threads, "kind": "port",
+            "single_thread_value": imgs1 / dt1, "nproc": nproc, "cpu_model": model,
+            "sample": f"{n} {what} in {dt:.1f} s on {threads} OpenBLAS threads (job share of {nproc} CPUs, {model}); "
+                      f"1 thread: {n1} steps in {dt1:.1f} s"}
+
+
+def cpu_baseline(D, H, Z, B, x, budget_s=10.0, max_steps=20000, continuous=False, warm=3, single_kw=None):
+    """The oracle's float32 NumPy restatement of the same step, on the host cores."""
+    return cpu_baseline_pair(_cpu_run_lb, budget_s, single_kw=single_kw, D=D, H=H, Z=Z, B=B, x=x,
+                             max_steps=max_steps, continuous=continuous, warm=warm)
+
+
+def _cpu_run_lb(budget_s, D, H, Z, B, x, max_steps=20000, continuous=False, warm=3):
+    from oracle import vaeb_oracle as O
     cfg = O.Config(D=D, H=H, Z=Z, continuous=continuous)
     params = O.init_params(cfg)
     acc = [np.zeros_like(p) for p in params]
     rng = np.random.default_rng(0)
     nb = x.shape[0] // B
-    ctx = threadpool_limits(limits=threads) if threadpool_limits else None
-    try:
-        for i in range(min(3, max_steps)):  # warm-up
-            eps = rng.standard_normal((1, B, Z)).astype(np.float32)
-            _, params, acc, _ = O.step(params, acc, x[i * B:(i + 1) * B], eps, cfg)
-        n = 0
-        t0 = time.perf_counter()
-        while True:
-            b = n % nb
-            eps = rng.standard_normal((1, B, Z)).astype(np.float32)
-            _, params, acc, _ = O.step(params, acc, x[b * B:(b + 1) * B], eps, cfg)
-            n += 1
-            dt = time.perf_counter() - t0
-            if dt >= budget_s or n >= max_steps:
-                break
-    finally:
-        if ctx is not None:
-            ctx.unregister() if hasattr(ctx, "unregister") else None
-    return {"value": n * B / dt, "unit": "images/s", "cores": threads, "kind": "port",
-            "sample": f"{n} float32 NumPy oracle steps ({D}-{H}-{Z}, B={B}) in {dt:.1f} s, OpenBLAS {threads} threads"}
+    for i in range(min(warm, max_steps, nb)):  # warm-up
+        eps = rng.standard_normal((1, B, Z)).astype(np.float32)
+        _, params, acc, _ = O.step(params, acc, x[i * B:(i + 1) * B], eps, cfg)
+    n = 0
+    t0 = time.perf_counter()
+    while True:
+        b = n % nb
+        eps = rng.standard_normal((1, B, Z)).astype(np.float32)
+        _, params, acc, _ = O.step(params, acc, x[b * B:(b + 1) * B], eps, cfg)
+        n += 1
+        dt = time.perf_counter() - t0
+        if dt >= budget_s or n >= max_steps:
+            break
+    return n, dt, n * B, f"float32 NumPy oracle steps ({D}-{H}-{Z}, B={B})"
 
 
 def cpu_baseline_fv(D, H, Z, B, x, budget_s=10.0, max_steps=20000, sample=False):
     """The oracle's full-variational step (literal, or with the weight sample: FVS) in
     float32 NumPy on the host cores."""
+    return cpu_baseline_pair(_cpu_run_fv, budget_s, D=D, H=H, Z=Z, B=B, x=x, max_steps=max_steps, sample=sample)
+
+
+def _cpu_run_fv(budget_s, D, H, Z, B, x, max_steps=20000, sample=False):
     from oracle import vaeb_oracle as O
-    try:
-        from threadpoolctl import threadpool_limits
-    except Exception:  # pragma: no cover
-        threadpool_limits = None
-    threads = min(16, os.cpu_count() or 1)
     cfg = O.Config(D=D, H=H, Z=Z, estimator="FV")
     theta = O.init_params(cfg)
     mu = [t.copy() for t in theta]
@@ -170,7 +216,6 @@ def cpu_baseline_fv(D, H, Z, B, x, budget_s=10.0, max_steps=20000, sample=False)
     as_ = [np.zeros_like(t) for t in theta]
     rng = np.random.default_rng(0)
     nb = x.shape[0] // B
-    ctx = threadpool_limits(limits=threads) if threadpool_limits else None
     n, t0 = 0, time.perf_counter()
     while True:
         b = n % nb
@@ -184,11 +229,7 @@ def cpu_baseline_fv(D, H, Z, B, x, budget_s=10.0, max_steps=20000, sample=False)
         dt = time.perf_counter() - t0
         if dt >= budget_s or n >= max_steps:
             break
-    if ctx is not None and hasattr(ctx, "unregister"):
-        ctx.unregister()
-    return {"value": n * B / dt, "unit": "images/s", "cores": threads, "kind": "port",
-            "sample": f"{n} float32 NumPy oracle {'FVS' if sample else 'FV'} steps ({D}-{H}-{Z}, B={B}) in {dt:.1f} s, "
-                      f"OpenBLAS {threads} threads"}
+    return n, dt, n * B, f"float32 NumPy oracle {'FVS' if sample else 'FV'} steps ({D}-{H}-{Z}, B={B})"
 
 
 CONFIGS = {
@@ -216,55 +257,47 @@ CONFIGS = {
 }
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--config", choices=sorted(CONFIGS), default="mnist")
-    ap.add_argument("--steps", type=int, default=None)
-    ap.add_argument("--warmup", type=int, default=None)
-    ap.add_argument("--batch", type=int, default=None)
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-graph", action="store_true")
-    ap.add_argument("--cpu-budget", type=float, default=10.0)
-    ap.add_argument("--scaling", choices=["weak", "strong"], default="weak",
-                    help="weak: B rows per GPU (default); strong: one B-row global minibatch split "
-                         "contiguously over the ranks (100 over 8 = 13,13,13,13,12,12,12,12; SURVEY 8(e))")
-    args = ap.parse_args()
-    C = CONFIGS[args.config]
-    steps = args.steps if args.steps is not None else C["steps"]
-    warmup = args.warmup if args.warmup is not None else C["warmup"]
+def free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus and world > 1:
-        print(f"warning: WORLD_SIZE={world} != --gpus {args.gpus}", file=sys.stderr)
-    dist = None
-    if world > 1:
-        import torch.distributed as dist  # host-side coordination only (gloo)
-        dist.init_process_group("gloo")
 
-    from oracle import vaeb_oracle as O  # synthetic data generator + initial theta (not the compute path)
+def spawn_ranks(n, argv, poll_s=0.2, script=None):
+    """`bench.py --gpus N` without a launcher: start N rank processes of this script (one
+    per GPU, RANK = LOCAL_RANK = r, WORLD_SIZE = N, rendezvous on 127.0.0.1) and wait.
+    The parent makes no GPU call.  If one rank fails the others are stopped (they would
+    wait in a collective forever); returns the first non-zero exit code, else 0."""
+    import subprocess
+    port = free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        procs.append(subprocess.Popen([sys.executable, script or os.path.abspath(__file__)] + list(argv), env=env))
+    rc = 0
+    while True:
+        codes = [p.poll() for p in procs]
+        bad = [c for c in codes if c not in (None, 0)]
+        if bad:
+            rc = bad[0]
+            for p in procs:
+                if p.poll() is None:
+                    p.kill()
+            for p in procs:
+                p.wait()
+            return rc
+        if all(c == 0 for c in codes):
+            return 0
+        time.sleep(poll_s)
+
+
+def make_context(C, D, H, Z, B, Bg, row_off, local, args, gauss, bf16, dist, rank, world):
+    """One library context (and, with world > 1, its RCCL communicator; the 128-byte id
+    travels over the gloo group)."""
     from vaeb_amd import _lib
-    from vaeb_amd.dp import row_split
-
-    D, H, Z = C["D"], C["H"], C["Z"]
-    B = args.batch if args.batch is not None else C["B"]
-    B, row_off, Bg = row_split(B, world, rank, args.scaling)
-    N = max(C["N"], 4 * Bg)
-    bf16 = C["dtype"] == "bf16"
-    gauss = C.get("continuous", False)
-    if bf16:
-        rng = np.random.default_rng(3)   # synth x ~ Bernoulli(0.5)
-        x = (rng.random((N, D), dtype=np.float32) < 0.5).astype(np.float32)
-    elif gauss:
-        x = O.synthetic_frey(n=N, D=D)   # Frey-shaped x ~ Beta(2, 2)
-    else:
-        x = O.synthetic_mnist(n=N, D=D)
-    cfg = O.Config(D=D, H=H, Z=Z, continuous=gauss)
-    fv = C.get("estimator") in ("FV", "FVS")
-    if fv and world > 1:
-        raise SystemExit("the full-variational paths are single-rank (vaeb_comm_init rejects them)")
     ctx = _lib.Context(D, H, Z, B, B_global=Bg, row_offset=row_off, device=local,
                        decoder=_lib.DEC_GAUSSIAN if gauss else _lib.DEC_BERNOULLI,
                        estimator={"FV": _lib.EST_FV, "FVS": _lib.EST_FVS}.get(C.get("estimator"), _lib.EST_LB),
@@ -274,23 +307,14 @@ def main():
         uid = [_lib.Context.comm_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
         ctx.comm_init(uid[0], rank, world)
-    ctx.set_data(x)
-    theta0 = O.flatten(O.init_params(cfg))
-    ctx.set_params(theta0)
-    if fv:   # VAEB.py:120-125: mu_theta = theta, sigma_theta = 1e-3, Adagrad state 0
-        ctx.set_fv_state(theta0, np.full_like(theta0, 1e-3), np.zeros_like(theta0), np.zeros_like(theta0))
-    ctx.set_eps_mode(_lib.EPS_PHILOX, seed=10)
-    nb = N // Bg
-    rs = np.random.RandomState(15485863)  # VAEB.py:526 --seed default
+        n = ctx.comm_count()
+        if n != world or n != args.gpus:
+            raise SystemExit(f"rank {rank}: the RCCL communicator holds {n} ranks, expected {args.gpus}")
+    return ctx
 
-    def order(n):
-        out = []
-        while len(out) < n:
-            o = np.arange(nb)
-            rs.shuffle(o)
-            out.extend(o.tolist())
-        return np.array(out[:n], np.int32)
 
+def timed_run(ctx, order, warmup, steps, dist):
+    """W untimed steps, then exactly K steps between barrier + stream sync; max over ranks."""
     ctx.update_many(order(warmup))
     ctx.synchronize()
     ctx.epoch_elbo()
@@ -310,6 +334,83 @@ def main():
         t = torch.tensor([el], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
+    return el
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--config", choices=sorted(CONFIGS), default="mnist")
+    ap.add_argument("--steps", type=int, default=None)
+    ap.add_argument("--warmup", type=int, default=None)
+    ap.add_argument("--batch", type=int, default=None)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--no-strong", action="store_true", help="N > 1, weak scaling: skip the strong-scaling leg")
+    ap.add_argument("--cpu-budget", type=float, default=10.0)
+    ap.add_argument("--scaling", choices=["weak", "strong"], default="weak",
+                    help="weak: B rows per GPU (default); strong: one B-row global minibatch split "
+                         "contiguously over the ranks (100 over 8 = 13,13,13,13,12,12,12,12; SURVEY 8(e))")
+    argv = sys.argv[1:] if argv is None else list(argv)
+    args = ap.parse_args(argv)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # no launcher: one process per GPU, started here before any GPU call
+        sys.exit(spawn_ranks(args.gpus, argv))
+    C = CONFIGS[args.config]
+    steps = args.steps if args.steps is not None else C["steps"]
+    warmup = args.warmup if args.warmup is not None else C["warmup"]
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"WORLD_SIZE={world} but --gpus {args.gpus}")
+    dist = None
+    if world > 1:
+        import torch.distributed as dist  # host-side coordination only (gloo); the data path is RCCL
+        dist.init_process_group("gloo")
+
+    from vaeb_amd.dp import row_split
+    from vaeb_amd.model import initial_params
+    from vaeb_amd.synthetic import frey_like, mnist_like, synth_like
+
+    D, H, Z = C["D"], C["H"], C["Z"]
+    Bn = args.batch if args.batch is not None else C["B"]
+    B, row_off, Bg = row_split(Bn, world, rank, args.scaling)
+    N = max(C["N"], 4 * Bg)
+    bf16 = C["dtype"] == "bf16"
+    gauss = C.get("continuous", False)
+    if bf16:
+        x = synth_like(N, D=D)             # synth x ~ Bernoulli(0.5)
+    elif gauss:
+        x = frey_like(n=N, D=D)            # Frey-shaped x ~ Beta(2, 2)
+    else:
+        x = mnist_like(n=N, D=D)
+    fv = C.get("estimator") in ("FV", "FVS")
+    if fv and world > 1:
+        raise SystemExit("the full-variational paths are single-rank (vaeb_comm_init rejects them)")
+    ctx = make_context(C, D, H, Z, B, Bg, row_off, local, args, gauss, bf16, dist, rank, world)
+    n_gpus = ctx.comm_count()
+    ctx.set_data(x)
+    theta0 = np.concatenate([a.ravel() for a in initial_params(D, H, Z, gauss)])
+    ctx.set_params(theta0)
+    if fv:   # VAEB.py:120-125: mu_theta = theta, sigma_theta = 1e-3, Adagrad state 0
+        ctx.set_fv_state(theta0, np.full_like(theta0, 1e-3), np.zeros_like(theta0), np.zeros_like(theta0))
+    ctx.set_eps_mode(0, seed=10)   # device Philox
+
+    def orders(nb):
+        rs = np.random.RandomState(15485863)  # VAEB.py:526 --seed default
+
+        def order(n):
+            out = []
+            while len(out) < n:
+                o = np.arange(nb)
+                rs.shuffle(o)
+                out.extend(o.tolist())
+            return np.array(out[:n], np.int32)
+        return order
+
+    el = timed_run(ctx, orders(N // Bg), warmup, steps, dist)
     elbo_sum, nsteps = ctx.epoch_elbo()
 
     # per-kernel device time (HIP events on the context's stream), after the timed region
@@ -334,7 +435,7 @@ def main():
         "metric": C["metric"],
         "value": Bg * steps / el,
         "unit": "images/s",
-        "n_gpus": world,
+        "n_gpus": n_gpus,
         "steps": steps,
         "warmup": warmup,
         "ms_per_step": el / steps * 1e3,
@@ -355,9 +456,22 @@ def main():
                      ("bytes_per_launch" if bound == "hbm" else "flops_per_launch"): fl[dom[0]],
                      "avg_launch_ms": dom[1]},
     }
+    ctx.close()
+    if world > 1 and args.scaling == "weak" and not args.no_strong:
+        # the same run with one Bn-row global minibatch split over the ranks
+        Bs, off_s, Bgs = row_split(Bn, world, rank, "strong")
+        ctx2 = make_context(C, D, H, Z, Bs, Bgs, off_s, local, args, gauss, bf16, dist, rank, world)
+        ctx2.set_data(x)
+        ctx2.set_params(theta0)
+        ctx2.set_eps_mode(0, seed=10)
+        el2 = timed_run(ctx2, orders(N // Bgs), warmup, steps, dist)
+        ctx2.close()
+        res["strong"] = {"value": Bgs * steps / el2, "ms_per_step": el2 / steps * 1e3, "global_batch": Bgs,
+                         "rows_per_gpu": [row_split(Bn, world, r, "strong")[0] for r in range(world)]}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         if bf16:
-            res["cpu_baseline"] = cpu_baseline(D, H, Z, B, x[:4 * B], budget_s=args.cpu_budget * 2, max_steps=8)
+            res["cpu_baseline"] = cpu_baseline(D, H, Z, B, x[:4 * B], budget_s=args.cpu_budget * 2, max_steps=8,
+                                               single_kw={"max_steps": 1, "warm": 0})
         elif fv:
             res["cpu_baseline"] = cpu_baseline_fv(D, H, Z, B, x, budget_s=args.cpu_budget,
                                                   sample=C.get("estimator") == "FVS")
@@ -365,7 +479,6 @@ def main():
             res["cpu_baseline"] = cpu_baseline(D, H, Z, B, x, budget_s=args.cpu_budget, continuous=gauss)
     if rank == 0:
         print(json.dumps(res), flush=True)
-    ctx.close()
     if dist:
         dist.destroy_process_group()
 

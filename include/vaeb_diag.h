@@ -1,0 +1,44 @@
+/*
+ * vaeb_diag.h -- diagnostics and measurement hooks of libvaeb_hip.so.
+ *
+ * NOT part of the drop-in boundary (include/vaeb_hip.h): these entry points have no
+ * counterpart in the reference (/root/reference/VAEB.py).  bench.py uses
+ * vaeb_profile_steps / vaeb_kernel_name for the per-kernel times it reports; the rest
+ * serves the kernel tests and the A/B scripts under scripts/.
+ */
+#ifndef VAEB_DIAG_H
+#define VAEB_DIAG_H
+
+#include "vaeb_hip.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Measurement: runs n_steps eager steps with HIP events around every launch on the
+ * context's stream; writes the average device time (ms) and the kernel id of each
+ * launch slot of one step.  vaeb_kernel_name maps a kernel id to its name. */
+int vaeb_profile_steps(vaeb_ctx* ctx, int32_t n_steps, float* out_ms_per_kernel,
+                       int32_t* out_kernel_ids, int32_t max_kernels, int32_t* out_n_kernels);
+int vaeb_kernel_name(int32_t kernel_id, char* out, int32_t cap);
+/* Diagnostics: one eager step with a 100 MHz s_memrealtime stamp per workgroup at the
+ * stage boundaries of every launch; out = [launch][1024 workgroups][8 slots]. */
+int vaeb_debug_timeline(vaeb_ctx* ctx, int32_t batch_index, uint64_t* out, int64_t cap,
+                        int32_t* out_launches);
+
+/* Test hook for the bf16 GEMM engine: C[M x N] = sum_k A(m, k) B(k, n) with the operands
+ * rounded to bf16 on device.  a_kouter = 0: A is stored [M x K], 1: [K x M]; b_kouter = 0:
+ * B is stored [N x K], 1: [K x N].  ksplit K slices are summed in fixed order.  Uses the
+ * context's device and stream. */
+int vaeb_test_gemm_bf16(vaeb_ctx* ctx, int32_t a_kouter, int32_t b_kouter, int32_t M, int32_t N, int32_t K,
+                        const float* A, const float* B, float* C, int32_t ksplit);
+/* Diagnostics: mean time (ms) of `reps` back-to-back launches of the bf16 GEMM on
+ * device-generated uniform [-1, 1) operands of the given layouts, bias + bf16-store
+ * epilogue; tile width 128 / 256 (0: the engine's choice). */
+int vaeb_bench_gemm_bf16(vaeb_ctx* ctx, int32_t a_kouter, int32_t b_kouter, int32_t M, int32_t N, int32_t K,
+                         int32_t tile_n, int32_t reps, float* out_ms);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* VAEB_DIAG_H */

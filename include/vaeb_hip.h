@@ -124,22 +124,33 @@ int vaeb_reconstruct_sampled(vaeb_ctx* ctx, const float* x, int64_t n, int32_t n
  * unique id is produced on rank 0 and broadcast by the host (e.g. torch.distributed). */
 int vaeb_comm_unique_id(uint8_t out_id[128]);
 int vaeb_comm_init(vaeb_ctx* ctx, const uint8_t id[128], int32_t rank, int32_t world);
+/* Ranks in the context's communicator (ncclCommCount); 1 without a communicator. */
+int vaeb_comm_count(vaeb_ctx* ctx, int32_t* out_world);
+
+/* Device-resident validation set (VAEB.validate(x_valid) once per epoch, VAEB.py:582):
+ * uploaded once; vaeb_validate_resident then evaluates this rank's contiguous share of
+ * the rows (all rows without a communicator) with no host round trip between device
+ * chunks and, with a communicator, all-reduces the SGVB sum over the ranks.  Noise rows
+ * are keyed by the GLOBAL row (Philox), or read from the pushed eps (host mode: eps for
+ * all n rows, global row order), so the result does not depend on the world size. */
+int vaeb_set_valid_data(vaeb_ctx* ctx, const float* x, int64_t n_rows);
+int vaeb_validate_resident(vaeb_ctx* ctx, double* out_sum);
+
+/* Philox step counter (the number of noise draws so far), for checkpoints. */
+int vaeb_get_step(vaeb_ctx* ctx, int64_t* step);
+
+/* Native checkpoint (SURVEY 5 "checkpoint / resume"; the reference's VAEB.save keeps theta
+ * only, VAEB.py:189-203, so a resumed run restarts Adagrad): one file holding the model
+ * shape, theta, the Adagrad accumulators, the Philox seed / step and (FV / FVS) the
+ * variational state.  A context loaded from it continues bit-identically to the run that
+ * wrote it.  Loading checks that the file's D, H, Z, L, decoder and estimator match. */
+int vaeb_checkpoint_save(vaeb_ctx* ctx, const char* path);
+int vaeb_checkpoint_load(vaeb_ctx* ctx, const char* path);
 
 /* Introspection for parity tests: last step's data gradients (reference order, before
  * the prior) and named device activations ("h","mu","lv","z","hd","dA2","dA3",...). */
 int vaeb_get_grads(vaeb_ctx* ctx, float* flat, int64_t n);
 int vaeb_get_activation(vaeb_ctx* ctx, const char* name, float* out, int64_t n);
-
-/* Measurement: runs n_steps eager steps with HIP events around every launch on the
- * context's stream; writes the average device time (ms) and the kernel id of each
- * launch slot of one step.  vaeb_kernel_name maps a kernel id to its name. */
-int vaeb_profile_steps(vaeb_ctx* ctx, int32_t n_steps, float* out_ms_per_kernel,
-                       int32_t* out_kernel_ids, int32_t max_kernels, int32_t* out_n_kernels);
-int vaeb_kernel_name(int32_t kernel_id, char* out, int32_t cap);
-/* Diagnostics: one eager step with a 100 MHz s_memrealtime stamp per workgroup at the
- * stage boundaries of every launch; out = [launch][1024 workgroups][8 slots]. */
-int vaeb_debug_timeline(vaeb_ctx* ctx, int32_t batch_index, uint64_t* out, int64_t cap,
-                        int32_t* out_launches);
 
 /* ------------------------------------------------------------------------------------------
  * degenerate-vae deterministic autoencoder (/root/reference/degenerate-vae/ae.py:41-117):
@@ -187,18 +198,6 @@ int vaeb_ae_train_many(vaeb_ae* ae, const int32_t* idx, int32_t n, int32_t batch
 int vaeb_ae_reconstruct(vaeb_ae* ae, const float* x, int64_t n, float* out);   /* ae.py:92-98  */
 int vaeb_ae_encode(vaeb_ae* ae, const float* x, int64_t n, float* z_out);      /* ae.py:101-107 */
 int vaeb_ae_decode(vaeb_ae* ae, const float* z, int64_t n, float* out);        /* ae.py:110-116 */
-
-/* Test hook for the bf16 GEMM engine: C[M x N] = sum_k A(m, k) B(k, n) with the operands
- * rounded to bf16 on device.  a_kouter = 0: A is stored [M x K], 1: [K x M]; b_kouter = 0:
- * B is stored [N x K], 1: [K x N].  ksplit K slices are summed in fixed order.  Uses the
- * context's device and stream. */
-int vaeb_test_gemm_bf16(vaeb_ctx* ctx, int32_t a_kouter, int32_t b_kouter, int32_t M, int32_t N, int32_t K,
-                        const float* A, const float* B, float* C, int32_t ksplit);
-/* Diagnostics: mean time (ms) of `reps` back-to-back launches of the bf16 GEMM on
- * device-generated uniform [-1, 1) operands of the given layouts, bias + bf16-store
- * epilogue; tile width 128 / 256 (0: the engine's choice). */
-int vaeb_bench_gemm_bf16(vaeb_ctx* ctx, int32_t a_kouter, int32_t b_kouter, int32_t M, int32_t N, int32_t K,
-                         int32_t tile_n, int32_t reps, float* out_ms);
 
 #ifdef __cplusplus
 }

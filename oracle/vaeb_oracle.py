@@ -84,6 +84,23 @@ def init_params(cfg: Config, dtype=np.float32):
     return [W[n].astype(dtype) for n in cfg.names]
 
 
+def init_params_fullbayes(cfg: Config, dtype=np.float32):
+    """VAEBfullbayes.VAE.__init__ (VAEBfullbayes.py:23-73): its own RandomState(10)
+    (:23), std 0.01 (:24), and each weight drawn ONCE in the order W3, W4, W5, W1, W2,
+    (W6) (:34-67) -- unlike VAEB.initialize_params' duplicated W3/W4 draws; zero biases
+    (:29); parameter list in the same reference order (:69-73)."""
+    prng = np.random.RandomState(10)
+    D, H, Z = cfg.D, cfg.H, cfg.Z
+    draw = lambda a, b: prng.normal(0, 0.01, (a, b)).astype(np.float32)
+    W = {"W3": draw(D, H), "W4": draw(H, Z), "W5": draw(H, Z), "W1": draw(Z, H), "W2": draw(H, D)}
+    if cfg.continuous:
+        W["W6"] = draw(H, D)
+    for n, s in param_shapes(cfg):
+        if n.startswith("b"):
+            W[n] = np.zeros(s, np.float32)
+    return [W[n].astype(dtype) for n in cfg.names]
+
+
 def flatten(params):
     return np.concatenate([np.asarray(p).ravel() for p in params])
 

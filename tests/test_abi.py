@@ -9,13 +9,18 @@ import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HEADER = os.path.join(ROOT, "include", "vaeb_hip.h")
+DIAG_HEADER = os.path.join(ROOT, "include", "vaeb_diag.h")
 LIB = os.path.join(ROOT, "vaeb_amd", "libvaeb_hip.so")
 
 
-def header_functions():
-    src = open(HEADER).read()
+def header_functions(path=HEADER):
+    src = open(path).read()
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
     return sorted(set(re.findall(r"\b(vaeb_[a-z0-9_]+)\s*\(", src)))
+
+
+def all_functions():
+    return sorted(set(header_functions()) | set(header_functions(DIAG_HEADER)))
 
 
 @pytest.fixture(scope="module")
@@ -33,18 +38,27 @@ def test_header_declares_expected_surface():
 
 
 def test_library_exports_every_declared_symbol(lib):
-    missing = [f for f in header_functions() if not hasattr(lib, f)]
+    missing = [f for f in all_functions() if not hasattr(lib, f)]
     assert not missing, missing
 
 
 def test_binding_covers_header():
     from vaeb_amd import _lib
     assert sorted(_lib.EXPORTS) == header_functions()
+    assert sorted(_lib.DIAG_EXPORTS) == header_functions(DIAG_HEADER)
+
+
+def test_diagnostics_are_not_in_the_dropin_header():
+    """The drop-in boundary (vaeb_hip.h) holds only the reference's operations and their
+    state transfers; timing / GEMM test hooks live in vaeb_diag.h."""
+    pub = header_functions()
+    for f in ("vaeb_debug_timeline", "vaeb_test_gemm_bf16", "vaeb_bench_gemm_bf16", "vaeb_profile_steps"):
+        assert f not in pub and f in header_functions(DIAG_HEADER)
 
 
 def test_exports_are_c_linkage():
     out = subprocess.run(["nm", "-D", "--defined-only", LIB], capture_output=True, text=True).stdout
-    for f in header_functions():
+    for f in all_functions():
         assert re.search(r"\bT %s$" % f, out, re.M), f
 
 

@@ -63,3 +63,49 @@ def test_cpu_baseline_fvs_leg_runs():
     x = O.synthetic_mnist(n=40, D=56)
     r = bench.cpu_baseline_fv(56, 20, 4, 10, x, budget_s=0.2, max_steps=3, sample=True)
     assert r["kind"] == "port" and r["value"] > 0 and "FVS" in r["sample"]
+
+
+STUB = r'''
+import json, os, sys, time
+out = sys.argv[1]
+rank = int(os.environ["RANK"])
+rec = {k: os.environ.get(k) for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT",
+                                      "HSA_ENABLE_IPC_MODE_LEGACY")}
+rec["argv"] = sys.argv[1:]
+json.dump(rec, open(os.path.join(out, f"rank{rank}.json"), "w"))
+if len(sys.argv) > 2 and sys.argv[2] == "fail" and rank == 1:
+    sys.exit(3)
+if len(sys.argv) > 2 and sys.argv[2] == "fail":
+    time.sleep(60)   # a healthy rank waiting in a collective: the launcher must stop it
+'''
+
+
+def test_launcher_spawns_one_process_per_gpu(tmp_path):
+    """bench.py --gpus N without WORLD_SIZE: N children, RANK = LOCAL_RANK = r, WORLD_SIZE = N,
+    one rendezvous on 127.0.0.1 (the GPU library is never touched by the parent)."""
+    stub = tmp_path / "stub.py"
+    stub.write_text(STUB)
+    rc = bench.spawn_ranks(4, [str(tmp_path)], script=str(stub))
+    assert rc == 0
+    import json
+    recs = [json.load(open(tmp_path / f"rank{r}.json")) for r in range(4)]
+    assert [r["RANK"] for r in recs] == ["0", "1", "2", "3"]
+    assert [r["LOCAL_RANK"] for r in recs] == ["0", "1", "2", "3"]
+    assert all(r["WORLD_SIZE"] == "4" and r["MASTER_ADDR"] == "127.0.0.1" for r in recs)
+    assert len({r["MASTER_PORT"] for r in recs}) == 1
+    assert all(r["HSA_ENABLE_IPC_MODE_LEGACY"] == "0" for r in recs)
+
+
+def test_launcher_stops_the_job_when_a_rank_fails(tmp_path):
+    import time
+    stub = tmp_path / "stub.py"
+    stub.write_text(STUB)
+    t0 = time.time()
+    rc = bench.spawn_ranks(3, [str(tmp_path), "fail"], script=str(stub))
+    assert rc == 3 and time.time() - t0 < 30
+
+
+def test_bench_main_refuses_world_mismatch(monkeypatch):
+    monkeypatch.setenv("WORLD_SIZE", "2")
+    with pytest.raises(SystemExit):
+        bench.main(["--gpus", "4"])

@@ -42,17 +42,29 @@ class FakeModel:
         self.batch_size = batch_size
         self.orders = []
         self.kw = kw
+        self.objective = kw.get("objective", "sum_prior")
+        self.resumed = None
         FakeModel.instances.append(self)
 
     def update_epoch(self, order):
         self.orders.append(np.array(order))
         return float(-10.0 * len(order))
 
-    def validate(self, x):
-        return -5.0 * x.shape[0]
+    def set_validation_data(self, x):
+        self.nvalid = x.shape[0]
+
+    def validate_resident(self):
+        # VAEB.validate: the SGVB sum; the mean_map objective returns the mean
+        return -5.0 if self.objective == "mean_map" else -5.0 * self.nvalid
 
     def save(self, f):
         open(f, "w").write("saved")
+
+    def save_state(self, f):
+        open(f, "w").write("state")
+
+    def load_state(self, f):
+        self.resumed = open(f).read()
 
 
 def test_train_model_epoch_loop_and_trace(tmp_path, monkeypatch, capsys):
@@ -89,3 +101,31 @@ def test_missing_dataset_raises_without_synthetic(tmp_path, monkeypatch):
         cli.load_dataset(False, synthetic=False)
     xt, xv = cli.load_dataset(False, synthetic=True)
     assert xt.shape == (50000, 784) and xv.shape == (10000, 784)
+
+
+def test_mean_map_validation_is_not_divided_twice(tmp_path, monkeypatch, capsys):
+    """--objective mean_map: validate already returns the per-row mean
+    (VAEBfullbayes.py:161-165), so Lvalid is printed as is; sum_prior divides the sum by
+    x_valid.shape[0] (VAEB.py:582).  Both give -5.0 here."""
+    from vaeb_amd import model
+    monkeypatch.setattr(model, "VAEB", FakeModel)
+    monkeypatch.chdir(tmp_path)
+    for obj in ("mean_map", "sum_prior"):
+        args = cli.parse_args(['--n_epochs', '1', '--synthetic', '--continuous', '--objective', obj])
+        cli.train_model(args)
+        out = capsys.readouterr().out
+        assert "          [Lower bound on validation set: -5.0]" in out, (obj, out)
+
+
+def test_state_file_and_resume_file(tmp_path, monkeypatch):
+    """--state_file writes the native checkpoint at the end; --resume_file loads one
+    before the first epoch (keys added to the args dict, never renamed)."""
+    from vaeb_amd import model
+    monkeypatch.setattr(model, "VAEB", FakeModel)
+    monkeypatch.chdir(tmp_path)
+    (tmp_path / "r.ckpt").write_text("prev")
+    args = cli.parse_args(['--n_epochs', '1', '--synthetic', '--continuous', '--state_file', str(tmp_path / "s.ckpt"),
+                           '--resume_file', str(tmp_path / "r.ckpt")])
+    cli.train_model(args)
+    assert FakeModel.instances[-1].resumed == "prev"
+    assert (tmp_path / "s.ckpt").read_text() == "state"

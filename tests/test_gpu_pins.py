@@ -1,0 +1,103 @@
+"""The HIP path pinned DIRECTLY to outputs the reference itself produced,
+not only to the CPU restatement:
+
+1. full_vb_res/continuous_2.trc -- the reference's 1000-epoch trace of the literal
+   --full_varational run (Frey 560-200-2, started from reconstruction_res/VAE_continuous_2.mdl;
+   fixture tests/golden/fv_frey2.npz).  Each trace value is SGVB/B = data + thetaPrior/B
+   (VAEB.py:349-367, 410), where thetaPrior depends only on the (mu, sigma) Adagrad
+   dynamics and the data term is a fixed-theta forward on the real (absent) Frey data.  The
+   HIP FV step is run for 100 epochs x 15 steps from the same mu0 on synthetic Frey-shaped
+   rows with eps = 0, the fixed-theta data term of each minibatch is measured by the HIP
+   validate, and the HIP thetaPrior/B series recovered as step value - data term.  The
+   reference trace minus that series must be the reference's constant data term:
+   mean 97343.7 +- 3 (the CPU pin's value), std < 10, slope < 0.05 per epoch.
+2. reconstruction_res/continuous_{2,10,20}.mdl and the reference's
+   `_image_0_{i}_original.jpg` / `_sample.jpg` pairs (fixture tests/golden/recon_frey.npz,
+   made by tests/golden/make_recon_fixture.py): vaeb_reconstruct on the decoded inputs
+   reproduces the decoded reference outputs to the JPEG's resolution (mean |diff| <= 0.021
+   per model), while a wrong model or the untrained initialisation misses by >= 0.025, and
+   for z = 10 and 20 every output is nearest to its own input's reconstruction.
+"""
+import os
+
+import numpy as np
+import pytest
+
+from oracle import vaeb_oracle as O
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def test_fv_trace_pin_on_hip_path():
+    from vaeb_amd import _lib
+    fv = np.load(os.path.join(GOLD, "fv_frey2.npz"))
+    mu0 = fv["mu0"].astype(np.float32)
+    trace = fv["trace_L"]
+    cfg = O.Config(D=560, H=200, Z=2, continuous=True)
+    B, E, S = 100, 100, 15
+    x = O.synthetic_frey(n=B * S)
+    ctx = _lib.Context(560, 200, 2, B, decoder=_lib.DEC_GAUSSIAN, estimator=_lib.EST_FV, max_eval_rows=B)
+    ctx.set_data(x)
+    ctx.set_params(mu0)
+    ctx.set_fv_state(mu0, np.full_like(mu0, 1e-3), np.zeros_like(mu0), np.zeros_like(mu0))
+    ctx.set_eps_mode(_lib.EPS_HOST)
+    zeros = np.zeros((1, B, 2), np.float32)
+    ctx.push_eps(zeros)
+    # fixed-theta data term of every minibatch (eps = 0), from the HIP forward
+    lb = _lib.Context(560, 200, 2, B, decoder=_lib.DEC_GAUSSIAN, estimator=_lib.EST_LB, max_eval_rows=B)
+    lb.set_data(x)
+    lb.set_params(mu0)
+    lb.set_eps_mode(_lib.EPS_HOST)
+    lb.push_eps(zeros)
+    data = np.array([lb.validate(x[b * B:(b + 1) * B]) for b in range(S)])
+    lb.close()
+    rs = np.random.RandomState(15485863)
+    order = np.arange(S)
+    resid = []
+    for e in range(E):
+        rs.shuffle(order)
+        tp_over_b = [ctx.update(int(b)) - data[b] for b in order]
+        resid.append(trace[e] - float(np.mean(tp_over_b)))
+    ctx.close()
+    resid = np.array(resid)
+    assert abs(resid.mean() - 97343.7) < 3.0, resid.mean()
+    assert resid.std() < 10.0, resid.std()
+    assert abs(np.polyfit(np.arange(E), resid, 1)[0]) < 0.05
+
+
+@pytest.fixture(scope="module")
+def recon():
+    return np.load(os.path.join(GOLD, "recon_frey.npz"))
+
+
+def _hip_recon(theta, x, z):
+    from vaeb_amd import _lib
+    ctx = _lib.Context(560, 200, z, 100, decoder=_lib.DEC_GAUSSIAN, max_eval_rows=64)
+    ctx.set_params(theta)
+    y = ctx.reconstruct(x)
+    ctx.close()
+    return y
+
+
+@pytest.mark.parametrize("z", [2, 10, 20])
+def test_reconstruction_pin_against_reference_images(recon, z):
+    theta = recon[f"theta_z{z}"]
+    x = recon[f"x_orig_z{z}"]
+    y_ref = recon[f"y_sample_z{z}"]
+    y = _hip_recon(theta, x, z)
+    cfg = O.Config(D=560, H=200, Z=z, continuous=True)
+    # the HIP path against the restatement on these exact inputs (1e-5)
+    ref = O.reconstruct(O.unflatten(theta.astype(np.float64), cfg), x.astype(np.float64), None, cfg)
+    assert np.abs(y - ref).max() <= 1e-5
+    # ... and against the reference's own outputs, to the JPEG's resolution
+    d = np.abs(y - y_ref).mean()
+    assert d <= 0.021, d
+    for z2 in (2, 10, 20):   # a wrong trained model misses
+        if z2 != z:
+            assert np.abs(_hip_recon(recon[f"theta_z{z2}"], x, z2) - y_ref).mean() >= 0.025
+    init = O.flatten(O.init_params(cfg))   # and so does the untrained initialisation
+    assert np.abs(_hip_recon(init, x, z) - y_ref).mean() >= 0.1
+    if z >= 10:   # each reference output is nearest to its own input's reconstruction
+        M = np.abs(y[None, :, :] - y_ref[:, None, :]).mean(-1)
+        assert np.array_equal(M.argmin(1), np.arange(8))

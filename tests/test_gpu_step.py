@@ -53,6 +53,7 @@ CASES = [
     ("frey_LA", dict(D=560, H=200, Z=5, continuous=True, estimator="LA", L=2), 100),
     ("mean_map_frey10", dict(D=560, H=200, Z=10, continuous=True, objective="mean_map"), 100),
     ("mean_map_mnist", dict(D=784, H=500, Z=10, objective="mean_map"), 100),
+    ("mean_map_mnist20", dict(D=784, H=500, Z=20, objective="mean_map"), 100),   # config 4 shapes
     ("wide_latent_generic", dict(D=64, H=40, Z=40, L=2), 20),
     ("wide_latent_LA", dict(D=66, H=48, Z=36, estimator="LA"), 30),
     ("gauss_odd_D", dict(D=45, H=30, Z=6, continuous=True), 17),

@@ -120,3 +120,36 @@ def test_init_draw_order():
     W4 = prng.normal(0, 0.01, (5, 3)).astype(np.float32)
     assert np.array_equal(p[0], W3) and np.array_equal(p[1], W4)
     assert all(np.all(b == 0) for b in p[5:])
+
+
+@pytest.mark.parametrize("z", [2, 10, 20])
+def test_oracle_reconstruction_matches_reference_images(z):
+    """reconstruction_res/continuous_{z}.mdl + its _image_0_{i}_original/_sample.jpg pairs
+    (tests/golden/recon_frey.npz): the restated encoder -> z = mu -> decoder mean
+    (VAEB.py:245-270) reproduces the reference's saved reconstructions to the JPEG's
+    resolution; a different trained model does not."""
+    f = np.load(os.path.join(os.path.dirname(__file__), "golden", "recon_frey.npz"))
+    cfg = O.Config(D=560, H=200, Z=z, continuous=True)
+    x, y_ref = f[f"x_orig_z{z}"].astype(np.float64), f[f"y_sample_z{z}"]
+    r = O.reconstruct(O.unflatten(f[f"theta_z{z}"].astype(np.float64), cfg), x, None, cfg)
+    assert np.abs(r - y_ref).mean() <= 0.021
+    z2 = 2 if z != 2 else 20
+    cfg2 = O.Config(D=560, H=200, Z=z2, continuous=True)
+    r2 = O.reconstruct(O.unflatten(f[f"theta_z{z2}"].astype(np.float64), cfg2), x, None, cfg2)
+    assert np.abs(r2 - y_ref).mean() >= 0.025
+
+
+def test_fullbayes_init_draw_order():
+    """VAEBfullbayes.py:28-67 draws each weight ONCE (W3, W4, W5, W1, W2[, W6]), unlike
+    VAEB.py's duplicated W3 / W4; the product's initialiser agrees with the oracle's."""
+    from vaeb_amd.fullbayes import initial_params_fullbayes
+    for cont in (False, True):
+        cfg = O.Config(D=9, H=6, Z=3, continuous=cont)
+        p = O.init_params_fullbayes(cfg)
+        prng = np.random.RandomState(10)
+        W3 = prng.normal(0, 0.01, (9, 6)).astype(np.float32)
+        W4 = prng.normal(0, 0.01, (6, 3)).astype(np.float32)
+        assert np.array_equal(p[0], W3) and np.array_equal(p[1], W4)
+        assert not np.array_equal(p[0], O.init_params(cfg)[0])
+        q = initial_params_fullbayes(9, 6, 3, cont)
+        assert all(np.array_equal(a, b) for a, b in zip(p, q))

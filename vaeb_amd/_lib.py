@@ -23,19 +23,22 @@ OBJ_SUM_PRIOR, OBJ_MEAN_MAP = 0, 1
 EPS_PHILOX, EPS_HOST = 0, 1
 DTYPE_F32, DTYPE_BF16 = 0, 1
 
-# Every symbol declared in include/vaeb_hip.h (checked by tests/test_abi.py).
+# Every symbol declared in include/vaeb_hip.h (the drop-in boundary) and in
+# include/vaeb_diag.h (measurement / test hooks); checked by tests/test_abi.py.
 EXPORTS = [
     "vaeb_last_error", "vaeb_version", "vaeb_create", "vaeb_destroy", "vaeb_num_params",
     "vaeb_set_data", "vaeb_set_params", "vaeb_get_params", "vaeb_set_adagrad_state",
     "vaeb_get_adagrad_state", "vaeb_set_fv_state", "vaeb_get_fv_state", "vaeb_set_eps_mode",
-    "vaeb_push_eps", "vaeb_set_step", "vaeb_update", "vaeb_update_async", "vaeb_update_many",
+    "vaeb_push_eps", "vaeb_set_step", "vaeb_get_step", "vaeb_update", "vaeb_update_async", "vaeb_update_many",
     "vaeb_epoch_elbo", "vaeb_synchronize", "vaeb_validate", "vaeb_reconstruct", "vaeb_reconstruct_sampled",
-    "vaeb_comm_unique_id", "vaeb_comm_init", "vaeb_get_grads", "vaeb_get_activation",
-    "vaeb_profile_steps", "vaeb_kernel_name", "vaeb_debug_timeline", "vaeb_test_gemm_bf16", "vaeb_bench_gemm_bf16", "vaeb_push_fv_noise",
+    "vaeb_comm_unique_id", "vaeb_comm_init", "vaeb_comm_count", "vaeb_set_valid_data", "vaeb_validate_resident",
+    "vaeb_checkpoint_save", "vaeb_checkpoint_load", "vaeb_get_grads", "vaeb_get_activation", "vaeb_push_fv_noise",
     "vaeb_ae_create", "vaeb_ae_destroy", "vaeb_ae_num_params", "vaeb_ae_set_data", "vaeb_ae_set_params",
     "vaeb_ae_get_params", "vaeb_ae_set_adagrad_state", "vaeb_ae_get_adagrad_state", "vaeb_ae_train",
     "vaeb_ae_train_many", "vaeb_ae_reconstruct", "vaeb_ae_encode", "vaeb_ae_decode",
 ]
+DIAG_EXPORTS = ["vaeb_profile_steps", "vaeb_kernel_name", "vaeb_debug_timeline", "vaeb_test_gemm_bf16",
+                "vaeb_bench_gemm_bf16"]
 AE_MAX_LAYERS = 8
 AE_BINARY, AE_CONT = 0, 1
 ACT = {"tanh": 0, "sigmoid": 1, "relu": 2}
@@ -96,6 +99,12 @@ def load():
         "vaeb_set_eps_mode": ([_P, ctypes.c_int32, ctypes.c_uint64], ctypes.c_int),
         "vaeb_push_eps": ([_P, _F, _I64, ctypes.c_int32], ctypes.c_int),
         "vaeb_set_step": ([_P, _I64], ctypes.c_int),
+        "vaeb_get_step": ([_P, ctypes.POINTER(_I64)], ctypes.c_int),
+        "vaeb_comm_count": ([_P, ctypes.POINTER(ctypes.c_int32)], ctypes.c_int),
+        "vaeb_set_valid_data": ([_P, _F, _I64], ctypes.c_int),
+        "vaeb_validate_resident": ([_P, ctypes.POINTER(ctypes.c_double)], ctypes.c_int),
+        "vaeb_checkpoint_save": ([_P, ctypes.c_char_p], ctypes.c_int),
+        "vaeb_checkpoint_load": ([_P, ctypes.c_char_p], ctypes.c_int),
         "vaeb_update": ([_P, ctypes.c_int32, _F], ctypes.c_int),
         "vaeb_update_async": ([_P, ctypes.c_int32], ctypes.c_int),
         "vaeb_update_many": ([_P, ctypes.POINTER(ctypes.c_int32), ctypes.c_int32], ctypes.c_int),
@@ -242,6 +251,18 @@ class Context:
     def set_step(self, step):
         check(self.lib.vaeb_set_step(self.h, int(step)))
 
+    def get_step(self):
+        n = _I64()
+        check(self.lib.vaeb_get_step(self.h, ctypes.byref(n)))
+        return n.value
+
+    # ---- native checkpoint (theta, Adagrad state, Philox seed / step, FV state)
+    def checkpoint_save(self, path):
+        check(self.lib.vaeb_checkpoint_save(self.h, os.fsencode(path)))
+
+    def checkpoint_load(self, path):
+        check(self.lib.vaeb_checkpoint_load(self.h, os.fsencode(path)))
+
     # ---- steps
     def update(self, index):
         out = ctypes.c_float()
@@ -265,6 +286,17 @@ class Context:
         x = np.ascontiguousarray(x, np.float32)
         out = ctypes.c_double()
         check(self.lib.vaeb_validate(self.h, fptr(x), x.shape[0], ctypes.byref(out)))
+        return out.value
+
+    def set_valid_data(self, x):
+        """Upload the validation set once (device-resident, VAEB.py:582's x_valid)."""
+        x = np.ascontiguousarray(x, np.float32)
+        check(self.lib.vaeb_set_valid_data(self.h, fptr(x), x.shape[0]))
+
+    def validate_resident(self):
+        """SGVB sum over the resident validation set (this rank's share, all-reduced)."""
+        out = ctypes.c_double()
+        check(self.lib.vaeb_validate_resident(self.h, ctypes.byref(out)))
         return out.value
 
     def reconstruct(self, x):
@@ -291,6 +323,12 @@ class Context:
     def comm_init(self, uid: bytes, rank, world):
         buf = (ctypes.c_uint8 * 128).from_buffer_copy(uid)
         check(self.lib.vaeb_comm_init(self.h, buf, rank, world))
+
+    def comm_count(self):
+        """Ranks in the library's RCCL communicator (ncclCommCount); 1 without one."""
+        n = ctypes.c_int32()
+        check(self.lib.vaeb_comm_count(self.h, ctypes.byref(n)))
+        return n.value
 
     def bench_gemm_bf16(self, a_kouter, b_kouter, M, N, K, tile_n=0, reps=10):
         """Mean ms per launch of the bf16 GEMM on device-generated operands (diagnostics)."""

@@ -4,7 +4,8 @@
 Same `command_line_args` / `command_line_flags` dicts (including the misspelt
 `full_varational`), the same `--name value` / `--flag` parsing with a warning (not an
 error) for unused arguments, the same stdout lines and trace CSV.  Keys ADDED (never
-renamed): device, rng, objective, max_eval_rows, trace_dedup (args) and synthetic (flag).
+renamed): device, rng, objective, max_eval_rows, trace_dedup, fv_sample, state_file,
+resume_file (args) and synthetic (flag).
 """
 from __future__ import annotations
 
@@ -35,8 +36,10 @@ command_line_args = {'seed': (15485863, int),
                      'objective': ('sum_prior', str),  # sum_prior (VAEB.py) | mean_map (VAEBfullbayes.py)
                      'max_eval_rows': (10000, int),
                      'trace_dedup': (0, int),       # 1: write each trace row once
-                     'fv_sample': (0, int)}         # 1 (with --full_varational): weight-posterior sample
+                     'fv_sample': (0, int),         # 1 (with --full_varational): weight-posterior sample
                                                     # theta~ = mu + |sigma| zeta (VAEB.py:127-129; extension)
+                     'state_file': ('', str),       # native checkpoint (theta + Adagrad + RNG) written at the end
+                     'resume_file': ('', str)}      # native checkpoint to resume from
 #   to add a new flag, add its name (VAEB.py:37-38)
 command_line_flags = ['continuous', 'generic_estimator', 'full_varational',
                       'synthetic']                 # added: synthetic data when the pickles are absent
@@ -152,6 +155,11 @@ def train_model(args):
     model = VAEB(x_train, continuous, hidden_unit, n_latent, batch_size, L, learning_rate, generic_estimator,
                  full_varational, params, **kw)
 
+    if args.get('resume_file'):
+        model.load_state(args['resume_file'])
+    # x_valid is uploaded once and evaluated on device each epoch (VAEB.py:582)
+    model.set_validation_data(x_valid)
+
     print("learning")
     dedup = bool(args.get('trace_dedup', 0))
     if len(trace_file) > 0:
@@ -163,7 +171,11 @@ def train_model(args):
         np.random.shuffle(batch_order)
         LB = model.update_epoch(batch_order)
         LB /= len(batch_order)
-        LBvalidation = model.validate(x_valid) / x_valid.shape[0]
+        # VAEB.validate returns the SGVB sum (VAEB.py:418-422), divided here (:582); the
+        # mean_map objective's validate already returns the mean (VAEBfullbayes.py:161-165)
+        LBvalidation = model.validate_resident()
+        if model.objective != "mean_map":
+            LBvalidation /= x_valid.shape[0]
         if len(trace_file) > 0:
             with open(trace_file, 'a') as f:
                 f.write('{0},{1},{2}\n'.format(model.N * (epoch + 1), LB, LBvalidation))
@@ -174,6 +186,8 @@ def train_model(args):
                 f.write('{0},{1},{2}\n'.format(model.N * (epoch + 1), LB, LBvalidation))
     if len(save_file) > 0:
         model.save(save_file)
+    if args.get('state_file'):
+        model.save_state(args['state_file'])
     return model, data
 
 

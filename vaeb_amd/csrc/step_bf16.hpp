@@ -399,6 +399,7 @@ struct BfState {
     bf16_t* shadow2[2] = {nullptr, nullptr};
     bf16_t* x = nullptr;               // dataset [N x D] bf16
     bf16_t* xeval = nullptr;           // eval chunk [R x D]
+    bf16_t* xval = nullptr;            // resident validation set [nval x D] (vaeb_set_valid_data)
     bf16_t *h = nullptr, *z = nullptr, *hd = nullptr, *dA = nullptr, *dA1 = nullptr, *dml = nullptr,
            *dA3 = nullptr;
     float *ml_slab = nullptr, *dz_slab = nullptr, *w_slab = nullptr;

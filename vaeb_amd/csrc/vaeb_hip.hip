@@ -17,7 +17,7 @@
 #include <string>
 #include <vector>
 
-#include "../../include/vaeb_hip.h"
+#include "../../include/vaeb_diag.h"   // includes vaeb_hip.h
 #include "hfuse.hpp"
 #include "latent.hpp"
 #include "step_bf16.hpp"
@@ -69,7 +69,7 @@ int dalloc(T** p, size_t n) {
 
 // Control block layout (ints): [0] cursor, [1] resolved batch, [2..] batch order.
 constexpr int kFvParts = 1024;   // FV stream grid (one thetaPrior partial per block)
-constexpr int kGraphSteps = 32;
+constexpr int kGraphLog2 = 5;    // the longest replayed graph: 2^5 = 32 steps
 constexpr int kMaxProfKernels = 24;
 constexpr int kDbgWG = 1024;      // diagnostics: stamp slots per launch (workgroups)
 
@@ -102,6 +102,8 @@ struct vaeb_ctx {
     float* data = nullptr;
     int64_t nrows = 0;
     float* xeval = nullptr;
+    float* xval = nullptr;        // resident validation set (vaeb_set_valid_data; bf16: bf.xval)
+    int64_t nval = 0;
     // control
     int* ictl = nullptr;          // cursor, cur_batch, order[kOrderCap], next (tile_engine.hpp)
     int64_t* step = nullptr;
@@ -127,7 +129,8 @@ struct vaeb_ctx {
     double* h_d2 = nullptr;
     hipEvent_t ctl_ev = nullptr;
     // graphs
-    hipGraphExec_t g1[2] = {nullptr, nullptr}, gS = nullptr;
+    hipGraphExec_t g1[2] = {nullptr, nullptr};
+    hipGraphExec_t gP[kGraphLog2 + 1] = {};   // gP[k]: 2^k steps from arena 0 (run_steps)
     bool graph_failed = false;
     // comm
     ncclComm_t comm = nullptr;
@@ -172,6 +175,8 @@ StepArgs make_args(vaeb_ctx* c, int par, int Mb, int mode, const float* xbase, b
     a.b6 = gs ? t + c->off[bo + 5] : nullptr;
     a.xbase = xbase;
     if (train) {
+        // this rank's rows of global minibatch b start at row b * B_global + row_offset
+        a.xbase = xbase + (int64_t)g.row_offset * g.D;
         a.order = c->ictl + 2;
         a.cursor = c->ictl;
         a.cur_batch = c->ictl + 1;
@@ -375,7 +380,7 @@ int prep_wgrad(vaeb_ctx* c, const WGroup* groups, int n, const OptArgs& opt, con
     w.opt = opt;
     w.with_elbo = e != nullptr;
     if (e) w.elbo = *e;
-    w.xbase = c->data; w.cur_batch = c->ictl + 1; w.batch_stride = a.batch_stride; w.P = c->P;
+    w.xbase = a.xbase; w.cur_batch = c->ictl + 1; w.batch_stride = a.batch_stride; w.P = c->P;
     w.dbg = a.dbg;
     // 16-byte panel loads need every panel row aligned with widths % 4 == 0 (the
     // activation buffers are hipMalloc'd; X rows are D floats apart)
@@ -383,7 +388,7 @@ int prep_wgrad(vaeb_ctx* c, const WGroup* groups, int n, const OptArgs& opt, con
     auto al = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
     for (int gi = 0; gi < n; ++gi) {
         const WGroup& G = w.g[gi];
-        vec = vec && (G.ld_at % 4 == 0) && (G.rowsW % 4 == 0) && (G.at_is_x ? al(c->data) : al(G.at)) &&
+        vec = vec && (G.ld_at % 4 == 0) && (G.rowsW % 4 == 0) && (G.at_is_x ? al(a.xbase) : al(G.at)) &&
               (G.ld0 % 4 == 0) && (G.N0 % 4 == 0) && al(G.b0) &&
               (G.N1 == 0 || ((G.ld1 % 4 == 0) && (G.N1 % 4 == 0) && al(G.b1)));
     }
@@ -638,8 +643,9 @@ bool flips(const vaeb_ctx* c) { return c->c.estimator != VAEB_EST_FV && c->c.est
 
 void free_graphs(vaeb_ctx* c) {
     for (auto& g1 : c->g1) if (g1) hipGraphExecDestroy(g1);
-    if (c->gS) hipGraphExecDestroy(c->gS);
-    c->g1[0] = c->g1[1] = c->gS = nullptr;
+    for (auto& gp : c->gP) if (gp) hipGraphExecDestroy(gp);
+    c->g1[0] = c->g1[1] = nullptr;
+    for (auto& gp : c->gP) gp = nullptr;
 }
 
 // Capture nsteps consecutive steps starting from parameter arena `par`.
@@ -666,14 +672,31 @@ int step_eager(vaeb_ctx* c) {
     return 0;
 }
 
-// Enqueue n steps (graph replay when enabled, else eager launches).  Graphs: g1[par]
-// is one step from arena par; gS is kGraphSteps (even) steps from arena 0.
+// Graph `k` of the power-of-two family: 2^k steps from arena 0 (k = 1 .. kGraphLog2),
+// captured on first use.
+int graph_pow2(vaeb_ctx* c, int k, hipGraphExec_t* out) {
+    if (!c->gP[k]) {
+        if (int rc = capture(c, 1 << k, 0, &c->gP[k])) {
+            c->graph_failed = true;
+            free_graphs(c);
+            (void)hipGetLastError();
+            return rc;
+        }
+    }
+    *out = c->gP[k];
+    return 0;
+}
+
+// Enqueue n steps (graph replay when enabled, else eager launches).  Graphs: g1[par] is
+// one step from arena par; gP[k] is 2^k (even) steps from arena 0.  Any n replays as
+// [one step back to arena 0] + n / 32 launches of the 32-step graph + one graph per set
+// bit of the remainder (16, 8, 4, 2) + [one step]: at most 6 graph launches besides the
+// 32-step ones, so the per-step cost does not depend on n % 32.
 int run_steps(vaeb_ctx* c, int n) {
     if (c->c.use_graph && !c->graph_failed) {
-        if (!c->gS) {
+        if (!c->g1[0]) {
             int rc = capture(c, 1, 0, &c->g1[0]);
             if (rc == 0) rc = capture(c, 1, 1, &c->g1[1]);
-            if (rc == 0) rc = capture(c, kGraphSteps, 0, &c->gS);
             if (rc) { c->graph_failed = true; free_graphs(c); (void)hipGetLastError(); }
         }
         if (!c->graph_failed) {
@@ -684,9 +707,23 @@ int run_steps(vaeb_ctx* c, int n) {
                 return 0;
             };
             if (c->par != 0 && n > 0) { if (int rc = one()) return rc; ++i; }
-            for (; i + kGraphSteps <= n; i += kGraphSteps) HIP_TRY(hipGraphLaunch(c->gS, c->s));
-            for (; i < n; ++i) if (int rc = one()) return rc;
-            return 0;
+            // FV / FVS never flip the arena: c->par stays 0 and every family graph applies
+            for (int k = kGraphLog2; k >= 1 && !c->graph_failed; --k) {
+                const int len = 1 << k;
+                if (k < kGraphLog2 && ((n - i) & len) == 0) continue;
+                while (n - i >= len && !c->graph_failed) {
+                    hipGraphExec_t g = nullptr;
+                    if (graph_pow2(c, k, &g)) break;
+                    HIP_TRY(hipGraphLaunch(g, c->s));
+                    i += len;
+                    if (k < kGraphLog2) break;
+                }
+            }
+            if (!c->graph_failed) {
+                for (; i < n; ++i) if (int rc = one()) return rc;
+                return 0;
+            }
+            n -= i;   // a capture failed: the rest runs eagerly
         }
     }
     for (int i = 0; i < n; ++i)
@@ -833,7 +870,7 @@ int vaeb_destroy(vaeb_ctx* c) {
     free_graphs(c);
     bf_free(c);
     if (c->comm) ncclCommDestroy(c->comm);
-    float* fp[] = {c->theta2[0], c->theta2[1], c->acc, c->grad, c->fvmu, c->fvsg, c->fvam, c->fvas, c->fv_part, c->data, c->xeval,
+    float* fp[] = {c->theta2[0], c->theta2[1], c->acc, c->grad, c->fvmu, c->fvsg, c->fvam, c->fvas, c->fv_part, c->data, c->xeval, c->xval,
                    c->elbo_out, c->eps_in, c->h, c->mu, c->lv, c->eps, c->z, c->hd, c->y, c->dA2, c->dA6, c->dA1,
                    c->dZ, c->dMuLv, c->dA3, c->kl_part, c->lp_part, c->slab_ml, c->slab_dz, c->yacc,
                    c->fvzeta};
@@ -997,6 +1034,9 @@ int vaeb_update_many(vaeb_ctx* c, const int32_t* idx, int32_t n) {
     if (!c || (!idx && n > 0) || n < 0) return fail(VAEB_ERR_ARG, "bad arguments");
     if (int rc = check_batches(c, idx, n)) return rc;
     if (int rc = host_eps_ready(c, c->c.B)) return rc;
+    // host eps holds ONE step's noise: a multi-step call would train every step on it
+    if (c->eps_mode == VAEB_EPS_HOST && n > 1)
+        return fail(VAEB_ERR_STATE, "host eps mode: one step per call (push eps before each vaeb_update)");
     for (int32_t done = 0; done < n;) {
         const int32_t m = std::min<int32_t>(n - done, kOrderCap);
         if (int rc = upload_order(c, idx + done, m)) return rc;
@@ -1024,7 +1064,67 @@ int vaeb_synchronize(vaeb_ctx* c) {
     return 0;
 }
 
-// Forward-only passes over host rows in device chunks (validate / reconstruct).
+// Forward-only passes in device chunks (validate / reconstruct).  The arena the data term
+// reads: the current theta, or for VAEB_EST_FVS the posterior mean mu_theta (copied into
+// the spare arena once per call).
+static int eval_arena(vaeb_ctx* c, int* epar) {
+    *epar = c->par;
+    if (c->c.estimator == VAEB_EST_FVS) {
+        *epar = c->par ^ 1;
+        HIP_TRY(hipMemcpyAsync(c->theta2[*epar], c->fvmu, sizeof(float) * (size_t)c->P, hipMemcpyDeviceToDevice, c->s));
+    }
+    return 0;
+}
+
+// One fp32 chunk: `rows` device rows at x = global rows [r0, r0 + rows).  MODE_EVAL adds
+// the chunk's SGVB into eval_acc; MODE_RECON copies the decoder means to out_y (host).
+static int eval_chunk_f32(vaeb_ctx* c, int epar, const float* x, int rows, int64_t r0, int mode, float* out_y) {
+    const vaeb_config& g = c->c;
+    StepArgs a = make_args(c, epar, rows, mode, x, false);
+    a.row_base_add = r0;
+    a.eps_in = c->eps_in ? c->eps_in + r0 * g.Z : nullptr;
+    a.eps_in_ld = c->eps_rows;
+    Prof pr{c, false};
+    if (int rc = enqueue_forward(c, a, pr)) return rc;
+    if (mode == MODE_RECON) {
+        HIP_TRY(hipMemcpyAsync(out_y, c->y, sizeof(float) * (size_t)rows * g.D, hipMemcpyDeviceToHost, c->s));
+    } else {
+        ElboArgs e = base_elbo(c, a);
+        e.eval_acc = c->eval_acc;
+        hipLaunchKernelGGL(elbo_kernel, dim3(1), dim3(256), 0, c->s, e);
+        CHECK_LAUNCH();
+    }
+    return 0;
+}
+
+// SGVB of n evaluated rows from eval_acc (after an optional all-reduce of it over the
+// ranks); the FV estimators add thetaPrior: x.shape[0] * (sum logp + sum KL) + thetaPrior
+// (VAEB.py:364).
+static int eval_finish(vaeb_ctx* c, int64_t n, bool allreduce, double* out_sum) {
+    const vaeb_config& g = c->c;
+    double tp = 0.0;
+    const bool fvx = g.estimator == VAEB_EST_FV || g.estimator == VAEB_EST_FVS;
+    if (fvx) {
+        hipLaunchKernelGGL(fv_kernel, dim3(kFvParts), dim3(256), 0, c->s, c->fvmu, c->fvsg, c->fvam, c->fvas, c->P,
+                           g.lr, g.adagrad_eps, 0, c->fv_part);
+        CHECK_LAUNCH();
+        std::vector<float> parts(kFvParts);
+        HIP_TRY(hipMemcpyAsync(parts.data(), c->fv_part, sizeof(float) * kFvParts, hipMemcpyDeviceToHost, c->s));
+        HIP_TRY(hipStreamSynchronize(c->s));
+        for (float p : parts) tp += p;
+    }
+    if (allreduce && c->comm) {
+        ncclResult_t r = ncclAllReduce(c->eval_acc, c->eval_acc, 1, ncclDouble, ncclSum, c->comm, c->s);
+        if (r != ncclSuccess) return fail(VAEB_ERR_COMM, "ncclAllReduce(validation): %s", ncclGetErrorString(r));
+    }
+    HIP_TRY(hipMemcpyAsync(c->h_d2, c->eval_acc, 2 * sizeof(double), hipMemcpyDeviceToHost, c->s));
+    HIP_TRY(hipStreamSynchronize(c->s));
+    const double data = c->h_d2[0];
+    *out_sum = fvx ? (double)n * data + tp : data;
+    return 0;
+}
+
+// Host rows: each chunk is staged through xeval (stream-ordered, one sync at the end).
 static int eval_rows(vaeb_ctx* c, const float* x, int64_t n, int mode, float* out_y, double* out_sum) {
     if (!c || !x || n <= 0) return fail(VAEB_ERR_ARG, "bad arguments");
     if (mode == MODE_EVAL && c->eps_mode == VAEB_EPS_HOST && c->eps_rows != n)
@@ -1033,57 +1133,174 @@ static int eval_rows(vaeb_ctx* c, const float* x, int64_t n, int mode, float* ou
     const vaeb_config& g = c->c;
     const int chunk = c->c.max_eval_rows;
     HIP_TRY(hipMemsetAsync(c->eval_acc, 0, 2 * sizeof(double), c->s));
+    int epar = c->par;
+    if (!is_bf16(c)) if (int rc = eval_arena(c, &epar)) return rc;
     for (int64_t r0 = 0; r0 < n; r0 += chunk) {
         const int rows = (int)std::min<int64_t>(chunk, n - r0);
+        float* yo = out_y ? out_y + r0 * g.D : nullptr;
         if (is_bf16(c)) {
-            if (int rc = bf_eval_chunk(c, x + r0 * g.D, rows, r0, mode, out_y ? out_y + r0 * g.D : nullptr)) return rc;
-            HIP_TRY(hipStreamSynchronize(c->s));
+            if (int rc = bf_eval_chunk(c, x + r0 * g.D, rows, r0, mode, yo)) return rc;
             continue;
         }
         HIP_TRY(hipMemcpyAsync(c->xeval, x + r0 * g.D, sizeof(float) * (size_t)rows * g.D, hipMemcpyHostToDevice, c->s));
-        int epar = c->par;
-        if (g.estimator == VAEB_EST_FVS) {   // the data term at the posterior mean mu_theta
-            epar = c->par ^ 1;
-            HIP_TRY(hipMemcpyAsync(c->theta2[epar], c->fvmu, sizeof(float) * (size_t)c->P, hipMemcpyDeviceToDevice, c->s));
-        }
-        StepArgs a = make_args(c, epar, rows, mode, c->xeval, false);
-        a.row_base_add = r0;
-        a.eps_in = c->eps_in ? c->eps_in + r0 * g.Z : nullptr;
-        a.eps_in_ld = c->eps_rows;
-        Prof pr{c, false};
-        if (int rc = enqueue_forward(c, a, pr)) return rc;
-        if (mode == MODE_RECON) {
-            HIP_TRY(hipMemcpyAsync(out_y + r0 * g.D, c->y, sizeof(float) * (size_t)rows * g.D, hipMemcpyDeviceToHost, c->s));
-        } else {
-            ElboArgs e = base_elbo(c, a);
-            e.eval_acc = c->eval_acc;
-            hipLaunchKernelGGL(elbo_kernel, dim3(1), dim3(256), 0, c->s, e);
-            CHECK_LAUNCH();
-        }
-        HIP_TRY(hipStreamSynchronize(c->s));
+        if (int rc = eval_chunk_f32(c, epar, c->xeval, rows, r0, mode, yo)) return rc;
     }
-    if (mode == MODE_EVAL) {
-        double tp = 0.0;
-        if (g.estimator == VAEB_EST_FV || g.estimator == VAEB_EST_FVS) {
-            hipLaunchKernelGGL(fv_kernel, dim3(kFvParts), dim3(256), 0, c->s, c->fvmu, c->fvsg, c->fvam, c->fvas, c->P,
-                               g.lr, g.adagrad_eps, 0, c->fv_part);
-            CHECK_LAUNCH();
-            std::vector<float> parts(kFvParts);
-            HIP_TRY(hipMemcpyAsync(parts.data(), c->fv_part, sizeof(float) * kFvParts, hipMemcpyDeviceToHost, c->s));
-            HIP_TRY(hipStreamSynchronize(c->s));
-            for (float p : parts) tp += p;
-        }
-        HIP_TRY(hipMemcpy(c->h_d2, c->eval_acc, 2 * sizeof(double), hipMemcpyDeviceToHost));
-        const double data = c->h_d2[0];
-        // FV validate: x.shape[0] * (sum logp + sum KL) + thetaPrior (VAEB.py:364)
-        *out_sum = (g.estimator == VAEB_EST_FV || g.estimator == VAEB_EST_FVS) ? (double)n * data + tp : data;
-    }
+    if (mode == MODE_EVAL) return eval_finish(c, n, false, out_sum);
+    HIP_TRY(hipStreamSynchronize(c->s));
     return 0;
 }
 
 int vaeb_validate(vaeb_ctx* c, const float* x, int64_t n, double* out_sum) {
     if (!out_sum) return fail(VAEB_ERR_ARG, "null out_sum");
     return eval_rows(c, x, n, MODE_EVAL, nullptr, out_sum);
+}
+
+int vaeb_set_valid_data(vaeb_ctx* c, const float* x, int64_t n) {
+    if (!c || !x || n <= 0) return fail(VAEB_ERR_ARG, "bad validation-set arguments");
+    HIP_TRY(hipStreamSynchronize(c->s));
+    if (c->xval) { hipFree(c->xval); c->xval = nullptr; }
+    if (c->bf.xval) { hipFree(c->bf.xval); c->bf.xval = nullptr; }
+    c->nval = 0;
+    if (is_bf16(c)) {
+        if (int rc = dalloc(&c->bf.xval, (size_t)n * c->c.D)) return rc;
+        if (int rc = bf_upload_rows(c, x, n, c->bf.xval)) return rc;
+        HIP_TRY(hipStreamSynchronize(c->s));
+    } else {
+        if (int rc = dalloc(&c->xval, (size_t)n * c->c.D)) return rc;
+        HIP_TRY(hipMemcpy(c->xval, x, sizeof(float) * (size_t)n * c->c.D, hipMemcpyHostToDevice));
+    }
+    c->nval = n;
+    return 0;
+}
+
+// This rank's contiguous share of the resident rows: the first (n % world) ranks take one
+// extra row (the row split of vaeb_amd/dp.py).
+static void valid_share(const vaeb_ctx* c, int64_t* lo, int64_t* rows) {
+    const int64_t W = c->comm ? c->world : 1, r = c->comm ? c->rank : 0;
+    const int64_t base = c->nval / W, extra = c->nval % W;
+    *rows = base + (r < extra ? 1 : 0);
+    *lo = r * base + std::min<int64_t>(r, extra);
+}
+
+int vaeb_validate_resident(vaeb_ctx* c, double* out_sum) {
+    if (!c || !out_sum) return fail(VAEB_ERR_ARG, "null argument");
+    if (c->nval <= 0) return fail(VAEB_ERR_STATE, "vaeb_set_valid_data has not been called");
+    if (c->eps_mode == VAEB_EPS_HOST && c->eps_rows != c->nval)
+        return fail(VAEB_ERR_STATE, "host eps mode: resident validation needs eps for all %lld rows (pushed %lld)",
+                    (long long)c->nval, (long long)c->eps_rows);
+    const vaeb_config& g = c->c;
+    int64_t lo = 0, rows = 0;
+    valid_share(c, &lo, &rows);
+    HIP_TRY(hipMemsetAsync(c->eval_acc, 0, 2 * sizeof(double), c->s));
+    int epar = c->par;
+    if (!is_bf16(c)) if (int rc = eval_arena(c, &epar)) return rc;
+    const int chunk = g.max_eval_rows;
+    for (int64_t r0 = lo; r0 < lo + rows; r0 += chunk) {
+        const int m = (int)std::min<int64_t>(chunk, lo + rows - r0);
+        if (is_bf16(c)) {
+            if (int rc = bf_eval_chunk_dev(c, c->bf.xval + r0 * g.D, m, r0, MODE_EVAL, nullptr)) return rc;
+        } else {
+            if (int rc = eval_chunk_f32(c, epar, c->xval + r0 * g.D, m, r0, MODE_EVAL, nullptr)) return rc;
+        }
+    }
+    return eval_finish(c, c->nval, true, out_sum);
+}
+
+int vaeb_get_step(vaeb_ctx* c, int64_t* step) {
+    if (!c || !step) return fail(VAEB_ERR_ARG, "null argument");
+    HIP_TRY(hipStreamSynchronize(c->s));
+    HIP_TRY(hipMemcpy(step, c->step, sizeof(int64_t), hipMemcpyDeviceToHost));
+    return 0;
+}
+
+int vaeb_comm_count(vaeb_ctx* c, int32_t* out_world) {
+    if (!c || !out_world) return fail(VAEB_ERR_ARG, "null argument");
+    if (!c->comm) { *out_world = 1; return 0; }
+    int n = 0;
+    ncclResult_t r = ncclCommCount(c->comm, &n);
+    if (r != ncclSuccess) return fail(VAEB_ERR_COMM, "ncclCommCount: %s", ncclGetErrorString(r));
+    *out_world = n;
+    return 0;
+}
+
+// ------------------------------------------------------------------ native checkpoint
+namespace {
+struct CkptHeader {
+    char magic[8];          // "VAEBCKPT"
+    int32_t version;        // 1
+    int32_t D, H, Z, L, decoder, estimator, objective, dtype;
+    int32_t eps_mode, has_fv;
+    int64_t P;
+    uint64_t seed;
+    int64_t step;
+    int64_t reserved[4];
+};
+constexpr char kCkptMagic[8] = {'V', 'A', 'E', 'B', 'C', 'K', 'P', 'T'};
+
+struct FileCloser { FILE* f; ~FileCloser() { if (f) fclose(f); } };
+}  // namespace
+
+int vaeb_checkpoint_save(vaeb_ctx* c, const char* path) {
+    if (!c || !path) return fail(VAEB_ERR_ARG, "null argument");
+    const vaeb_config& g = c->c;
+    CkptHeader h{};
+    memcpy(h.magic, kCkptMagic, 8);
+    h.version = 1;
+    h.D = g.D; h.H = g.H; h.Z = g.Z; h.L = g.L;
+    h.decoder = g.decoder; h.estimator = g.estimator; h.objective = g.objective; h.dtype = g.dtype;
+    h.eps_mode = c->eps_mode;
+    h.has_fv = c->fvmu ? 1 : 0;
+    h.P = c->P;
+    h.seed = c->seed;
+    HIP_TRY(hipStreamSynchronize(c->s));
+    HIP_TRY(hipMemcpy(&h.step, c->step, sizeof(int64_t), hipMemcpyDeviceToHost));
+    std::vector<float*> arrs = {c->theta2[c->par], c->acc};
+    if (h.has_fv) arrs.insert(arrs.end(), {c->fvmu, c->fvsg, c->fvam, c->fvas});
+    std::vector<float> buf((size_t)c->P);
+    FileCloser fc{fopen(path, "wb")};
+    if (!fc.f) return fail(VAEB_ERR_ARG, "checkpoint: cannot open %s for writing", path);
+    if (fwrite(&h, sizeof(h), 1, fc.f) != 1) return fail(VAEB_ERR_ARG, "checkpoint: write failed (%s)", path);
+    for (float* d : arrs) {
+        HIP_TRY(hipMemcpy(buf.data(), d, sizeof(float) * buf.size(), hipMemcpyDeviceToHost));
+        if (fwrite(buf.data(), sizeof(float), buf.size(), fc.f) != buf.size())
+            return fail(VAEB_ERR_ARG, "checkpoint: write failed (%s)", path);
+    }
+    if (fflush(fc.f) != 0) return fail(VAEB_ERR_ARG, "checkpoint: flush failed (%s)", path);
+    return 0;
+}
+
+int vaeb_checkpoint_load(vaeb_ctx* c, const char* path) {
+    if (!c || !path) return fail(VAEB_ERR_ARG, "null argument");
+    const vaeb_config& g = c->c;
+    FileCloser fc{fopen(path, "rb")};
+    if (!fc.f) return fail(VAEB_ERR_ARG, "checkpoint: cannot open %s", path);
+    CkptHeader h{};
+    if (fread(&h, sizeof(h), 1, fc.f) != 1 || memcmp(h.magic, kCkptMagic, 8) != 0 || h.version != 1)
+        return fail(VAEB_ERR_ARG, "checkpoint: %s is not a version-1 vaeb checkpoint", path);
+    if (h.D != g.D || h.H != g.H || h.Z != g.Z || h.L != g.L || h.decoder != g.decoder ||
+        h.estimator != g.estimator || h.P != c->P)
+        return fail(VAEB_ERR_ARG, "checkpoint: %s holds a %d-%d-%d L=%d dec=%d est=%d model, the context is "
+                    "%d-%d-%d L=%d dec=%d est=%d", path, h.D, h.H, h.Z, h.L, h.decoder, h.estimator,
+                    g.D, g.H, g.Z, g.L, g.decoder, g.estimator);
+    if (h.has_fv && !c->fvmu) return fail(VAEB_ERR_ARG, "checkpoint: variational state without an FV context");
+    std::vector<float> buf((size_t)c->P);
+    std::vector<float*> arrs = {c->theta2[c->par], c->acc};
+    if (h.has_fv) arrs.insert(arrs.end(), {c->fvmu, c->fvsg, c->fvam, c->fvas});
+    HIP_TRY(hipStreamSynchronize(c->s));
+    for (float* d : arrs) {
+        if (fread(buf.data(), sizeof(float), buf.size(), fc.f) != buf.size())
+            return fail(VAEB_ERR_ARG, "checkpoint: %s is truncated", path);
+        HIP_TRY(hipMemcpy(d, buf.data(), sizeof(float) * buf.size(), hipMemcpyHostToDevice));
+    }
+    if (is_bf16(c)) {
+        if (int rc = bf_make_shadow(c, c->par)) return rc;
+        HIP_TRY(hipStreamSynchronize(c->s));
+    }
+    HIP_TRY(hipMemcpy(c->step, &h.step, sizeof(int64_t), hipMemcpyHostToDevice));
+    if (h.eps_mode != c->eps_mode) { free_graphs(c); c->graph_failed = false; }
+    c->eps_mode = h.eps_mode;
+    c->seed = h.seed;
+    return 0;
 }
 
 int vaeb_reconstruct(vaeb_ctx* c, const float* x, int64_t n, float* out_y) {

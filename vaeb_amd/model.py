@@ -198,6 +198,7 @@ class VAEB:
         per-step SGVB/B values (what train_model accumulates, VAEB.py:577-579)."""
         if self._stream is not None:
             return float(sum(self.update(int(b)) for b in batch_order))
+        self._ctx.epoch_elbo()   # drop what earlier update() calls added to the accumulator
         self._ctx.update_many(np.asarray(batch_order, np.int32))
         s, n = self._ctx.epoch_elbo()
         return s
@@ -210,6 +211,21 @@ class VAEB:
             self._ctx.push_eps(self._stream.draw(x.shape[0], self.n_latent))
         v = self._ctx.validate(x)
         return v / x.shape[0] if self.objective == "mean_map" else v
+
+    def set_validation_data(self, x):
+        """Upload x_valid once (device-resident); validate_resident() then evaluates it
+        each epoch with no host copy, sharded over the ranks when data-parallel."""
+        x = np.asarray(x, np.float32)
+        self._nvalid = x.shape[0]
+        self._ctx.set_valid_data(x)
+
+    def validate_resident(self):
+        """validate(x_valid) on the resident validation set: SGVB sum (mean for the
+        mean_map objective), all-reduced over the ranks."""
+        if self._stream is not None:
+            self._ctx.push_eps(self._stream.draw(self._nvalid, self.n_latent))
+        v = self._ctx.validate_resident()
+        return v / self._nvalid if self.objective == "mean_map" else v
 
     def reconstruct(self, x, n_samples=0):
         """VAEB.reconstruct (VAEB.py:267-300): the decoder mean at z = mu for n_samples <= 0,
@@ -237,6 +253,16 @@ class VAEB:
                 pickle.dump(v, f, protocol=2)
             for a in self._param_arrays():
                 pickle.dump(a, f, protocol=2)
+
+    def save_state(self, file_name):
+        """Native checkpoint (vaeb_checkpoint_save): theta, the Adagrad accumulators, the
+        Philox seed / step and the variational state -- everything a bit-identical resume
+        needs, unlike the reference's .mdl (VAEB.py:189-203 keeps theta only)."""
+        self._ctx.checkpoint_save(file_name)
+
+    def load_state(self, file_name):
+        """Resume from save_state's file (shape and estimator must match)."""
+        self._ctx.checkpoint_load(file_name)
 
     @staticmethod
     def read_checkpoint(file_name):

@@ -286,7 +286,12 @@ def read_array_pickle(path):
     """A pickled ndarray / tuple of ndarrays (freyfaces.pkl, mnist.pkl.gz, modelFrey.pkl)."""
     opener = gzip.open if str(path).endswith(".gz") else open
     with opener(path, "rb") as fh:
-        obj = load_frames(fh.read(), max_frames=1)[0]
+        return read_array_pickle_bytes(fh.read())
+
+
+def read_array_pickle_bytes(data: bytes):
+    """read_array_pickle on an in-memory pickle stream."""
+    obj = load_frames(data, max_frames=1)[0]
 
     def conv(o):
         a = to_array(o)
