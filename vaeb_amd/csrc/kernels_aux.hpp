@@ -80,7 +80,7 @@ DEV double block_sum256w(double v, double* sh) {
 DEV void advance_cursor(int* cursor) {
     const int c1 = *cursor + 1;
     *cursor = c1;
-    cursor[kCtlNext] = cursor[2 + c1];
+    cursor[kCtlNext] = cursor[kCtlOrder + c1];
 }
 
 DEV void elbo_reduce(const ElboArgs& e, double* sh) {
@@ -117,6 +117,19 @@ DEV void elbo_emit(const ElboArgs& e, double lp, double kl, double fv) {
     }
     if (e.cursor) advance_cursor(e.cursor);
     if (e.step) *e.step += 1;
+}
+
+// A short batch order as a kernel argument (vaeb_hip.hip upload_order): writes
+// [cursor = 0, cur_batch = 0, next = order[0], order...] on the step stream.
+constexpr int kArgOrder = 960;   // 3.8 KB of kernel argument
+struct OrderArg { int n; int v[kArgOrder]; };
+__global__ __launch_bounds__(256) void set_order_kernel(int* ictl, OrderArg u) {
+    for (int i = threadIdx.x; i < u.n; i += 256) ictl[kCtlOrder + i] = u.v[i];
+    if (threadIdx.x == 0) {
+        ictl[0] = 0;
+        ictl[1] = 0;
+        ictl[kCtlNext] = u.n > 0 ? u.v[0] : 0;
+    }
 }
 
 // Measurement helper: holds the stream for ~`ticks` x 10 ns (s_memrealtime runs at

@@ -49,12 +49,14 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 namespace vaeb {
 
-// Device control block (vaeb_hip.hip: ictl): [cursor, cur_batch, order[kOrderCap], next].
+// Device control block (vaeb_hip.hip: ictl): [cursor, cur_batch, next, order[kOrderCap]].
 // `next` = order[cursor] is kept by whoever advances the cursor (the step's last launch;
 // upload_order for a fresh order), so the next step's encoder resolves its input rows
-// with ONE dependent load instead of the cursor -> order[cursor] chain.
+// with ONE dependent load instead of the cursor -> order[cursor] chain.  The head words
+// and the order are contiguous, so a fresh order is one upload.
 constexpr int kOrderCap = 1 << 20;
-constexpr int kCtlNext = kOrderCap + 2;   // offset of `next` from the cursor
+constexpr int kCtlNext = 2;    // offset of `next` from the cursor
+constexpr int kCtlOrder = 3;   // offset of order[0]
 
 // A control word that no workgroup of this launch writes (cursor / next / cur_batch, all
 // written by earlier launches): read through the constant address space, i.e. a scalar

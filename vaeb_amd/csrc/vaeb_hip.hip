@@ -177,7 +177,7 @@ StepArgs make_args(vaeb_ctx* c, int par, int Mb, int mode, const float* xbase, b
     if (train) {
         // this rank's rows of global minibatch b start at row b * B_global + row_offset
         a.xbase = xbase + (int64_t)g.row_offset * g.D;
-        a.order = c->ictl + 2;
+        a.order = c->ictl + kCtlOrder;
         a.cursor = c->ictl;
         a.cur_batch = c->ictl + 1;
         a.batch_stride = (int64_t)g.B_global * g.D;
@@ -695,8 +695,12 @@ int graph_pow2(vaeb_ctx* c, int k, hipGraphExec_t* out) {
 int run_steps(vaeb_ctx* c, int n) {
     if (c->c.use_graph && !c->graph_failed) {
         if (!c->g1[0]) {
+            // the whole family at first use: a capture inside a later (timed) call would
+            // cost more than the launches it saves
             int rc = capture(c, 1, 0, &c->g1[0]);
             if (rc == 0) rc = capture(c, 1, 1, &c->g1[1]);
+            hipGraphExec_t g = nullptr;
+            for (int k = 1; k <= kGraphLog2 && rc == 0; ++k) rc = graph_pow2(c, k, &g);
             if (rc) { c->graph_failed = true; free_graphs(c); (void)hipGetLastError(); }
         }
         if (!c->graph_failed) {
@@ -731,15 +735,25 @@ int run_steps(vaeb_ctx* c, int n) {
     return 0;
 }
 
-// Upload a batch order (cursor reset to 0) through the pinned staging buffer.
+// Upload a batch order (cursor reset to 0).  Up to kArgOrder entries travel as a kernel
+// argument of set_order_kernel (a kernel on the step stream starts sooner than a host ->
+// device copy: the fixed cost of a short update_many call), longer ones through the
+// pinned staging buffer in one contiguous copy of [cursor, cur_batch, next, order...].
 int upload_order(vaeb_ctx* c, const int32_t* idx, int n) {
+    if (n <= kArgOrder) {
+        OrderArg u;
+        u.n = n;
+        memcpy(u.v, idx, sizeof(int) * (size_t)n);
+        hipLaunchKernelGGL(set_order_kernel, dim3(1), dim3(256), 0, c->s, c->ictl, u);
+        CHECK_LAUNCH();
+        return 0;
+    }
     HIP_TRY(hipEventSynchronize(c->ctl_ev));
     c->h_ctl[0] = 0;
     c->h_ctl[1] = 0;
-    memcpy(c->h_ctl + 2, idx, sizeof(int) * (size_t)n);
     c->h_ctl[kCtlNext] = n > 0 ? idx[0] : 0;
-    HIP_TRY(hipMemcpyAsync(c->ictl, c->h_ctl, sizeof(int) * (size_t)(n + 2), hipMemcpyHostToDevice, c->s));
-    HIP_TRY(hipMemcpyAsync(c->ictl + kCtlNext, c->h_ctl + kCtlNext, sizeof(int), hipMemcpyHostToDevice, c->s));
+    memcpy(c->h_ctl + kCtlOrder, idx, sizeof(int) * (size_t)n);
+    HIP_TRY(hipMemcpyAsync(c->ictl, c->h_ctl, sizeof(int) * (size_t)(n + kCtlOrder), hipMemcpyHostToDevice, c->s));
     HIP_TRY(hipEventRecord(c->ctl_ev, c->s));
     return 0;
 }
@@ -820,7 +834,7 @@ int vaeb_create(const vaeb_config* cfg, vaeb_ctx** out) {
     }
     rc = rc ? rc : dalloc(&c->fv_part, kFvParts);
     rc = rc ? rc : dalloc(&c->xeval, (size_t)R * D);
-    rc = rc ? rc : dalloc(&c->ictl, kCtlNext + 1);
+    rc = rc ? rc : dalloc(&c->ictl, kCtlOrder + kOrderCap);
     rc = rc ? rc : dalloc(&c->step, 1);
     rc = rc ? rc : dalloc(&c->elbo_out, 1);
     rc = rc ? rc : dalloc(&c->epoch, 2);
@@ -849,7 +863,7 @@ int vaeb_create(const vaeb_config* cfg, vaeb_ctx** out) {
     }
     if (!rc && is_bf16(c)) rc = bf_alloc(c);
     if (rc) { vaeb_destroy(c); return rc; }
-    if (hipHostMalloc((void**)&c->h_ctl, sizeof(int) * (kCtlNext + 1), 0) != hipSuccess ||
+    if (hipHostMalloc((void**)&c->h_ctl, sizeof(int) * (kCtlOrder + kOrderCap), 0) != hipSuccess ||
         hipHostMalloc((void**)&c->h_elbo, sizeof(float) * 4, 0) != hipSuccess ||
         hipHostMalloc((void**)&c->h_d2, sizeof(double) * 4, 0) != hipSuccess) {
         vaeb_destroy(c);
