@@ -200,6 +200,19 @@ struct WGroup {
     int tiles_j, wg_begin, wg_end;
 };
 
+// dA3 = ([dMu | dLv] [W4 | W5]^T) (1 - h^2) computed inside the dW3 workgroups (the
+// folded latent backward, latent_bwd.hpp): the B panel of dW3 = [X | 1]^T dA3 is formed
+// from dMuLv, W4 / W5 (pre-update arena) and h instead of being loaded.
+struct Da3Src {
+    const float *dml, *W4, *W5, *h;
+    float* dA3;           // the column slice is also stored (by the D-row tile 0 workgroups)
+    int Z, H, Mb, Mbp;
+};
+
+// Kernel arguments of a weight-gradient launch: up to two groups (WGradArgs), or the three
+// groups + dA3 source of the folded latent backward's last launch (WGradArgs3).  Separate
+// types because the kernarg size shows in every launch that takes it (the 3-group form as
+// the common type cost the 2-group launch 6.9 -> 8.6 us).
 struct WGradArgs {
     WGroup g[2];
     int ngroups, total_wgs;
@@ -210,13 +223,100 @@ struct WGradArgs {
     int64_t P;
     uint64_t* dbg;
 };
+struct WGradArgs3 {
+    WGroup g[3];
+    int ngroups, total_wgs;
+    OptArgs opt;
+    ElboArgs elbo;
+    int with_elbo;
+    const float* xbase; const int* cur_batch; int64_t batch_stride;
+    int64_t P;
+    uint64_t* dbg;
+    Da3Src da3;
+};
+
+// [W4 | W5]^T element block B(k, n) = W4[n][k] (k < Z) | W5[n][k - Z] (Z <= k < 2Z), four
+// consecutive k at row n (16-byte loads when vz: Z % 4 == 0 and both bases aligned).
+DEV f32x4 ld_w45(rsrc_t bw4, rsrc_t bw5, int Z, int H, int n, int k, bool vz) {
+    if (vz) return (k < Z) ? kc4(bw4, Z, n, k, H, Z, true) : kc4(bw5, Z, n, k - Z, H, Z, true);
+    f32x4 v;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+        const int kk = k + s;
+        const bool ok = n < H;
+        v[s] = bld(bw4, (ok && kk < Z) ? (uint32_t)(n * Z + kk) * 4u : kOOB) +
+               bld(bw5, (ok && kk >= Z && kk < 2 * Z) ? (uint32_t)(n * Z + kk - Z) * 4u : kOOB);
+    }
+    return v;
+}
+
+// dA3 rows [kb, kb + kWKB) x columns [j0, j0 + 16 TS) into the B panel sb (Da3Src): wave
+// w of NWV takes the 16-row blocks w, w + NWV, ... (NR = kWKB / 16 / NWV of them); K = 2Z
+// <= 64.  Every operand of all NR blocks is issued before the first MFMA (one round trip;
+// a per-block load -> MFMA loop cost the launch a second one), the [W4 | W5]^T slice once.
+template <int NWV, int TS>
+DEV void da3_panel(const Da3Src& d, int kb, int j0, bool store, float (*sb)[kWP]) {
+    constexpr int NR = kWKB / 16 / NWV;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int li = lane & 15, q = lane >> 4;
+    const int Z = d.Z, H = d.H, K2 = 2 * d.Z;
+    const rsrc_t bd = mkbuf(d.dml, (int64_t)d.Mbp * K2 * 4);
+    const rsrc_t bw4 = mkbuf(d.W4, (int64_t)H * Z * 4), bw5 = mkbuf(d.W5, (int64_t)H * Z * 4);
+    const rsrc_t bh = mkbuf(d.h, (int64_t)d.Mbp * H * 4);
+    const bool vz = (Z & 3) == 0 && aligned16(d.W4) && aligned16(d.W5);
+    const bool vd = (K2 & 3) == 0 && aligned16(d.dml);
+    const int nkc = (K2 + 15) >> 4;
+    f32x4 bw[TS][4], av[NR][4], hv[NR][TS];
+#pragma unroll
+    for (int ts = 0; ts < TS; ++ts)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) bw[ts][c] = ld_w45(bw4, bw5, Z, c < nkc ? H : 0, j0 + 16 * ts + li, c * 16 + 4 * q, vz);
+#pragma unroll
+    for (int u = 0; u < NR; ++u) {
+        const int r0 = kb + 16 * (wv + NWV * u);
+        const int rl = r0 < d.Mbp ? d.Mbp : 0;   // blocks past the padded batch load nothing
+#pragma unroll
+        for (int c = 0; c < 4; ++c) av[u][c] = kc4(bd, K2, r0 + li, c * 16 + 4 * q, c < nkc ? rl : 0, K2, vd);
+#pragma unroll
+        for (int ts = 0; ts < TS; ++ts) {
+            const int n = j0 + 16 * ts + li;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int mm = r0 + 4 * q + r;
+                hv[u][ts][r] = bld(bh, (n < H && mm < d.Mb) ? (uint32_t)(mm * H + n) * 4u : kOOB);
+            }
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < NR; ++u) {
+        const int t = wv + NWV * u;
+        const int r0 = kb + 16 * t;
+        if (r0 >= d.Mbp) break;
+#pragma unroll
+        for (int ts = 0; ts < TS; ++ts) {
+            f32x4 acc = zero4();
+#pragma unroll
+            for (int c = 0; c < 4; ++c)
+                if (c < nkc) acc = mfma4(av[u][c], bw[ts][c], acc);
+            const int n = j0 + 16 * ts + li;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int mm = r0 + 4 * q + r;
+                const float v = (mm < d.Mb && n < H) ? acc[r] * (1.f - hv[u][ts][r] * hv[u][ts][r]) : 0.f;
+                sb[16 * t + 4 * q + r][16 * ts + li] = v;
+                if (store && n < H) d.dA3[(int64_t)mm * H + n] = v;
+            }
+        }
+    }
+}
 
 // One 64 x (16 TS) tile of group g (passed with a compile-time index, so its fields are
 // scalar kernel-argument loads; a dynamic index made hipcc fetch them with serialized
 // per-lane vector loads).  NWV = 4 waves (standalone launch) or 8 (a 512-thread fused
 // launch): waves w and w + 4 then take alternate K chunks and are summed through LDS.
-template <bool VEC, int NWV, int TS>
-DEV void wgrad_body(const WGradArgs& p, const WGroup& g, int bid, float (*sa)[kWP], float (*sb)[kWP]) {
+// DA3: the B panel is dA3, formed in the workgroup (da3_panel) instead of loaded.
+template <bool VEC, int NWV, int TS, bool DA3 = false, class WA>
+DEV void wgrad_body(const WA& p, const WGroup& g, int bid, float (*sa)[kWP], float (*sb)[kWP]) {
     static_assert(NWV == 4 || NWV == 8, "wgrad: 4 or 8 waves");
     static_assert(TS == 1 || TS == 2 || TS == 4, "wgrad: 16, 32 or 64 columns per tile");
     constexpr int kWTS = TS, kWTJ = 16 * TS;
@@ -284,7 +384,9 @@ DEV void wgrad_body(const WGradArgs& p, const WGroup& g, int bid, float (*sa)[kW
                 for (int s = 0; s < 4; ++s)
                     ra[u][s] = bld(ba, (k < g.klim_at && i + s < g.rowsW) ? (uint32_t)(k * g.ld_at + i + s) * 4u : kOOB);
             }
-            if (vb) {
+            if (DA3) {
+                rb[u] = zero4();
+            } else if (vb) {
                 const bool in0 = j < g.N0;
                 const uint32_t o0 = (jt && k < g.K && in0) ? (uint32_t)(k * g.ld0 + j) * 4u : kOOB;
                 const uint32_t o1 = (jt && k < g.K && !in0 && j - g.N0 < g.N1) ? (uint32_t)(k * g.ld1 + j - g.N0) * 4u : kOOB;
@@ -299,6 +401,7 @@ DEV void wgrad_body(const WGradArgs& p, const WGroup& g, int bid, float (*sa)[kW
                 }
             }
         }
+        if constexpr (DA3) da3_panel<NWV, TS>(p.da3, kb, j0, i0 == 0, sb);
 #pragma unroll
         for (int u = 0; u < NU; ++u) {
             const int e = threadIdx.x + NTH * u;
@@ -309,7 +412,7 @@ DEV void wgrad_body(const WGradArgs& p, const WGroup& g, int bid, float (*sa)[kW
 #pragma unroll
             for (int s = 0; s < 4; ++s) v[s] = (i + s == g.rowsW) ? ((kb + kr < g.K) ? 1.f : 0.f) : v[s];
             *reinterpret_cast<f32x4*>(&sa[kr][4 * c4]) = v;
-            *reinterpret_cast<f32x4*>(&sb[kr][4 * c4]) = rb[u];
+            if constexpr (!DA3) *reinterpret_cast<f32x4*>(&sb[kr][4 * c4]) = rb[u];
         }
         __syncthreads();
         const int nch = min(kWKB, g.K - kb) >> 4;
@@ -380,6 +483,27 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WGradArgs p) {
     }
     if (p.ngroups > 1 && bid >= p.g[1].wg_begin) wgrad_body<VEC, 4, TS>(p, p.g[1], bid, sa, sb);
     else wgrad_body<VEC, 4, TS>(p, p.g[0], bid, sa, sb);
+}
+
+// The folded latent backward's last launch: dW3 (dA3 formed in the workgroup) | dW4 | dW5
+// | dW1, and the ELBO workgroup first.
+template <bool VEC, int TS>
+__global__ __launch_bounds__(256) void wgrad3_kernel(WGradArgs3 p) {
+    __shared__ float sa[kWKB][kWP];
+    __shared__ float sb[kWKB][kWP];
+    int bid;
+    if (p.with_elbo)
+        bid = blockIdx.x == 0 ? p.total_wgs : xcd_remap((int)blockIdx.x - 1, p.total_wgs);
+    else
+        bid = xcd_remap(blockIdx.x, p.total_wgs);
+    if (p.dbg && threadIdx.x == 0) p.dbg[bid * 8 + 0] = __builtin_amdgcn_s_memrealtime();
+    if (bid >= p.total_wgs) {
+        elbo_reduce(p.elbo, reinterpret_cast<double*>(&sa[0][0]));
+        return;
+    }
+    if (bid >= p.g[2].wg_begin) wgrad_body<VEC, 4, TS>(p, p.g[2], bid, sa, sb);
+    else if (bid >= p.g[1].wg_begin) wgrad_body<VEC, 4, TS>(p, p.g[1], bid, sa, sb);
+    else wgrad_body<VEC, 4, TS, true>(p, p.g[0], bid, sa, sb);
 }
 
 // ----------------------------------------------------------------- DP optimizer

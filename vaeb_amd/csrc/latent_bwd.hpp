@@ -1,0 +1,195 @@
+// latent_bwd.hpp -- the latent-width backward folded into the dhd launch (training step,
+// Z <= 32): the backward counterpart of latent.hpp's encoder fold.
+//
+//  dhd_dz_body (one 16 x 16 tile of dA1, 8 waves splitting K = D (| 2D Gaussian)):
+//      dA1 = (dA2 W2^T (+ dA6 W6^T)) (1 - hd^2)                         
+//      and the tile's share of dZ = dA1 W1^T: its 16 x 16 dA1 block times the matching
+//      16 columns of W1^T, published as a write-through partial slab; the LAST tile of each
+//      16-row latent block (over the H column tiles and the L sample planes) sums the
+//      slabs in fixed order (bitwise reproducible) and runs the element-wise latent
+//      backward: dZ, [dMu | dLv] = (sum_l dZ_l - sc mu, 1/2 s sum_l dZ_l eps_l +
+//      sc/2 (1 - e^lv)), or the LA direct terms (VAEB.py:315-346).
+//
+// dA3 = ([dMu | dLv] [W4 | W5]^T) (1 - h^2) is then formed inside the dW3 workgroups of the
+// last launch (kernels_aux.hpp: da3_panel), so the former dz / dh launch -- 56 workgroups
+// that each recomputed dZ from 72 KB of dA1 and W1 -- and its kernel boundary are gone.
+//
+// Slab hand-off: the encoder's form (latent.hpp arrive_last and the guide rule cited
+// there): sc1 slab stores by wave 0 only, its vmcnt drain, one relaxed agent-scope ticket
+// per tile on the row block's counter, sc1 slab loads by the last arriver.
+#pragma once
+#include "latent.hpp"
+#include "kernels_aux.hpp"
+
+namespace vaeb {
+
+// [dMu | dLv] of element (m, j) from dzsum = sum_l dZ_l and dzes = sum_l dZ_l eps_l
+// (LB / FV: KL direct terms; LA: the prior-logQ direct terms, VAEB.py:322-325).
+DEV void latent_bwd_elem(const StepArgs& a, bool valid, int m, int j, float mu, float lv, const float* epre,
+                         const float* zpre, float dzsum, float dzes, float& dmu, float& dlv) {
+    const int Z = a.Z;
+    const float sl = a.sc / (float)a.L;
+    const float sd = fexp(0.5f * lv);
+    dmu = 0.f;
+    dlv = 0.f;
+    if (!valid) return;
+    if (a.est == EST_LA) {
+        float tm = 0.f, tv = 0.f;
+        for (int l = 0; l < a.L; ++l) {
+            const int64_t ol = ((int64_t)l * a.Mbp + m) * Z + j;
+            const float z = (l < kLP) ? zpre[l] : a.z[ol];
+            const float e = (l < kLP) ? epre[l] : a.eps[ol];
+            tm += -z;
+            tv += 0.5f - 0.5f * z * sd * e;
+        }
+        dmu = dzsum + sl * tm;
+        dlv = dzes * 0.5f * sd + sl * tv;
+    } else {
+        dmu = dzsum - a.sc * mu;
+        dlv = dzes * 0.5f * sd + a.sc * 0.5f * (1.f - fexp(lv));
+    }
+}
+
+// One dhd tile (bx = row block of the L * Mbp decoder rows, by = H column tile) + its dZ
+// slab; the last arriver of latent row block bx % (Mbp / 16) finishes the latent backward.
+// red: >= 512 f32x4 of LDS.
+template <int NCT, int GCH, bool V>
+DEV void dhd_dz_body(const PDhdT<V>& p0, int bx, int by, f32x4* red, int sid) {
+    __shared__ float ts[16][20];
+    __shared__ int sflag;
+    PDhdT<V> p = p0;
+    p.prepare();
+    const StepArgs& a = p.a;
+    VAEB_STAMP_AT(a, sid, 0);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int li = lane & 15, q = lane >> 4;
+    const int Z = a.Z, H = a.H;
+    const int m0 = bx * 16, n0 = by * 16;
+    const int nrb = a.Mbp >> 4, nctH = (H + 15) >> 4;
+    const int l = bx / nrb, rbl = bx % nrb;
+
+    typename PDhdT<V>::Pre pre{};
+    f32x4 w1v[NCT];
+    if (wave == 0) {
+        pre = p.prefetch(m0, n0);
+        // W1^T rows n0 .. n0 + 15 at latent j = ct * 16 + li: 4 consecutive n per lane
+        const rsrc_t bw1 = mkbuf(a.W1, (int64_t)Z * H * 4);
+        const bool vh = (H & 3) == 0 && aligned16(a.W1);
+#pragma unroll
+        for (int ct = 0; ct < NCT; ++ct) w1v[ct] = kc4(bw1, H, ct * 16 + li, n0 + 4 * q, Z, H, vh);
+    }
+    f32x4 acc[1] = {zero4()};
+    wave_mainloop<1, 8, GCH>(p, m0 + li, n0 + li, p.K, wave, acc);
+    VAEB_STAMP_AT(a, sid, 1);
+    red[wave * 64 + lane] = acc[0];
+    __syncthreads();
+    if (wave == 0) {
+#pragma unroll
+        for (int s = 1; s < 8; ++s) acc[0] += red[s * 64 + lane];
+        const int n = n0 + li;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int m = m0 + 4 * q + r;
+            const float hd = pre.hd[r];
+            const float v = (n < H && (m % a.Mbp) < a.Mb) ? acc[0][r] * (1.f - hd * hd) : 0.f;
+            if (n < H) a.dA1[(int64_t)m * H + n] = v;
+            ts[4 * q + r][li] = v;
+        }
+        // partial dZ of this tile: (16 x 16 dA1) . (16 rows of W1^T)
+        f32x4 av;
+#pragma unroll
+        for (int s = 0; s < 4; ++s) av[s] = ts[li][4 * q + s];
+        const rsrc_t bs = mkbuf(a.slab_dz, (int64_t)a.L * a.Mbp * nctH * Z * 4);
+        const int64_t blk = ((int64_t)l * nrb + rbl) * nctH + by;
+#pragma unroll
+        for (int ct = 0; ct < NCT; ++ct) {
+            const f32x4 sv = mfma4(av, w1v[ct], zero4());
+            const int j = ct * 16 + li;
+            st4_sc1(bs, j < Z ? (uint32_t)(((blk * Z + j) * 16 + 4 * q) * 4) : kOOB, sv);
+        }
+    }
+    VAEB_STAMP_AT(a, sid, 2);
+    if (!arrive_last(a.cnt_dz + rbl, nctH * a.L, &sflag)) return;
+    VAEB_STAMP_AT(a, sid, 3);
+
+    // ---- reducer: latent row block rbl, all L planes.  Thread (ml, j) owns one element;
+    // its element-wise operands ride the round trip of the first slab loads.
+    const int ml = threadIdx.x >> 5, j = threadIdx.x & 31;
+    const int m = rbl * 16 + ml;
+    const bool valid = j < Z && m < a.Mb;
+    const uint32_t oj = valid ? (uint32_t)(m * Z + j) * 4u : kOOB;
+    const float mu = bld(mkbuf(a.mu, (int64_t)a.Mbp * Z * 4), oj);
+    const float lv = bld(mkbuf(a.lv, (int64_t)a.Mbp * Z * 4), oj);
+    float epre[kLP], zpre[kLP];
+    {
+        const rsrc_t be = mkbuf(a.eps, (int64_t)a.Me * Z * 4);
+        const rsrc_t bz = mkbuf(a.z, (int64_t)a.Me * Z * 4);
+#pragma unroll
+        for (int s = 0; s < kLP; ++s) {
+            const uint32_t o = (valid && s < a.L) ? (uint32_t)((s * a.Mbp + m) * Z + j) * 4u : kOOB;
+            epre[s] = bld(be, o);
+            zpre[s] = (a.est == EST_LA) ? bld(bz, o) : 0.f;
+        }
+    }
+    const rsrc_t bs = mkbuf(a.slab_dz, (int64_t)a.L * a.Mbp * nctH * Z * 4);
+    const int NF4 = 4 * Z;            // float4 per slab (Z columns x 16 rows)
+    const int NP = 512 / NF4;         // slab partitions (threads >= NP * NF4 idle)
+    const int f = threadIdx.x % NF4, part = threadIdx.x / NF4;
+    float dzsum = 0.f, dzes = 0.f;
+    for (int s = 0; s < a.L; ++s) {
+        const int64_t first = ((int64_t)s * nrb + rbl) * nctH * NF4;
+        constexpr int SV = 12;
+        f32x4 sum = zero4();
+        for (int c0 = part; c0 < nctH; c0 += SV * NP) {
+            f32x4 v[SV];
+#pragma unroll
+            for (int u = 0; u < SV; ++u) {
+                const int ct = c0 + u * NP;
+                v[u] = ld4_sc1(bs, (part < NP && ct < nctH) ? (uint32_t)((first + (int64_t)ct * NF4 + f) * 16) : kOOB);
+            }
+#pragma unroll
+            for (int u = 0; u < SV; ++u) sum += v[u];
+        }
+        red[threadIdx.x] = sum;
+        __syncthreads();
+        float dz = 0.f;
+        if (j < Z) {
+            const int ff = (j * 16 + ml) >> 2, comp = ml & 3;
+            for (int pp = 0; pp < NP; ++pp) dz += red[pp * NF4 + ff][comp];
+        }
+        dz = valid ? dz : 0.f;
+        const float e = (s < kLP) ? epre[s] : (valid ? a.eps[((int64_t)s * a.Mbp + m) * Z + j] : 0.f);
+        dzsum += dz;
+        dzes += dz * e;
+        if (j < Z) a.dZ[((int64_t)s * a.Mbp + m) * Z + j] = dz;
+        __syncthreads();
+    }
+    VAEB_STAMP_AT(a, sid, 4);
+    if (j < Z) {
+        float dmu, dlv;
+        latent_bwd_elem(a, valid, m, j, mu, lv, epre, zpre, dzsum, dzes, dmu, dlv);
+        a.dMuLv[(int64_t)m * 2 * Z + j] = dmu;
+        a.dMuLv[(int64_t)m * 2 * Z + Z + j] = dlv;
+    }
+    VAEB_STAMP_AT(a, sid, 5);
+}
+
+// dhd (+ dZ slabs, latent backward) tiles and the dW2 (| dW6) weight-gradient tiles in one
+// grid.  The dhd tiles are dispatched first: with the latent backward behind them they are
+// the launch's critical path (tile_wgrad_kernel, without it, puts the dW2 blocks first).
+template <int NCT, int GCH, bool VEC, int TS>
+__global__ __launch_bounds__(512) void dhd_dz_wgrad_kernel(PDhdT<VEC> p, WGradArgs w, int ntile, int gx) {
+    __shared__ float sa[kWKB][kWP];
+    __shared__ float sb[kWKB][kWP];
+    const int nwg = (int)gridDim.x - ntile;
+    const int b0 = blockIdx.x;
+    const int bid = b0 < ntile ? xcd_remap(b0, ntile) : ntile + xcd_remap(b0 - ntile, nwg);
+    if (bid < ntile) {
+        dhd_dz_body<NCT, GCH, VEC>(p, bid % gx, bid / gx, reinterpret_cast<f32x4*>(&sa[0][0]), bid);
+        return;
+    }
+    if (w.dbg && threadIdx.x == 0) w.dbg[bid * 8 + 0] = __builtin_amdgcn_s_memrealtime();
+    wgrad_body<VEC, 8, TS>(w, w.g[0], bid, sa, sb);
+}
+
+}  // namespace vaeb

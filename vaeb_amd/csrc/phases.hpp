@@ -296,29 +296,41 @@ struct PDecOut {
 };
 
 // ----------------------------------------------------------------------------- P5
-struct PDhd {
+// [dA2 | dA6] and [W2 | W6] are each ONE allocation (dA6 = dA2 + dplane elements, W6 = W2 +
+// H D in the arena), so both K halves go through one buffer descriptor and a per-lane
+// offset select: the loaders are branch-free.  (With a descriptor chosen per K half in a
+// branch -- and the 16-byte form chosen at run time -- hipcc drained vmcnt inside every
+// chunk's branch, serialising the wave's eight chunk loads into eight round trips.)
+// V (host-chosen): D % 4 == 0 and 16-byte aligned dA2 / W2: one 16-byte load per operand.
+template <bool V>
+struct PDhdT {
     StepArgs a;
     int M, N, K;  // K = D (Bernoulli) or Dp + D (Gaussian: [dA2|dA6] . [W2|W6]^T, Dp = D rounded to 4)
     int Dp;
-    bool vw;
-    rsrc_t bd2, bd6, bw2, bw6;
+    int64_t dplane, wplane;   // elements from dA2 to dA6 / from W2 to W6 (0: Bernoulli)
+    rsrc_t bd, bw;
     DEV void prepare() {
         Dp = (a.D + 3) & ~3;
-        vw = (a.D & 3) == 0 && aligned16(a.W2) && (a.W6 == nullptr || aligned16(a.W6));
-        bd2 = mkbuf(a.dA2, (int64_t)a.Me * a.D * 4);
-        bd6 = mkbuf(a.dA6 ? a.dA6 : a.dA2, (int64_t)a.Me * a.D * 4);
-        bw2 = mkbuf(a.W2, (int64_t)a.H * a.D * 4);
-        bw6 = mkbuf(a.W6 ? a.W6 : a.W2, (int64_t)a.H * a.D * 4);
+        const bool gs = a.dec == DEC_GAUSSIAN;
+        dplane = gs ? (int64_t)(a.dA6 - a.dA2) : 0;
+        wplane = gs ? (int64_t)(a.W6 - a.W2) : 0;
+        bd = mkbuf(a.dA2, (dplane + (int64_t)a.Me * a.D) * 4);
+        bw = mkbuf(a.W2, (wplane + (int64_t)a.H * a.D) * 4);
     }
-    // k in [Dp, Dp + D) addresses the Gaussian half; chunks past K read zeros.
-    DEV f32x4 a4(int m, int k) const {
-        if (k < Dp) return kc4(bd2, a.D, m, k, a.Me, a.D, (a.D & 3) == 0);
-        return kc4(bd6, a.D, m, k - Dp, k < K ? a.Me : 0, a.D, (a.D & 3) == 0);
+    // element (r, k) of the K-concatenated operand: k in [Dp, Dp + D) is the Gaussian half
+    DEV f32x4 ld(rsrc_t b, int64_t plane, int r, int rlim, int k) const {
+        const bool hi = k >= Dp;
+        const int kk = hi ? k - Dp : k;
+        const uint32_t base = (uint32_t)((hi ? plane : 0) + (int64_t)r * a.D + kk) * 4u;
+        const bool rok = r < rlim && (!hi || plane != 0);
+        if (V) return bld4(b, (rok && kk < a.D) ? base : kOOB);
+        f32x4 v;
+#pragma unroll
+        for (int s = 0; s < 4; ++s) v[s] = bld(b, (rok && kk + s < a.D) ? base + 4u * s : kOOB);
+        return v;
     }
-    DEV f32x4 b4(int n, int k, int) const {
-        if (k < Dp) return kc4(bw2, a.D, n, k, a.H, a.D, vw);
-        return kc4(bw6, a.D, n, k - Dp, k < K ? a.H : 0, a.D, vw);
-    }
+    DEV f32x4 a4(int m, int k) const { return ld(bd, dplane, m, a.Me, k); }
+    DEV f32x4 b4(int n, int k, int) const { return ld(bw, wplane, n, a.H, k); }
     struct Pre { f32x4 hd; };
     DEV Pre prefetch(int m0, int n0) const {
         const int lane = threadIdx.x & 63;

@@ -35,6 +35,14 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
                 __builtin_amdgcn_s_memrealtime();                                         \
     } while (0)
 
+// ... at an explicit (logical) workgroup index, for fused grids whose parts stamp by
+// logical id so their slots do not collide.
+#define VAEB_STAMP_AT(A, idx, slot)                                                       \
+    do {                                                                                  \
+        if ((A).dbg && threadIdx.x == 0)                                                  \
+            (A).dbg[(uint64_t)(idx) * 8 + (slot)] = __builtin_amdgcn_s_memrealtime();     \
+    } while (0)
+
 // Diagnostics variant that first drains this wave's outstanding vector-memory operations,
 // so the stamp marks when its loads have actually landed (debug launches only).
 #define VAEB_STAMP_SYNC(A, slot)                                                          \

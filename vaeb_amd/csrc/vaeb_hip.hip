@@ -20,6 +20,7 @@
 #include "../../include/vaeb_diag.h"   // includes vaeb_hip.h
 #include "hfuse.hpp"
 #include "latent.hpp"
+#include "latent_bwd.hpp"
 #include "step_bf16.hpp"
 #include "ae_mlp.hpp"
 
@@ -82,7 +83,9 @@ const char* kKernelNames[] = {"p1_enc", "p2_heads", "p3_dechid", "p4_decout", "p
                               "bf_dz", "bf_dW1", "bf_dW1_opt", "bf_latent_bwd", "bf_dh", "bf_dW45", "bf_dW45_opt",
                               "bf_dW3", "bf_bias_elbo", "bf_adagrad_dp",
                               // weight-sampling full-variational extension, ids 35..38
-                              "unused35", "unused36", "fvs_sample", "fvs_update"};
+                              "unused35", "unused36", "fvs_sample", "fvs_update",
+                              // folded latent backward (latent_bwd.hpp), ids 39..40
+                              "p5_dhd_dz_w2", "p8_wgrad_w3w45w1"};
 
 }  // namespace
 
@@ -139,6 +142,8 @@ struct vaeb_ctx {
     hipEvent_t dp_ev[3] = {};     // fork after dW2, bucket A reduced, bucket A updated
     bool dp_overlap = false;      // bucket A on s2 (bf16 engine; VAEB_DP_OVERLAP=0/1 overrides)
     int dz_split = 8;             // P67 column splits per row block (fused.hpp dz_dh_body; VAEB_DZ_SPLIT)
+    bool fold_bwd = true;         // Z <= 32: latent backward folded into the dhd launch (VAEB_FOLD_BWD=0: P67)
+    int w3_ts = 1;                // folded path's last launch: tile width / 16 (VAEB_W3_TS)
     // profiling
     hipEvent_t pev[kMaxProfKernels + 1] = {};
     int prof_n = 0, prof_reps = 1;
@@ -351,6 +356,13 @@ OptArgs make_opt(vaeb_ctx* c, int par, bool update, bool store) {
     return o;
 }
 
+// 16-byte dhd operand loads (PDhdT<true>): D % 4 == 0 and 16-byte aligned dA2 / W2 (the
+// Gaussian halves dA6 / W6 then are too: they sit a multiple of 4 elements further).
+bool dhd_vec(const StepArgs& a) {
+    auto al = [](const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
+    return (a.D & 3) == 0 && al(a.dA2) && al(a.W2);
+}
+
 // Weight-gradient tile widths (columns; rows are kWT = 64).  Narrower tiles mean more
 // workgroups, each streaming fewer theta / accumulator / panel bytes through its CU: at
 // MNIST-20, 64 -> 32 wide took the dW2 launch 11.7 -> 9.5 us and the dW3 | dW45 launch
@@ -362,11 +374,13 @@ constexpr int kWTJ_W = 16;     // standalone launches: dW3 | dW45 (+ ELBO), non-
 
 // Weight-gradient arguments over `n` groups whose tiles start at block `base` of the
 // launch (+ the ELBO workgroup when e != nullptr).  *vec: 16-byte panel loads are legal.
+template <class WA>
 int prep_wgrad(vaeb_ctx* c, const WGroup* groups, int n, const OptArgs& opt, const ElboArgs* e, const StepArgs& a,
-               int base, WGradArgs& w, bool& vec, int tw) {
-    w = WGradArgs{};
+               int base, WA& w, bool& vec, int tw) {
+    w = WA{};
     int begin = base;
-    if (n < 1 || n > 2) return fail(VAEB_ERR_ARG, "internal: 1 or 2 weight-gradient groups per launch");
+    constexpr int kMaxG = (int)(sizeof(w.g) / sizeof(w.g[0]));
+    if (n < 1 || n > kMaxG) return fail(VAEB_ERR_ARG, "internal: 1 to %d weight-gradient groups per launch", kMaxG);
     for (int gi = 0; gi < n; ++gi) {
         w.g[gi] = groups[gi];
         WGroup& G = w.g[gi];
@@ -395,14 +409,32 @@ int prep_wgrad(vaeb_ctx* c, const WGroup* groups, int n, const OptArgs& opt, con
     return 0;
 }
 
-// A standalone weight-gradient launch (256-thread blocks).
+// A standalone weight-gradient launch (256-thread blocks).  da3: group 0 (dW3) forms its
+// dA3 panel from [dMu | dLv] in the workgroup (the folded latent backward).
 int launch_wgrad(vaeb_ctx* c, hipStream_t s, const WGroup* groups, int n, const OptArgs& opt, const ElboArgs* e,
-                 const StepArgs& a) {
-    WGradArgs w;
+                 const StepArgs& a, const Da3Src* da3 = nullptr) {
     bool vec;
-    if (int rc = prep_wgrad(c, groups, n, opt, e, a, 0, w, vec, kWTJ_W)) return rc;
-    if (vec) hipLaunchKernelGGL((wgrad_kernel<true, kWTJ_W / 16>), dim3(w.total_wgs + (e ? 1 : 0)), dim3(256), 0, s, w);
-    else hipLaunchKernelGGL((wgrad_kernel<false, kWTJ_W / 16>), dim3(w.total_wgs + (e ? 1 : 0)), dim3(256), 0, s, w);
+    if (da3) {
+        if (n != 3) return fail(VAEB_ERR_ARG, "internal: the dA3-forming launch takes three groups");
+        WGradArgs3 w;
+        const int tw = c->w3_ts * 16;
+        if (int rc = prep_wgrad(c, groups, n, opt, e, a, 0, w, vec, tw)) return rc;
+        w.da3 = *da3;
+        const dim3 grid(w.total_wgs + (e ? 1 : 0));
+        if (tw == 32) {
+            if (vec) hipLaunchKernelGGL((wgrad3_kernel<true, 2>), grid, dim3(256), 0, s, w);
+            else hipLaunchKernelGGL((wgrad3_kernel<false, 2>), grid, dim3(256), 0, s, w);
+        } else {
+            if (vec) hipLaunchKernelGGL((wgrad3_kernel<true, 1>), grid, dim3(256), 0, s, w);
+            else hipLaunchKernelGGL((wgrad3_kernel<false, 1>), grid, dim3(256), 0, s, w);
+        }
+    } else {
+        WGradArgs w;
+        if (int rc = prep_wgrad(c, groups, n, opt, e, a, 0, w, vec, kWTJ_W)) return rc;
+        const dim3 grid(w.total_wgs + (e ? 1 : 0));
+        if (vec) hipLaunchKernelGGL((wgrad_kernel<true, kWTJ_W / 16>), grid, dim3(256), 0, s, w);
+        else hipLaunchKernelGGL((wgrad_kernel<false, kWTJ_W / 16>), grid, dim3(256), 0, s, w);
+    }
     CHECK_LAUNCH();
     return 0;
 }
@@ -554,31 +586,70 @@ int enqueue_train_step(vaeb_ctx* c, int par, bool prof, bool fresh = true) {
         return 0;
     };
 
+    // folded latent backward (Z <= 32, latent_bwd.hpp): the dhd launch also finishes dZ and
+    // [dMu | dLv]; dA3 is formed inside the dW3 workgroups of the last launch (with dW1)
+    const bool fold = fused_latent(c) && c->fold_bwd;
     // P5 + dW2 (| dW6) = [hd|1]^T [dA2 (| dA6)] in one grid: both need only P4's outputs
     a.dbg = next_dbg(c);
-    {
+    if (fold) {
         WGroup g4 = make_group(c, c->hd, a.H, a.Me, 0, a.H, c->dA2, a.D, a.D, gs ? c->dA6 : nullptr, a.D, gs ? a.D : 0,
                                a.Me, 4, bo + 4, gs ? 5 : -1, gs ? bo + 5 : -1);
-        const PDhd p5{a, a.Me, a.H, gs ? ((a.D + 3) & ~3) + a.D : a.D};
+        const PDhdT<true> p5{a, a.Me, a.H, gs ? ((a.D + 3) & ~3) + a.D : a.D};
+        const PDhdT<false> p5s{a, a.Me, a.H, p5.K};
         const int gx = cdiv(p5.M, 16), ntile = gx * cdiv(p5.N, 16);
         WGradArgs w;
         bool vec;
         if (int rc = prep_wgrad(c, &g4, 1, opt, nullptr, a, ntile, w, vec, kWTJ_P5)) return rc;
+        // the dhd loaders' 16-byte form needs D % 4 == 0 and aligned dA2 / W2 too
+        vec = vec && dhd_vec(a);
+        const dim3 grid(w.total_wgs);
+        const bool deep = cdiv(cdiv(p5.K, 16), 8) > 4;
+        pr.mark(39);
+        REP(pr) {
+            if (a.Z <= 16) {
+                if (deep) {
+                    if (vec) hipLaunchKernelGGL((dhd_dz_wgrad_kernel<1, 8, true, kWTJ_P5 / 16>), grid, dim3(512), 0, s, p5, w, ntile, gx);
+                    else hipLaunchKernelGGL((dhd_dz_wgrad_kernel<1, 8, false, kWTJ_P5 / 16>), grid, dim3(512), 0, s, p5s, w, ntile, gx);
+                } else {
+                    if (vec) hipLaunchKernelGGL((dhd_dz_wgrad_kernel<1, 4, true, kWTJ_P5 / 16>), grid, dim3(512), 0, s, p5, w, ntile, gx);
+                    else hipLaunchKernelGGL((dhd_dz_wgrad_kernel<1, 4, false, kWTJ_P5 / 16>), grid, dim3(512), 0, s, p5s, w, ntile, gx);
+                }
+            } else {
+                if (deep) {
+                    if (vec) hipLaunchKernelGGL((dhd_dz_wgrad_kernel<2, 8, true, kWTJ_P5 / 16>), grid, dim3(512), 0, s, p5, w, ntile, gx);
+                    else hipLaunchKernelGGL((dhd_dz_wgrad_kernel<2, 8, false, kWTJ_P5 / 16>), grid, dim3(512), 0, s, p5s, w, ntile, gx);
+                } else {
+                    if (vec) hipLaunchKernelGGL((dhd_dz_wgrad_kernel<2, 4, true, kWTJ_P5 / 16>), grid, dim3(512), 0, s, p5, w, ntile, gx);
+                    else hipLaunchKernelGGL((dhd_dz_wgrad_kernel<2, 4, false, kWTJ_P5 / 16>), grid, dim3(512), 0, s, p5s, w, ntile, gx);
+                }
+            }
+        }
+        CHECK_LAUNCH();
+    } else {
+        WGroup g4 = make_group(c, c->hd, a.H, a.Me, 0, a.H, c->dA2, a.D, a.D, gs ? c->dA6 : nullptr, a.D, gs ? a.D : 0,
+                               a.Me, 4, bo + 4, gs ? 5 : -1, gs ? bo + 5 : -1);
+        const PDhdT<true> p5{a, a.Me, a.H, gs ? ((a.D + 3) & ~3) + a.D : a.D};
+        const PDhdT<false> p5s{a, a.Me, a.H, p5.K};
+        const int gx = cdiv(p5.M, 16), ntile = gx * cdiv(p5.N, 16);
+        WGradArgs w;
+        bool vec;
+        if (int rc = prep_wgrad(c, &g4, 1, opt, nullptr, a, ntile, w, vec, kWTJ_P5)) return rc;
+        vec = vec && dhd_vec(a);
         const dim3 grid(w.total_wgs);
         pr.mark(4);
         REP(pr) if (cdiv(cdiv(p5.K, 16), 8) <= 4) {
-            if (vec) hipLaunchKernelGGL((tile_wgrad_kernel<1, 1, 8, 1, 4, PDhd, true, kWTJ_P5 / 16>), grid, dim3(512), 0, s, p5, w, ntile, gx);
-            else hipLaunchKernelGGL((tile_wgrad_kernel<1, 1, 8, 1, 4, PDhd, false, kWTJ_P5 / 16>), grid, dim3(512), 0, s, p5, w, ntile, gx);
+            if (vec) hipLaunchKernelGGL((tile_wgrad_kernel<1, 1, 8, 1, 4, PDhdT<true>, true, kWTJ_P5 / 16>), grid, dim3(512), 0, s, p5, w, ntile, gx);
+            else hipLaunchKernelGGL((tile_wgrad_kernel<1, 1, 8, 1, 4, PDhdT<false>, false, kWTJ_P5 / 16>), grid, dim3(512), 0, s, p5s, w, ntile, gx);
         } else {
-            if (vec) hipLaunchKernelGGL((tile_wgrad_kernel<1, 1, 8, 1, 8, PDhd, true, kWTJ_P5 / 16>), grid, dim3(512), 0, s, p5, w, ntile, gx);
-            else hipLaunchKernelGGL((tile_wgrad_kernel<1, 1, 8, 1, 8, PDhd, false, kWTJ_P5 / 16>), grid, dim3(512), 0, s, p5, w, ntile, gx);
+            if (vec) hipLaunchKernelGGL((tile_wgrad_kernel<1, 1, 8, 1, 8, PDhdT<true>, true, kWTJ_P5 / 16>), grid, dim3(512), 0, s, p5, w, ntile, gx);
+            else hipLaunchKernelGGL((tile_wgrad_kernel<1, 1, 8, 1, 8, PDhdT<false>, false, kWTJ_P5 / 16>), grid, dim3(512), 0, s, p5s, w, ntile, gx);
         }
         CHECK_LAUNCH();
     }
     if (dp) if (int rc = dp_bucket_a(c, pr, dp_opt)) return rc;
     // P67 (+ dW1 = [z|1]^T dA1 on the fused path): both need only P5's output
-    a.dbg = next_dbg(c);
-    {
+    if (!fold) {
+        a.dbg = next_dbg(c);
         WGroup g3 = make_group(c, c->z, a.Z, a.Me, 0, a.Z, c->dA1, a.H, a.H, nullptr, 0, 0, a.Me, 3, bo + 3, -1, -1);
         if (fused_latent(c)) {
             const int nrow = a.Mbp / 16 * std::max(1, std::min(c->dz_split, cdiv(a.H, 16)));
@@ -608,17 +679,25 @@ int enqueue_train_step(vaeb_ctx* c, int par, bool prof, bool fresh = true) {
             CHECK_LAUNCH();
         }
     }
-    // dW3 = [X|1]^T dA3 and dW4|dW5 = [h|1]^T [dMu|dLv], plus the ELBO workgroup
+    // dW3 = [X|1]^T dA3 and dW4|dW5 = [h|1]^T [dMu|dLv] (+ dW1 = [z|1]^T dA1 when the latent
+    // backward is folded: dA3 is then formed in the dW3 workgroups), plus the ELBO workgroup
     {
-        WGroup g12[2] = {
+        WGroup g12[3] = {
             make_group(c, nullptr, a.D, a.Mb, 1, a.D, c->dA3, a.H, a.H, nullptr, 0, 0, a.Mbp, 0, bo + 0, -1, -1),
             make_group(c, c->h, a.H, a.Mbp, 0, a.H, c->dMuLv, 2 * a.Z, a.Z, c->dMuLv + a.Z, 2 * a.Z, a.Z, a.Mbp, 1,
-                       bo + 1, 2, bo + 2)};
+                       bo + 1, 2, bo + 2),
+            make_group(c, c->z, a.Z, a.Me, 0, a.Z, c->dA1, a.H, a.H, nullptr, 0, 0, a.Me, 3, bo + 3, -1, -1)};
         ElboArgs e1 = e;
         if (dp || fvs) { e1.dp_slot = c->grad + c->P; e1.elbo_out = nullptr; e1.cursor = nullptr; e1.step = nullptr; }
         a.dbg = next_dbg(c);
-        pr.mark(7);
-        REP(pr) if (int rc = launch_wgrad(c, s, g12, 2, opt, &e1, a)) return rc;
+        if (fold) {
+            const Da3Src d3{c->dMuLv, a.W4, a.W5, c->h, c->dA3, a.Z, a.H, a.Mb, a.Mbp};
+            pr.mark(40);
+            REP(pr) if (int rc = launch_wgrad(c, s, g12, 3, opt, &e1, a, &d3)) return rc;
+        } else {
+            pr.mark(7);
+            REP(pr) if (int rc = launch_wgrad(c, s, g12, 2, opt, &e1, a)) return rc;
+        }
     }
     if (fvs) {   // Adagrad on (mu_theta, sigma_theta), then the step's SGVB / B and cursor++
         pr.mark(38);
@@ -809,6 +888,8 @@ int vaeb_create(const vaeb_config* cfg, vaeb_ctx** out) {
     if (e != hipSuccess) { delete c; return fail(VAEB_ERR_HIP, "hipSetDevice(%d): %s", g.device, hipGetErrorString(e)); }
     e = hipStreamCreateWithFlags(&c->s, hipStreamNonBlocking);
     if (const char* ds = getenv("VAEB_DZ_SPLIT")) c->dz_split = atoi(ds);
+    if (const char* fb = getenv("VAEB_FOLD_BWD")) c->fold_bwd = atoi(fb) != 0;
+    if (const char* ts = getenv("VAEB_W3_TS")) c->w3_ts = atoi(ts) == 2 ? 2 : 1;
     if (e != hipSuccess) { delete c; return fail(VAEB_ERR_HIP, "stream/event create: %s", hipGetErrorString(e)); }
     const int64_t D = g.D, H = g.H, Z = g.Z;
     std::vector<int64_t> sz = {D * H, H * Z, H * Z, Z * H, H * D};
@@ -846,8 +927,9 @@ int vaeb_create(const vaeb_config* cfg, vaeb_ctx** out) {
     rc = rc ? rc : dalloc(&c->z, (size_t)RL * Z);
     rc = rc ? rc : dalloc(&c->hd, (size_t)RL * H);
     rc = rc ? rc : dalloc(&c->y, (size_t)RL * D);
-    rc = rc ? rc : dalloc(&c->dA2, (size_t)RL * D);
-    if (gaussian(c)) rc = rc ? rc : dalloc(&c->dA6, (size_t)RL * D);
+    // dA6 directly after dA2: the dhd loaders address both through one descriptor (PDhdT)
+    rc = rc ? rc : dalloc(&c->dA2, (size_t)RL * D * (gaussian(c) ? 2 : 1));
+    if (!rc && gaussian(c)) c->dA6 = c->dA2 + (size_t)RL * D;
     rc = rc ? rc : dalloc(&c->dA1, (size_t)RL * H);
     rc = rc ? rc : dalloc(&c->dZ, (size_t)RL * Z);
     rc = rc ? rc : dalloc(&c->dMuLv, (size_t)R * 2 * Z);
@@ -885,7 +967,7 @@ int vaeb_destroy(vaeb_ctx* c) {
     bf_free(c);
     if (c->comm) ncclCommDestroy(c->comm);
     float* fp[] = {c->theta2[0], c->theta2[1], c->acc, c->grad, c->fvmu, c->fvsg, c->fvam, c->fvas, c->fv_part, c->data, c->xeval, c->xval,
-                   c->elbo_out, c->eps_in, c->h, c->mu, c->lv, c->eps, c->z, c->hd, c->y, c->dA2, c->dA6, c->dA1,
+                   c->elbo_out, c->eps_in, c->h, c->mu, c->lv, c->eps, c->z, c->hd, c->y, c->dA2, c->dA1,   // dA6 lives in dA2's block
                    c->dZ, c->dMuLv, c->dA3, c->kl_part, c->lp_part, c->slab_ml, c->slab_dz, c->yacc,
                    c->fvzeta};
     for (float* p : fp) if (p) hipFree(p);
