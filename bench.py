@@ -71,6 +71,11 @@ def phase_flops(D, H, Z, B, L=1, gaussian=False):
         "bf_dh": 2 * B * 2 * Z * H,
         "bf_dW45": 2 * B * H * 2 * Z,
         "bf_dW3": 2 * B * D * H,
+        "bf_dhd_dW26": 2 * L * B * D * g * H + 2 * L * B * H * D * g,   # one grid (gemm2_kernel)
+        # folded latent backward (latent_bwd.hpp): dhd + dZ slabs + latent backward | dW2; the
+        # last launch dW3 (dA3 formed in-workgroup) | dW45 | dW1
+        "p5_dhd_dz_w2": 2 * L * B * D * H * g + 2 * L * B * H * Z + 2 * L * B * H * D * g,
+        "p8_wgrad_w3w45w1": 2 * B * (D * H + H * 2 * Z) + 2 * B * 2 * Z * H + 2 * L * B * Z * H,
     }
 
 
@@ -92,7 +97,8 @@ KERNEL_SYMBOLS = {"p1_enc": "PEnc", "p23_heads_dechid": "heads_dechid_kernel", "
                   # (all listed substrings must appear: the tile width is a template argument)
                   "bf_enc": ("gemm_kernel<0, 1,", "EpiBiasAct>"), "bf_decout": ("EpiDecOut<false>",),
                   "bf_dhd": ("gemm_kernel<0, 0,", "EpiDTanh>"), "bf_dW26": ("EpiAdagrad",),
-                  "bf_dW3": ("EpiAdagrad",)}
+                  "bf_dW3": ("EpiAdagrad",), "bf_dhd_dW26": ("gemm2_kernel",),
+                  "p5_dhd_dz_w2": "vaeb::dhd_dz_wgrad_kernel", "p8_wgrad_w3w45w1": "vaeb::wgrad3_kernel"}
 PMC_FILES = {"mnist": os.path.join(ROOT, "profiles", "r1", "pmc_per_launch.json"),
              "frey": os.path.join(ROOT, "profiles", "r1", "pmc_frey_per_launch.json"),
              "fv": os.path.join(ROOT, "profiles", "r1", "pmc_fv_per_launch.json"),

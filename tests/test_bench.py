@@ -29,6 +29,16 @@ def test_fused_launch_flops_sum_to_step():
         assert sum(fl[k] for k in parts) == bench.step_flops(784, 500, 20, 100, gaussian=gauss)
 
 
+def test_folded_launch_flops_sum_to_step():
+    """The folded latent backward's four launches (latent.hpp, latent_bwd.hpp) cover the step."""
+    for gauss in (False, True):
+        fl = bench.phase_flops(784, 500, 20, 100, gaussian=gauss)
+        parts = ["p1_enc_latent", "p4_decout_z", "p5_dhd_dz_w2", "p8_wgrad_w3w45w1"]
+        assert sum(fl[k] for k in parts) == bench.step_flops(784, 500, 20, 100, gaussian=gauss)
+    fl = bench.phase_flops(4096, 2048, 128, 8192)
+    assert fl["bf_dhd_dW26"] == fl["bf_dhd"] + fl["bf_dW26"]
+
+
 def test_bf16_launch_flops_sum_to_step():
     fl = bench.phase_flops(4096, 2048, 128, 8192)
     parts = ["bf_enc", "bf_heads", "bf_dechid", "bf_decout", "bf_dhd", "bf_dW26", "bf_dz", "bf_dW1", "bf_dh",

@@ -13,14 +13,19 @@
 //    the forward (X W3), the data-gradient (dA2 W2^T) and the weight-gradient
 //    (X^T dA3) products all read the same single copy of each weight / activation and
 //    no transposed copies are ever written;
-//  * 128 x 128 x 64 block tile, 256 threads = 4 waves (2 x 2), 64 x 64 per wave
-//    (4 x 4 MFMA tiles, 64 accumulator VGPRs), register-staged double buffer
-//    (next tile's global loads issued before this tile's MFMAs, written to the other
-//    LDS buffer after them: one barrier per K tile), 64 KiB LDS, 2 blocks per CU;
-//  * LDS images are XOR-swizzled so the fragment reads are bank-conflict free:
-//    KC (128-B rows): 16-B chunk c of row r at c ^ ((r >> 1) & 7)  (ds_read_b128 lane
-//    groups of MI355X_MICROARCH.md §LDS);  KO (256-B k-rows): chunk c of k-row r at
-//    c ^ (((r & 3) << 1) | (((r >> 3) & 1) << 3))  (ds_read_b64_tr_b16 32-lane halves);
+//  * block tile 256 x BNT x 32 (BK), 512 threads = 8 waves: BNT = 256 (waves 2 x 4,
+//    128 x 64 each) or BNT = 128 for products with too few 256-wide tiles to fill the chip
+//    (waves 4 x 2, 64 x 64 each); one block per CU;
+//  * operand tiles reach LDS by LDS-DMA (buffer_load_dwordx4 ... lds, inline asm) into a
+//    4-stage ring, prefetch distance 3, with counted s_waitcnt vmcnt(N) (never 0 inside the
+//    loop); on the 256 x 256 tile waves 4-7 run one barrier behind waves 0-3 (wave-group
+//    ping-pong: one reads fragments while its SIMD partner issues MFMAs);
+//  * LDS images are XOR-swizzled so the fragment reads are bank-conflict free, the
+//    swizzle applied to the DMA SOURCE chunk (the DMA writes each 1-KiB piece linearly):
+//    KC (64-B rows): 16-B chunk c of row r at c ^ g[(r >> 2) & 3], g = {0, 2, 3, 1}
+//    (ds_read_b128 lane groups of MI355X_MICROARCH.md §LDS); KO (2 BNT-byte k-rows):
+//    chunk c of k-row r at c ^ (((r & 3) << 1) | (((r >> 3) & 1) << 3))
+//    (ds_read_b64_tr_b16 32-lane halves);
 //  * operand loads are 16-B raw buffer loads; a chunk outside [0, rows) x [0, K) is
 //    redirected out of range and reads 0 (tails need rows and K to be multiples of 8);
 //  * split-K over gridDim.y for the thin products (latent-width N or M): each slice
@@ -28,7 +33,8 @@
 //  * tile order: the linear block id is remapped so that the blocks sharing one XCD
 //    (blockIdx % 8, guide T1) take a contiguous run of tiles, grouped 8 row tiles at a
 //    time so concurrently running blocks share operand panels in that XCD's L2.
-// Epilogues are functors applied to the wave's 64 x 64 accumulator block in registers.
+// Epilogues are functors applied to the wave's accumulator block (128 x 64 or 64 x 64) in
+// registers.
 #pragma once
 #include "tile_engine.hpp"
 
@@ -76,11 +82,11 @@ DEV float bf2f(uint32_t b) { return __builtin_bit_cast(float, b << 16); }
 DEV int swz_kc(int r) { return (0x78 >> (((r >> 2) & 3) * 2)) & 3; }   // g = {0, 2, 3, 1}
 DEV int swz_ko(int r) { return ((r & 3) << 1) | (((r >> 3) & 1) << 3); }
 
-// One R-row x 64-k operand tile, HBM -> LDS directly (buffer_load_dwordx4 ... lds): each
-// wave-instruction writes 1 KiB of the tile image linearly (lane l at byte 16 l), so the
-// XOR swizzle is applied to the SOURCE chunk each lane fetches (guide rule 21): the lane
-// that fills physical chunk p of a row loads logical chunk p ^ swz(row).  KC image:
-// [R rows][64 k] (128-B rows); KO image: [64 k-rows][R] (2R-byte rows).  Out-of-range
+// One R-row x 32-k (BK) operand tile, HBM -> LDS directly (buffer_load_dwordx4 ... lds):
+// each wave-instruction writes 1 KiB of the tile image linearly (lane l at byte 16 l), so
+// the XOR swizzle is applied to the SOURCE chunk each lane fetches (guide rule 21): the
+// lane that fills physical chunk p of a row loads logical chunk p ^ swz(row).  KC image:
+// [R rows][32 k] (64-B rows); KO image: [32 k-rows][R] (2R-byte rows).  Out-of-range
 // chunks are redirected past the buffer end and land as zeros.
 typedef int v4i __attribute__((ext_vector_type(4)));
 // Buffer descriptor as four SGPRs (base, stride 0, num_records, raw-buffer flags).
@@ -178,11 +184,11 @@ struct GemmArgs {
 };
 
 // Bijective XCD-contiguous remap of the linear tile id (guide §5 template), then a
-// grouped order: runs of GM row tiles sweep all column tiles.
-DEV void tile_of(const GemmArgs& g, int& tm, int& tn) {
+// grouped order: runs of GM row tiles sweep all column tiles.  b: the block's index within
+// this product's blocks (blockIdx.x, or its offset inside a two-product grid).
+DEV void tile_of(const GemmArgs& g, int b, int& tm, int& tn) {
     constexpr int GM = 8;
     const int nwg = g.tiles_m * g.tiles_n;
-    const int b = blockIdx.x;
     int t = b;
     if (nwg >= 16) {
         const int xcd = b & 7, q = nwg >> 3, r = nwg & 7;
@@ -211,15 +217,14 @@ DEV void ring_wait(int after) {   // wait for all but `after` tiles' worth of LD
     asm volatile("" ::: "memory");
 }
 
+// One block tile (block `bid` of the product, K slice kz) of C = A B with epilogue e.
 template <int LA, int LB, int BNT, class Epi>
-__global__ __launch_bounds__(NTHR, 2 * Shape<BNT>::kBlocksPerCU) void gemm_kernel(GemmArgs g, Epi e) {
+DEV void gemm_body(const GemmArgs& g, const Epi& e, int bid, int kz, char* smem) {
     using S = Shape<BNT>;
     constexpr int TM = S::TM, TN = S::TN;
-    extern __shared__ __attribute__((aligned(16))) char smem[];
     int tm, tn;
-    tile_of(g, tm, tn);
+    tile_of(g, bid, tm, tn);
     const int m0 = tm * BM, n0 = tn * BNT;
-    const int kz = blockIdx.y;
     const int kbeg = kz * g.kslice;
     const int kend = min(g.K, kbeg + g.kslice);
     const int lane = threadIdx.x & 63;
@@ -326,6 +331,31 @@ __global__ __launch_bounds__(NTHR, 2 * Shape<BNT>::kBlocksPerCU) void gemm_kerne
         __syncthreads();
         e.template store_out<BNT>(m0, n0, smem);
     }
+}
+
+template <int LA, int LB, int BNT, class Epi>
+__global__ __launch_bounds__(NTHR, 2 * Shape<BNT>::kBlocksPerCU) void gemm_kernel(GemmArgs g, Epi e) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    gemm_body<LA, LB, BNT, Epi>(g, e, blockIdx.x, blockIdx.y, smem);
+}
+
+// Two independent products in one grid (no split-K): blocks [0, nb1) run product 1, the
+// rest product 2.  Used where a product with too few 256 x 256 tiles to fill the chip
+// (the weight gradient dW2 | dW6: 128 tiles at config 5, each twice as deep as the other
+// product's) can share the launch with a product that needs only the same inputs (dhd:
+// 256 tiles): product 1's blocks are dispatched first and each CU then holds one product-1
+// tile or two product-2 tiles in sequence (config 5: 270 us against 112 + 174 us as two
+// launches).  Measured and rejected: product 1 as a two-slice split-K combined in the
+// launch (slice-1 blocks waiting on a flag for their slice-0 partner's fp32 partial) --
+// 299 us, and dW3 the same way 169 vs 160 us: the partial slabs' write-through traffic
+// and the longer epilogue tail cost more than the balanced grid saved.
+template <int LA1, int LB1, class E1, int LA2, int LB2, class E2, int BNT>
+__global__ __launch_bounds__(NTHR, 2 * Shape<BNT>::kBlocksPerCU) void gemm2_kernel(GemmArgs g1, E1 e1, GemmArgs g2,
+                                                                                  E2 e2, int nb1) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int b = blockIdx.x;
+    if (b < nb1) gemm_body<LA1, LB1, BNT, E1>(g1, e1, b, 0, smem);
+    else gemm_body<LA2, LB2, BNT, E2>(g2, e2, b - nb1, 0, smem);
 }
 
 // ------------------------------------------------------------------ helpers

@@ -85,7 +85,9 @@ const char* kKernelNames[] = {"p1_enc", "p2_heads", "p3_dechid", "p4_decout", "p
                               // weight-sampling full-variational extension, ids 35..38
                               "unused35", "unused36", "fvs_sample", "fvs_update",
                               // folded latent backward (latent_bwd.hpp), ids 39..40
-                              "p5_dhd_dz_w2", "p8_wgrad_w3w45w1"};
+                              "p5_dhd_dz_w2", "p8_wgrad_w3w45w1",
+                              // bf16 engine: dhd and dW2 (| dW6) in one grid, id 41
+                              "bf_dhd_dW26"};
 
 }  // namespace
 
@@ -144,6 +146,8 @@ struct vaeb_ctx {
     int dz_split = 8;             // P67 column splits per row block (fused.hpp dz_dh_body; VAEB_DZ_SPLIT)
     bool fold_bwd = true;         // Z <= 32: latent backward folded into the dhd launch (VAEB_FOLD_BWD=0: P67)
     int w3_ts = 1;                // folded path's last launch: tile width / 16 (VAEB_W3_TS)
+    bool bf_fuse = true;          // bf16 engine: dhd + dW2 (| dW6) in one grid (VAEB_BF_FUSE=0: two launches)
+    int num_cus = 256;            // compute units of the device (hipDeviceProp_t)
     // profiling
     hipEvent_t pev[kMaxProfKernels + 1] = {};
     int prof_n = 0, prof_reps = 1;
@@ -886,10 +890,16 @@ int vaeb_create(const vaeb_config* cfg, vaeb_ctx** out) {
     if (c->c.max_eval_rows <= 0) c->c.max_eval_rows = 10000;
     hipError_t e = hipSetDevice(g.device);
     if (e != hipSuccess) { delete c; return fail(VAEB_ERR_HIP, "hipSetDevice(%d): %s", g.device, hipGetErrorString(e)); }
+    {
+        hipDeviceProp_t prop;
+        if (hipGetDeviceProperties(&prop, g.device) == hipSuccess && prop.multiProcessorCount > 0)
+            c->num_cus = prop.multiProcessorCount;
+    }
     e = hipStreamCreateWithFlags(&c->s, hipStreamNonBlocking);
     if (const char* ds = getenv("VAEB_DZ_SPLIT")) c->dz_split = atoi(ds);
     if (const char* fb = getenv("VAEB_FOLD_BWD")) c->fold_bwd = atoi(fb) != 0;
     if (const char* ts = getenv("VAEB_W3_TS")) c->w3_ts = atoi(ts) == 2 ? 2 : 1;
+    if (const char* bf = getenv("VAEB_BF_FUSE")) c->bf_fuse = atoi(bf) != 0;
     if (e != hipSuccess) { delete c; return fail(VAEB_ERR_HIP, "stream/event create: %s", hipGetErrorString(e)); }
     const int64_t D = g.D, H = g.H, Z = g.Z;
     std::vector<int64_t> sz = {D * H, H * Z, H * Z, Z * H, H * D};
