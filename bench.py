@@ -99,11 +99,8 @@ KERNEL_SYMBOLS = {"p1_enc": "PEnc", "p23_heads_dechid": "heads_dechid_kernel", "
                   "bf_dhd": ("gemm_kernel<0, 0,", "EpiDTanh>"), "bf_dW26": ("EpiAdagrad",),
                   "bf_dW3": ("EpiAdagrad",), "bf_dhd_dW26": ("gemm2_kernel",),
                   "p5_dhd_dz_w2": "vaeb::dhd_dz_wgrad_kernel", "p8_wgrad_w3w45w1": "vaeb::wgrad3_kernel"}
-PMC_FILES = {"mnist": os.path.join(ROOT, "profiles", "r1", "pmc_per_launch.json"),
-             "frey": os.path.join(ROOT, "profiles", "r1", "pmc_frey_per_launch.json"),
-             "fv": os.path.join(ROOT, "profiles", "r1", "pmc_fv_per_launch.json"),
-             "fvs": os.path.join(ROOT, "profiles", "r1", "pmc_fvs_per_launch.json"),
-             "synth": os.path.join(ROOT, "profiles", "r1", "pmc_synth_per_launch.json")}
+PMC_FILES = {c: os.path.join(ROOT, "profiles", "r2", f"pmc_{c}_per_launch.json")
+             for c in ("mnist", "frey", "fv", "fvs", "synth")}
 
 
 def committed_traffic(kernel, path=PMC_FILES["mnist"], symbols=KERNEL_SYMBOLS):
@@ -171,10 +168,15 @@ def cpu_baseline_pair(fn, budget_s, single_kw=None, **kw):
     finally:
         if ctx1 is not None and hasattr(ctx1, "unregister"):
             ctx1.unregister()
-    return {"value": imgs / dt, "unit": "images/s", "cores": threads, "kind": "port",
-            "single_thread_value": imgs1 / dt1, "nproc": nproc, "cpu_model": model,
+    multi, single = imgs / dt, imgs1 / dt1
+    # the faster of the two is the baseline (at B = 100 the threaded BLAS can lose to one
+    # thread); both figures are kept
+    best_threads, best = (threads, multi) if multi >= single else (1, single)
+    return {"value": best, "unit": "images/s", "cores": best_threads, "kind": "port",
+            "threaded_value": multi, "threads": threads, "single_thread_value": single,
+            "nproc": nproc, "cpu_model": model,
             "sample": f"{n} {what} in {dt:.1f} s on {threads} OpenBLAS threads (job share of {nproc} CPUs, {model}); "
-                      f"1 thread: {n1} steps in {dt1:.1f} s"}
+                      f"1 thread: {n1} steps in {dt1:.1f} s; value = the faster"}
 
 
 def cpu_baseline(D, H, Z, B, x, budget_s=10.0, max_steps=20000, continuous=False, warm=3, single_kw=None):

@@ -6,7 +6,7 @@ set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 for cfg in mnist frey synth; do
-  O=gpurun_out/mfma/$cfg
+  O=gpurun_out/mfma2/$cfg
   mkdir -p $O
   if [ $cfg = synth ]; then P="--steps 10 --warmup 2"; else P="--steps 200 --warmup 20"; fi
   timeout -s KILL 200 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_MFMA SQ_BUSY_CYCLES SQ_WAVES GRBM_GUI_ACTIVE --output-format csv -d $O/p1 -o run -- python3 bench.py --config $cfg $P --no-cpu-baseline > /dev/null 2> $O/p1.err || { tail $O/p1.err; exit 1; }
