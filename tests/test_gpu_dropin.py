@@ -224,3 +224,38 @@ def test_fv_literal_step_mnist20():
     assert np.abs(gs - O.flatten(s64)).max() <= 1e-7
     assert np.array_equal(ctx.get_params(), flat)
     ctx.close()
+
+
+@pytest.mark.parametrize("scaling", ["weak", "strong"])
+def test_two_rank_decomposition_on_the_hip_path(scaling):
+    """The data-parallel decomposition with the real kernels, on one GPU: two contexts play
+    ranks 0 and 1 of a world of 2 (the RCCL all-reduce itself needs one GPU per rank).  The
+    SUM of their data gradients and SGVB values equals one context's on the whole global
+    minibatch (VAEB.py:340-344: the objective is a sum over rows); Philox noise is keyed by
+    the global row, so the ranks draw the single context's eps."""
+    from vaeb_amd import _lib
+    from vaeb_amd.dp import row_split
+    cfg = O.Config(D=784, H=500, Z=20)
+    Bg = 100 if scaling == "strong" else 200
+    x = O.synthetic_mnist(n=4 * Bg)
+    theta = O.flatten(O.init_params(cfg))
+
+    def run(B, off, B_global):
+        c = _lib.Context(784, 500, 20, B, B_global=B_global, row_offset=off, keep_grads=True, max_eval_rows=100)
+        c.comm_init(_lib.Context.comm_unique_id(), 0, 1)   # the DP path: gradients stored, then reduced
+        c.set_data(x)
+        c.set_params(theta)
+        c.set_eps_mode(_lib.EPS_PHILOX, 10)
+        c.set_step(3)
+        e = c.update(2)
+        g = c.get_grads()
+        c.close()
+        return e, g
+
+    full_e, full_g = run(Bg, 0, Bg)
+    parts = [run(*row_split(Bg if scaling == "strong" else Bg // 2, 2, r, scaling)) for r in range(2)]
+    # ELBO per row of the global batch: each rank reports its local SGVB / B_global
+    assert abs(sum(p[0] for p in parts) - full_e) <= 1e-5 * abs(full_e)
+    gsum = parts[0][1] + parts[1][1]
+    for (n, s), a, b in zip(O.param_shapes(cfg), O.unflatten(gsum, cfg), O.unflatten(full_g, cfg)):
+        assert rel(a, b) <= 1e-5, n
