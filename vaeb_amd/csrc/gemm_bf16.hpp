@@ -54,19 +54,20 @@ enum : int { KC = 0, KO = 1 };
 // chip).  BN is the widest tile (it sizes the epilogue LDS tile).
 constexpr int BM = 256, BN = 256, BK = 32, NTHR = 512, NWAVE = 8;
 constexpr int kATileBytes = BM * BK * 2;         // A operand tile image (16 KiB)
-template <int BNT>
+template <int BNT, int ST = 4>
 struct Shape {
     static constexpr int WGN = BNT / 64, WGM = NWAVE / WGN;   // wave grid
     static constexpr int TM = BM / WGM / 16, TN = 4;          // MFMA tiles per wave
     static constexpr int kB = BNT * BK * 2;                   // B operand tile image
     static constexpr int kStage = kATileBytes + kB;
     static constexpr int kPieces = (kATileBytes + kB) / 1024 / NWAVE;   // vmcnt unit per tile
-    // LDS ring: 4 stages (prefetch distance 3), one block per CU.  Measured and rejected:
-    // a 3-stage ring on the 256 x 128 tile (72 KiB with its epilogue tile, <= 128 VGPRs,
-    // two blocks per CU so one block's epilogue overlaps the other's mainloop) -- the
-    // weight-gradient launches went from 161-169 to 171-183 us.
-    static constexpr int kStages = 4;
-    static constexpr int kBlocksPerCU = 1;
+    // LDS ring: 4 stages (prefetch distance 3), one block per CU; or (ST = 3, 256 x 128
+    // only) 3 stages, 72 KiB with its epilogue tile, <= 128 VGPRs, two blocks per CU so
+    // one block's epilogue overlaps the other's mainloop.  The weight-gradient launches
+    // measured 171-183 us that way against 161-169 us with one block per CU.
+    static_assert(ST == 4 || (ST == 3 && BNT == 128), "ring shape");
+    static constexpr int kStages = ST;
+    static constexpr int kBlocksPerCU = ST == 3 ? 2 : 1;
 };
 
 // f32 -> bf16, round to nearest even (inputs here are finite)
@@ -218,9 +219,9 @@ DEV void ring_wait(int after) {   // wait for all but `after` tiles' worth of LD
 }
 
 // One block tile (block `bid` of the product, K slice kz) of C = A B with epilogue e.
-template <int LA, int LB, int BNT, class Epi>
+template <int LA, int LB, int BNT, class Epi, int ST = 4>
 DEV void gemm_body(const GemmArgs& g, const Epi& e, int bid, int kz, char* smem) {
-    using S = Shape<BNT>;
+    using S = Shape<BNT, ST>;
     constexpr int TM = S::TM, TN = S::TN;
     int tm, tn;
     tile_of(g, bid, tm, tn);
@@ -333,10 +334,10 @@ DEV void gemm_body(const GemmArgs& g, const Epi& e, int bid, int kz, char* smem)
     }
 }
 
-template <int LA, int LB, int BNT, class Epi>
-__global__ __launch_bounds__(NTHR, 2 * Shape<BNT>::kBlocksPerCU) void gemm_kernel(GemmArgs g, Epi e) {
+template <int LA, int LB, int BNT, class Epi, int ST = 4>
+__global__ __launch_bounds__(NTHR, (2 * Shape<BNT, ST>::kBlocksPerCU)) void gemm_kernel(GemmArgs g, Epi e) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    gemm_body<LA, LB, BNT, Epi>(g, e, blockIdx.x, blockIdx.y, smem);
+    gemm_body<LA, LB, BNT, Epi, ST>(g, e, blockIdx.x, blockIdx.y, smem);
 }
 
 // Two independent products in one grid (no split-K): blocks [0, nb1) run product 1, the
@@ -377,9 +378,9 @@ DEV float colsum_lanes(float s) {
 // (544 or 288 B, 8 (mod 32) dwords): the four 16-lane groups of a per-element access
 // (rows 4(l>>4)+r, 16 consecutive columns) land on disjoint banks.
 template <int W> constexpr int epitch() { return W * 2 + 32; }
-template <int BNT>
+template <int BNT, int ST = 4>
 constexpr int lds_bytes() {
-    constexpr int ring = Shape<BNT>::kStages * Shape<BNT>::kStage, epi = BM * epitch<BNT>();
+    constexpr int ring = Shape<BNT, ST>::kStages * Shape<BNT, ST>::kStage, epi = BM * epitch<BNT>();
     return ring > epi ? ring : epi;   // 128 KiB / 136 KiB at 256 wide, 72 KiB at 128
 }
 template <int W> DEV int eoff(int row, int col) { return row * epitch<W>() + col * 2; }
@@ -568,6 +569,7 @@ struct EpiDecOut {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             float rs[4] = {0.f, 0.f, 0.f, 0.f};
+            float pd[4] = {1.f, 1.f, 1.f, 1.f};   // Bernoulli: prod_j (1 + e^-|a|), one log per row
 #pragma unroll
             for (int j = 0; j < JN; ++j)
 #pragma unroll
@@ -578,9 +580,13 @@ struct EpiDecOut {
                     const float a2 = acc[i][j][r] + bb2[j];
                     float y, lpv, g2, g6 = 0.f;
                     if constexpr (!GAUSS) {
-                        float sp;
-                        sigmoid_softplus(a2, y, sp);
-                        lpv = xv * a2 - sp;
+                        // log p = x a - softplus(a) = x a - max(a, 0) - log(1 + e^-|a|): the
+                        // logs of a row's JN elements are taken once, of their product (<= 2^JN)
+                        const float t = fexp(-fabsf(a2));
+                        const float dd = 1.f + t, rc = frcp(dd);
+                        y = a2 >= 0.f ? rc : t * rc;
+                        lpv = xv * a2 - fmaxf(a2, 0.f);
+                        pd[r] *= ok ? dd : 1.f;
                         g2 = sl * (xv - y);
                     } else {
                         y = sigmoidf(a2);
@@ -604,6 +610,7 @@ struct EpiDecOut {
             if (nw < N) {
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
+                    if constexpr (!GAUSS) rs[r] -= flog(pd[r]);
                     const float sr = sum16(rs[r]);
                     const int row = erow(mw, i, r, lane);
                     if ((lane & 15) == 0 && row < M) lp[(int64_t)row * nlp + (nw >> 6)] = sr;

@@ -146,6 +146,7 @@ struct vaeb_ctx {
     int dz_split = 8;             // P67 column splits per row block (fused.hpp dz_dh_body; VAEB_DZ_SPLIT)
     bool fold_bwd = true;         // Z <= 32: latent backward folded into the dhd launch (VAEB_FOLD_BWD=0: P67)
     int w3_ts = 1;                // folded path's last launch: tile width / 16 (VAEB_W3_TS)
+    bool decout_2b = true;        // bf16 Bernoulli decout on 256 x 128 tiles, 2 blocks / CU (VAEB_DECOUT_2B=0: 256 x 256)
     bool bf_fuse = true;          // bf16 engine: dhd + dW2 (| dW6) in one grid (VAEB_BF_FUSE=0: two launches)
     int num_cus = 256;            // compute units of the device (hipDeviceProp_t)
     // profiling
@@ -900,6 +901,7 @@ int vaeb_create(const vaeb_config* cfg, vaeb_ctx** out) {
     if (const char* fb = getenv("VAEB_FOLD_BWD")) c->fold_bwd = atoi(fb) != 0;
     if (const char* ts = getenv("VAEB_W3_TS")) c->w3_ts = atoi(ts) == 2 ? 2 : 1;
     if (const char* bf = getenv("VAEB_BF_FUSE")) c->bf_fuse = atoi(bf) != 0;
+    if (const char* d2 = getenv("VAEB_DECOUT_2B")) c->decout_2b = atoi(d2) != 0;
     if (e != hipSuccess) { delete c; return fail(VAEB_ERR_HIP, "stream/event create: %s", hipGetErrorString(e)); }
     const int64_t D = g.D, H = g.H, Z = g.Z;
     std::vector<int64_t> sz = {D * H, H * Z, H * Z, Z * H, H * D};
