@@ -226,22 +226,28 @@ def test_fv_literal_step_mnist20():
     ctx.close()
 
 
+@pytest.mark.parametrize("engine", ["f32", "bf16"])
 @pytest.mark.parametrize("scaling", ["weak", "strong"])
-def test_two_rank_decomposition_on_the_hip_path(scaling):
+def test_two_rank_decomposition_on_the_hip_path(scaling, engine):
     """The data-parallel decomposition with the real kernels, on one GPU: two contexts play
     ranks 0 and 1 of a world of 2 (the RCCL all-reduce itself needs one GPU per rank).  The
     SUM of their data gradients and SGVB values equals one context's on the whole global
     minibatch (VAEB.py:340-344: the objective is a sum over rows); Philox noise is keyed by
-    the global row, so the ranks draw the single context's eps."""
+    the global row, so the ranks draw the single context's eps.  fp32 engine at MNIST
+    784-500-20 (1e-5: only the accumulation order differs); bf16 engine at 256-128-32 (1e-3:
+    its split-K slab counts depend on the rows per rank, so a few bf16 roundings differ)."""
     from vaeb_amd import _lib
     from vaeb_amd.dp import row_split
-    cfg = O.Config(D=784, H=500, Z=20)
-    Bg = 100 if scaling == "strong" else 200
-    x = O.synthetic_mnist(n=4 * Bg)
+    bf = engine == "bf16"
+    cfg = O.Config(D=256, H=128, Z=32) if bf else O.Config(D=784, H=500, Z=20)
+    Bg = (256 if bf else 100) * (2 if scaling == "weak" else 1)
+    x = O.synthetic_mnist(n=4 * Bg, D=cfg.D)
     theta = O.flatten(O.init_params(cfg))
+    tol = 1e-3 if bf else 1e-5
 
     def run(B, off, B_global):
-        c = _lib.Context(784, 500, 20, B, B_global=B_global, row_offset=off, keep_grads=True, max_eval_rows=100)
+        c = _lib.Context(cfg.D, cfg.H, cfg.Z, B, B_global=B_global, row_offset=off, keep_grads=True,
+                         max_eval_rows=B, dtype=_lib.DTYPE_BF16 if bf else _lib.DTYPE_F32)
         c.comm_init(_lib.Context.comm_unique_id(), 0, 1)   # the DP path: gradients stored, then reduced
         c.set_data(x)
         c.set_params(theta)
@@ -254,8 +260,8 @@ def test_two_rank_decomposition_on_the_hip_path(scaling):
 
     full_e, full_g = run(Bg, 0, Bg)
     parts = [run(*row_split(Bg if scaling == "strong" else Bg // 2, 2, r, scaling)) for r in range(2)]
-    # ELBO per row of the global batch: each rank reports its local SGVB / B_global
-    assert abs(sum(p[0] for p in parts) - full_e) <= 1e-5 * abs(full_e)
+    # each rank reports its local SGVB / B_global
+    assert abs(sum(p[0] for p in parts) - full_e) <= tol * abs(full_e)
     gsum = parts[0][1] + parts[1][1]
     for (n, s), a, b in zip(O.param_shapes(cfg), O.unflatten(gsum, cfg), O.unflatten(full_g, cfg)):
-        assert rel(a, b) <= 1e-5, n
+        assert rel(a, b) <= tol, (n, rel(a, b))
