@@ -70,7 +70,7 @@ int dalloc(T** p, size_t n) {
 
 // Control block layout (ints): [0] cursor, [1] resolved batch, [2..] batch order.
 constexpr int kFvParts = 1024;   // FV stream grid (one thetaPrior partial per block)
-constexpr int kGraphLog2 = 5;    // the longest replayed graph: 2^5 = 32 steps
+constexpr int kGraphSteps = 32;  // the longest replayed graph
 constexpr int kMaxProfKernels = 24;
 constexpr int kDbgWG = 1024;      // diagnostics: stamp slots per launch (workgroups)
 
@@ -135,7 +135,7 @@ struct vaeb_ctx {
     hipEvent_t ctl_ev = nullptr;
     // graphs
     hipGraphExec_t g1[2] = {nullptr, nullptr};
-    hipGraphExec_t gP[kGraphLog2 + 1] = {};   // gP[k]: 2^k steps from arena 0 (run_steps)
+    hipGraphExec_t gN[kGraphSteps + 1] = {};  // gN[n]: n steps from arena 0 (run_steps)
     bool graph_failed = false;
     // comm
     ncclComm_t comm = nullptr;
@@ -727,9 +727,9 @@ bool flips(const vaeb_ctx* c) { return c->c.estimator != VAEB_EST_FV && c->c.est
 
 void free_graphs(vaeb_ctx* c) {
     for (auto& g1 : c->g1) if (g1) hipGraphExecDestroy(g1);
-    for (auto& gp : c->gP) if (gp) hipGraphExecDestroy(gp);
+    for (auto& gn : c->gN) if (gn) hipGraphExecDestroy(gn);
     c->g1[0] = c->g1[1] = nullptr;
-    for (auto& gp : c->gP) gp = nullptr;
+    for (auto& gn : c->gN) gn = nullptr;
 }
 
 // Capture nsteps consecutive steps starting from parameter arena `par`.
@@ -756,62 +756,35 @@ int step_eager(vaeb_ctx* c) {
     return 0;
 }
 
-// Graph `k` of the power-of-two family: 2^k steps from arena 0 (k = 1 .. kGraphLog2),
-// captured on first use.
-int graph_pow2(vaeb_ctx* c, int k, hipGraphExec_t* out) {
-    if (!c->gP[k]) {
-        if (int rc = capture(c, 1 << k, 0, &c->gP[k])) {
-            c->graph_failed = true;
-            free_graphs(c);
-            (void)hipGetLastError();
-            return rc;
-        }
-    }
-    *out = c->gP[k];
-    return 0;
-}
-
 // Enqueue n steps (graph replay when enabled, else eager launches).  Graphs: g1[par] is
-// one step from arena par; gP[k] is 2^k (even) steps from arena 0.  Any n replays as
-// [one step back to arena 0] + n / 32 launches of the 32-step graph + one graph per set
-// bit of the remainder (16, 8, 4, 2) + [one step]: at most 6 graph launches besides the
-// 32-step ones, so the per-step cost does not depend on n % 32.
+// one step from arena par; gN[m] is m steps from arena 0 (m = 1 .. 32), the whole family
+// captured at the first call (a capture inside a later, timed call would cost more than
+// the launches it saves).  A call replays as [one step back to arena 0] + n / 32 launches
+// of gN[32] + ONE launch of gN[n % 32]: a 20-step call is one graph, not 16 + 4 (each
+// graph-to-graph boundary left the GPU idle for ~9 us).
 int run_steps(vaeb_ctx* c, int n) {
     if (c->c.use_graph && !c->graph_failed) {
         if (!c->g1[0]) {
-            // the whole family at first use: a capture inside a later (timed) call would
-            // cost more than the launches it saves
             int rc = capture(c, 1, 0, &c->g1[0]);
             if (rc == 0) rc = capture(c, 1, 1, &c->g1[1]);
-            hipGraphExec_t g = nullptr;
-            for (int k = 1; k <= kGraphLog2 && rc == 0; ++k) rc = graph_pow2(c, k, &g);
+            for (int m = 1; m <= kGraphSteps && rc == 0; ++m) rc = capture(c, m, 0, &c->gN[m]);
             if (rc) { c->graph_failed = true; free_graphs(c); (void)hipGetLastError(); }
         }
         if (!c->graph_failed) {
             int i = 0;
-            auto one = [&]() -> int {
-                HIP_TRY(hipGraphLaunch(c->g1[c->par], c->s));
-                if (flips(c)) c->par ^= 1;
-                return 0;
-            };
-            if (c->par != 0 && n > 0) { if (int rc = one()) return rc; ++i; }
             // FV / FVS never flip the arena: c->par stays 0 and every family graph applies
-            for (int k = kGraphLog2; k >= 1 && !c->graph_failed; --k) {
-                const int len = 1 << k;
-                if (k < kGraphLog2 && ((n - i) & len) == 0) continue;
-                while (n - i >= len && !c->graph_failed) {
-                    hipGraphExec_t g = nullptr;
-                    if (graph_pow2(c, k, &g)) break;
-                    HIP_TRY(hipGraphLaunch(g, c->s));
-                    i += len;
-                    if (k < kGraphLog2) break;
-                }
+            if (c->par != 0 && n > 0) {
+                HIP_TRY(hipGraphLaunch(c->g1[c->par], c->s));
+                c->par ^= 1;
+                ++i;
             }
-            if (!c->graph_failed) {
-                for (; i < n; ++i) if (int rc = one()) return rc;
-                return 0;
+            while (n - i > 0) {
+                const int m = std::min(kGraphSteps, n - i);
+                HIP_TRY(hipGraphLaunch(c->gN[m], c->s));
+                if (flips(c)) c->par = m & 1;
+                i += m;
             }
-            n -= i;   // a capture failed: the rest runs eagerly
+            return 0;
         }
     }
     for (int i = 0; i < n; ++i)
