@@ -61,6 +61,9 @@ CASES = [
     ("latent1_LA_L2", dict(D=30, H=17, Z=1, estimator="LA", L=2), 5),
     ("mnist_B1024", dict(D=784, H=500, Z=20), 1024),         # fp32 engine at a large batch
     ("gauss_B333", dict(D=560, H=200, Z=2, continuous=True), 333),
+    # atomic latent hand-offs (fan-in <= 16) with two fx slots per thread (Z > 16)
+    ("latent24_atomic_L2", dict(D=784, H=128, Z=24, L=2), 100),
+    ("latent28_atomic_LA", dict(D=200, H=96, Z=28, estimator="LA", L=2), 50),
 ]
 
 
@@ -367,3 +370,40 @@ def test_epoch_throughput_mode_matches_sync_mode():
         res.append((tot, ctx.get_params()))
     assert abs(res[0][0] - res[1][0]) <= 1e-5 * abs(res[0][0])
     assert np.array_equal(res[0][1], res[1][1])
+
+
+@pytest.mark.parametrize("kw", [dict(D=560, H=200, Z=2, continuous=True), dict(D=784, H=128, Z=24, L=2)],
+                         ids=["frey2", "latent24_L2"])
+def test_atomic_and_slab_handoffs_agree(kw, monkeypatch):
+    """The counted fixed-point atomic hand-offs (latent.hpp fx_*, chosen at fan-in <= 16)
+    against the slab + ticket + reducer form (VAEB_ATOMIC_HO=0) on the same 6 Philox steps:
+    the two sum the same partials in different arithmetic (exact integer vs ordered fp32),
+    so they agree to rounding, and each is bitwise deterministic (graph == eager)."""
+    from vaeb_amd import _lib
+    cfg = O.Config(**kw)
+    B = 100
+    x = data_for(cfg, 8 * B)
+    order = np.array([3, 1, 4, 1, 5, 7], np.int32)
+    out = {}
+    for mode in ("atomic", "slab"):
+        for use_graph in (True, False):
+            monkeypatch.setenv("VAEB_ATOMIC_HO", "1" if mode == "atomic" else "0")
+            ctx = _lib.Context(cfg.D, cfg.H, cfg.Z, B, L=cfg.L,
+                               decoder=_lib.DEC_GAUSSIAN if cfg.continuous else _lib.DEC_BERNOULLI,
+                               max_eval_rows=B, use_graph=use_graph)
+            ctx.set_data(x)
+            ctx.set_params(O.flatten(O.init_params(cfg)))
+            ctx.set_eps_mode(_lib.EPS_PHILOX, 10)
+            ctx.set_step(0)
+            ctx.update_many(order)
+            s_, n_ = ctx.epoch_elbo()
+            out[mode, use_graph] = (s_ / n_, ctx.get_params())
+            ctx.close()
+    for mode in ("atomic", "slab"):
+        assert out[mode, True][0] == out[mode, False][0]
+        assert np.array_equal(out[mode, True][1], out[mode, False][1])
+    ea, es = out["atomic", True][0], out["slab", True][0]
+    assert abs(ea - es) <= 1e-5 * abs(es), (ea, es)
+    d = np.abs(out["atomic", True][1] - out["slab", True][1])
+    assert d.max() <= 2 * len(order) * cfg.lr          # a ~lr sign(g) step may flip where |g| ~ 1e-7
+    assert float((d > 1e-3 * cfg.lr).mean()) <= 1e-3

@@ -87,6 +87,71 @@ DEV bool arrive_last(int* cnt, int target, int* sflag) {
     return last;
 }
 
+// ---------------------------------------------------------------- atomic hand-off
+// The alternative to slab + ticket + reducer: every contributing workgroup adds its
+// partial of element e into ONE 64-bit accumulator with a returning agent-scope atomic,
+// as a counted fixed-point number  inc = 2^56 + round(v * 2^32)  (two's complement).  The
+// add that brings the count field to n (the number of contributors) returns the complete
+// sum, so that workgroup -- whichever it is -- finishes element e itself: no slab stores,
+// no drain, no ticket, no reducer.  Every access to an accumulator is an atomic RMW on
+// that one location (a single modification order), so no cross-location ordering, fence or
+// cache rule is involved; the completer resets it (atomic store) for the next launch.
+// Integer adds are associative: the sum, and so the result, is bitwise the same for any
+// arrival order.  Range |sum| < 2^23, resolution 2^-32 (the latent sums here are O(1..100)).
+typedef __attribute__((address_space(1))) unsigned long long gu64;
+constexpr double kFxScale = 4294967296.0;   // 2^32
+DEV uint64_t fx_inc(float v) {
+    const int64_t q = (int64_t)__builtin_rint((double)v * kFxScale);
+    return (1ull << 56) + (uint64_t)q;
+}
+// adds inc to *p and returns the accumulator's new value (issue every add of a lane
+// before decoding any: each decode waits for its add's return)
+DEV uint64_t fx_add(uint64_t* p, uint64_t inc) {
+    return __hip_atomic_fetch_add((gu64*)p, (unsigned long long)inc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) +
+           inc;
+}
+// true (and the element's sum in `out`) when tot is the value after the n-th add
+DEV bool fx_done(uint64_t tot, int n, float& out) {
+    const uint64_t cnt = (tot + (1ull << 55)) >> 56;
+    out = (float)((double)(int64_t)(tot - (cnt << 56)) * (1.0 / kFxScale));
+    return cnt == (uint64_t)n;
+}
+DEV void fx_reset(uint64_t* p) { __hip_atomic_store((gu64*)p, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+// Accumulator e lives at word e * kFxStride: the atomics execute at the memory side, and
+// consecutive 8-B words would put a whole hand-off (a few thousand accumulators, 32 adds
+// each) on a handful of memory channels.
+constexpr int kFxStride = 33;
+DEV uint64_t* fx_at(uint64_t* base, int64_t e) { return base + e * kFxStride; }
+
+// A tile's 16 rows x 2Z partials (Z <= 32) are handed off by all 512 threads of its
+// workgroup, repacked through LDS so that no lane adds for a padding column: thread t takes
+// elements t and t + 512 (NS = 2 slots when Z > 16, then the first is always present), element
+// e = (column e >> 4, row e & 15).  Only the second slot's add sits in a branch, so at most
+// one wait separates the two adds (a branch around every add made hipcc wait for each).
+template <int NS>
+struct FxSlots {
+    uint64_t t[NS];
+    bool ok[NS];
+    int col[NS], row[NS];
+    DEV void add(uint64_t* acc, int64_t row0, int ncol, const float (*pm)[17], int ne) {
+#pragma unroll
+        for (int u = 0; u < NS; ++u) {
+            const int e = (int)threadIdx.x + 512 * u;
+            ok[u] = e < ne;
+            col[u] = ok[u] ? e >> 4 : 0;
+            row[u] = e & 15;
+        }
+#pragma unroll
+        for (int u = 0; u < NS; ++u) {
+            const uint64_t inc = fx_inc(pm[col[u]][row[u]]);
+            uint64_t* p = fx_at(acc, (row0 + row[u]) * ncol + col[u]);
+            t[u] = 0;
+            if (NS == 2 && u == 0) t[u] = fx_add(p, inc);   // always present when NS == 2
+            else if (ok[u]) t[u] = fx_add(p, inc);
+        }
+    }
+};
+
 // ----------------------------------------------------------------------------- P1'
 // Grid (Mbp/16, ceil(H/16)), 512 threads: 8 waves split K = D.  Tile (bx, by) stores its
 // partial [mu | lv] slab column-major: slab[((bx * nctH + by) * 2Z + c) * 16 + m]
@@ -145,11 +210,16 @@ DEV void fv_stream_block(const FvFold& a, int fb, int nfb, double* sh) {
     }
 }
 
-template <int NCT, int GCH, bool FV>
+// AT (atomic hand-off): tile (bx, by) adds its partial [mu | lv] into acc_ml; the add that
+// completes an element stores mu or lv (+ bias).  Meanwhile waves 1-7 of column tile 0
+// write the row block's eps (Philox keyed by the global row, the host buffer, or 0); z and
+// the KL / LA terms are formed by decout_z_kernel<.., AT>.
+template <int NCT, int GCH, bool FV, bool AT>
 DEV void enc_latent_body(const StepArgs& a, const FvFold& fvf) {
     __shared__ f32x4 red[512];
     __shared__ float hs[16][20];
     __shared__ int sflag;
+    __shared__ float pm[AT ? 64 : 1][17];   // AT: the tile's [mu | lv] partials, [column][row]
     const int nctH = FV ? (a.H + 15) >> 4 : (int)gridDim.y;   // FV: rows beyond run the stream
     if (FV && (int)blockIdx.y >= nctH) {
         fv_stream_block(fvf, (blockIdx.y - nctH) * gridDim.x + blockIdx.x, (gridDim.y - nctH) * gridDim.x,
@@ -178,6 +248,17 @@ DEV void enc_latent_body(const StepArgs& a, const FvFold& fvf) {
             bw[2 * ct + 1] = mc4(bw5, Z, ct * 16 + li, n0 + 4 * q, Z, H);
         }
     }
+    // AT: the bias of each element this thread may complete (column c: b4[c] | b5[c - Z])
+    float bias[NCT];
+    if constexpr (AT) {
+        const rsrc_t b4 = mkbuf(a.b4, (int64_t)Z * 4), b5 = mkbuf(a.b5, (int64_t)Z * 4);
+#pragma unroll
+        for (int u = 0; u < NCT; ++u) {
+            const int e = (int)threadIdx.x + 512 * u, c = e >> 4;
+            const bool ok = e < 32 * Z;
+            bias[u] = bld(b4, ok && c < Z ? (uint32_t)c * 4u : kOOB) + bld(b5, ok && c >= Z ? (uint32_t)(c - Z) * 4u : kOOB);
+        }
+    }
     f32x4 acc[1] = {zero4()};
     wave_mainloop<1, 8, GCH>(p, m0 + li, n0 + li, p.K, wave, acc);
     VAEB_STAMP(a, 1);
@@ -200,12 +281,58 @@ DEV void enc_latent_body(const StepArgs& a, const FvFold& fvf) {
 #pragma unroll
         for (int s = 0; s < 4; ++s) av[s] = hs[li][4 * q + s];
         const int64_t base = ((int64_t)bx * nctH + by) * 2 * Z;
+        if constexpr (AT) {
 #pragma unroll
-        for (int w = 0; w < 2 * NCT; ++w) {
-            const f32x4 sv = mfma4(av, bw[w], zero4());
-            const int nz = (w >> 1) * 16 + li;  // latent column of this lane
-            st4_sc1(bs, nz < Z ? (uint32_t)(((base + (w & 1) * Z + nz) * 16 + 4 * q) * 4) : kOOB, sv);
+            for (int w = 0; w < 2 * NCT; ++w) {
+                const f32x4 sv = mfma4(av, bw[w], zero4());
+                const int nz = (w >> 1) * 16 + li;
+                if (nz < Z)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) pm[(w & 1) * Z + nz][4 * q + r] = sv[r];
+            }
+        } else {
+#pragma unroll
+            for (int w = 0; w < 2 * NCT; ++w) {
+                const f32x4 sv = mfma4(av, bw[w], zero4());
+                const int nz = (w >> 1) * 16 + li;  // latent column of this lane
+                st4_sc1(bs, nz < Z ? (uint32_t)(((base + (w & 1) * Z + nz) * 16 + 4 * q) * 4) : kOOB, sv);
+            }
         }
+    }
+    if constexpr (AT) {
+        __syncthreads();
+        FxSlots<NCT> fx;
+        fx.add(a.acc_ml, m0, 2 * Z, pm, 32 * Z);
+        if (by == 0) {   // the row block's eps, while the adds are in flight
+            // the row base comes from `next` (kCtlNext): cur_batch is written by tile (0,0)
+            // of this same launch, which need not have run yet
+            const int64_t grow0 =
+                (a.order ? (int64_t)ld_launch_const(a.cursor + kCtlNext) * a.row_base_mul : 0) + a.row_base_add;
+            const uint64_t c23 = philox_c23(a.step ? *a.step : 0, a.domain);
+            const int per = 16 * Z;
+            for (int id = threadIdx.x; id < a.L * per; id += 512) {
+                const int l = id / per, ml = (id - l * per) / Z, j = id - l * per - ml * Z;
+                const int m = m0 + ml;
+                float e = 0.f;
+                if (m < a.Mb) {
+                    if (a.eps_mode == 0) e = philox_normal(a.seed, (uint32_t)(grow0 + m), (uint32_t)(l * Z + j), c23);
+                    else if (a.eps_mode == 1) e = a.eps_in[((int64_t)l * a.eps_in_ld + m) * Z + j];
+                }
+                a.eps[((int64_t)l * a.Mbp + m) * Z + j] = e;
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < NCT; ++u) {
+            float v;
+            if (fx.ok[u] && fx_done(fx.t[u], nctH, v)) {
+                const int c = fx.col[u], m = m0 + fx.row[u];
+                float* dst = c < Z ? a.mu : a.lv;
+                dst[(int64_t)m * Z + (c < Z ? c : c - Z)] = m < a.Mb ? v + bias[u] : 0.f;
+                fx_reset(fx_at(a.acc_ml, (int64_t)m * 2 * Z + c));
+            }
+        }
+        VAEB_STAMP(a, 2);
+        return;
     }
     VAEB_STAMP(a, 2);
     if (!arrive_last(a.cnt_ml + bx, nctH, &sflag)) return;
@@ -293,13 +420,13 @@ DEV void enc_latent_body(const StepArgs& a, const FvFold& fvf) {
     }
     VAEB_STAMP(a, 5);
 }
-template <int NCT, int GCH>
+template <int NCT, int GCH, bool AT>
 __global__ __launch_bounds__(512) void enc_latent_kernel(StepArgs a) {
-    enc_latent_body<NCT, GCH, false>(a, FvFold{});
+    enc_latent_body<NCT, GCH, false, AT>(a, FvFold{});
 }
-template <int NCT, int GCH>
+template <int NCT, int GCH, bool AT>
 __global__ __launch_bounds__(512) void enc_latent_fv_kernel(StepArgs a, FvFold f) {
-    enc_latent_body<NCT, GCH, true>(a, f);
+    enc_latent_body<NCT, GCH, true, AT>(a, f);
 }
 
 // ----------------------------------------------------------------------------- P4'
@@ -314,7 +441,10 @@ __global__ __launch_bounds__(512) void enc_latent_fv_kernel(StepArgs a, FvFold f
 // vmcnt at each, serialising the z, W1 / b1 and W2 round trips.  The x rows for the
 // likelihood are resolved (scalar load of cur_batch) only after wave 0 has issued its
 // first block's operand loads.
-template <int NB, int ZS, bool V1>
+// AT (atomic hand-off, enc_latent_body<.., AT>): z = mu + exp(lv / 2) eps is formed here
+// from mu, lv and eps (all written by the encoder launch), and column tile 0 stores z and
+// the row's KL (LB / FV, plane 0) or LA partial for the backward and the ELBO.
+template <int NB, int ZS, bool V1, bool AT>
 __global__ __launch_bounds__(512, 4) void decout_z_kernel(StepArgs a) {
     VAEB_STAMP(a, 0);
     PDecOut p{a, nullptr, a.Me, a.D, a.H};
@@ -331,10 +461,49 @@ __global__ __launch_bounds__(512, 4) void decout_z_kernel(StepArgs a) {
     const rsrc_t bb1 = mkbuf(a.b1, (int64_t)H * 4);
     constexpr bool v1 = V1;
     float zb[ZS];
-    {
+    if constexpr (!AT) {
         const rsrc_t bz = mkbuf(a.z, (int64_t)a.Me * Z * 4);
 #pragma unroll
         for (int t = 0; t < ZS; ++t) zb[t] = bld(bz, (4 * t + q < Z) ? (uint32_t)((m0 + li) * Z + 4 * t + q) * 4u : kOOB);
+    } else {
+        // the row block's 16 x Z block of z, once per workgroup: thread (ml, j) loads mu, lv
+        // and eps of one element (coalesced), the waves then read their fragments from LDS
+        __shared__ float zs[16][33];
+        __shared__ float gs[16][33];
+        const int per = 16 * Z;
+        const int l = m0 / a.Mbp;                 // a 16-row block never straddles two planes
+        const int i0 = m0 - l * a.Mbp;
+        if ((int)threadIdx.x < per) {
+            const int ml = threadIdx.x / Z, j = threadIdx.x - ml * Z;
+            const int i = i0 + ml;
+            const float mu = a.mu[(int64_t)i * Z + j], lv = a.lv[(int64_t)i * Z + j];
+            const float e = a.eps[((int64_t)l * a.Mbp + i) * Z + j];
+            const bool rv = i < a.Mb;
+            const float z = rv ? mu + fexp(0.5f * lv) * e : 0.f;
+            zs[ml][j] = z;
+            if (col0) {
+                a.z[((int64_t)l * a.Mbp + i) * Z + j] = z;
+                const float elv = fexp(lv);
+                float g;
+                if (a.est == EST_LA) {
+                    const float d = z - mu;
+                    g = (-0.5f * z * z) - (-0.5f * lv - 0.5f * d * d / elv);
+                } else {
+                    g = 0.5f * (1.f + lv - mu * mu - elv);
+                }
+                gs[ml][j] = rv ? g : 0.f;
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int t = 0; t < ZS; ++t) zb[t] = (4 * t + q < Z) ? zs[li][4 * t + q] : 0.f;
+        if (col0 && threadIdx.x < 16 && (a.est == EST_LA || l == 0)) {
+            float f = 0.f;
+            for (int j = 0; j < Z; ++j) f += gs[threadIdx.x][j];
+            const int i = i0 + threadIdx.x;
+            float* dst = a.est == EST_LA ? a.la_part + ((int64_t)l * a.Mbp + i) * a.nctZ : a.kl_part + (int64_t)i * a.nctZ;
+            for (int n = 0; n < a.nctZ; ++n) dst[n] = n == 0 ? f : 0.f;
+        }
     }
     PDecOut::Pre pre{};
     f32x4 acc[NB];

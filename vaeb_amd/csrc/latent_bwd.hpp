@@ -53,10 +53,15 @@ DEV void latent_bwd_elem(const StepArgs& a, bool valid, int m, int j, float mu, 
 // One dhd tile (bx = row block of the L * Mbp decoder rows, by = H column tile) + its dZ
 // slab; the last arriver of latent row block bx % (Mbp / 16) finishes the latent backward.
 // red: >= 512 f32x4 of LDS.
-template <int NCT, int GCH, bool V>
+// AT (atomic hand-off, latent.hpp fx_*): instead of a dZ slab, the tile adds its partial
+// dZ_l(m, j) into S(m, j) = sum_l dZ_l and dZ_l eps_l(m, j) into E(m, j) = sum_l dZ_l eps_l
+// (acc_dz; L * H/16 contributors each); the add completing S stores dMu(m, j), the one
+// completing E stores dLv(m, j).  dZ itself is not stored on this path.
+template <int NCT, int GCH, bool V, bool AT>
 DEV void dhd_dz_body(const PDhdT<V>& p0, int bx, int by, f32x4* red, int sid) {
     __shared__ float ts[16][20];
     __shared__ int sflag;
+    __shared__ float pm[AT ? 64 : 1][17];   // AT: [dZ | dZ eps] partials, [column][row]
     PDhdT<V> p = p0;
     p.prepare();
     const StepArgs& a = p.a;
@@ -70,6 +75,7 @@ DEV void dhd_dz_body(const PDhdT<V>& p0, int bx, int by, f32x4* red, int sid) {
 
     typename PDhdT<V>::Pre pre{};
     f32x4 w1v[NCT];
+    float ev[NCT][4];   // AT: eps_l at (row 4q + r, latent j)
     if (wave == 0) {
         pre = p.prefetch(m0, n0);
         // W1^T rows n0 .. n0 + 15 at latent j = ct * 16 + li: 4 consecutive n per lane
@@ -77,6 +83,28 @@ DEV void dhd_dz_body(const PDhdT<V>& p0, int bx, int by, f32x4* red, int sid) {
         const bool vh = (H & 3) == 0 && aligned16(a.W1);
 #pragma unroll
         for (int ct = 0; ct < NCT; ++ct) w1v[ct] = kc4(bw1, H, ct * 16 + li, n0 + 4 * q, Z, H, vh);
+        if constexpr (AT) {
+            const rsrc_t be = mkbuf(a.eps, (int64_t)a.Me * Z * 4);
+#pragma unroll
+            for (int ct = 0; ct < NCT; ++ct)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int j = ct * 16 + li, m = rbl * 16 + 4 * q + r;
+                    ev[ct][r] = bld(be, j < Z ? (uint32_t)((l * a.Mbp + m) * Z + j) * 4u : kOOB);
+                }
+        }
+    }
+    // AT: mu, lv of each element this thread may complete (column c: dMu | dLv of latent c % Z)
+    float muv[NCT], lvv[NCT];
+    if constexpr (AT) {
+        const rsrc_t bm = mkbuf(a.mu, (int64_t)a.Mbp * Z * 4), bl = mkbuf(a.lv, (int64_t)a.Mbp * Z * 4);
+#pragma unroll
+        for (int u = 0; u < NCT; ++u) {
+            const int e = (int)threadIdx.x + 512 * u, c = e >> 4, m = rbl * 16 + (e & 15);
+            const uint32_t o = e < 32 * Z ? (uint32_t)(m * Z + (c < Z ? c : c - Z)) * 4u : kOOB;
+            muv[u] = bld(bm, o);
+            lvv[u] = bld(bl, o);
+        }
     }
     f32x4 acc[1] = {zero4()};
     wave_mainloop<1, 8, GCH>(p, m0 + li, n0 + li, p.K, wave, acc);
@@ -99,14 +127,61 @@ DEV void dhd_dz_body(const PDhdT<V>& p0, int bx, int by, f32x4* red, int sid) {
         f32x4 av;
 #pragma unroll
         for (int s = 0; s < 4; ++s) av[s] = ts[li][4 * q + s];
-        const rsrc_t bs = mkbuf(a.slab_dz, (int64_t)a.L * a.Mbp * nctH * Z * 4);
-        const int64_t blk = ((int64_t)l * nrb + rbl) * nctH + by;
+        if constexpr (AT) {
 #pragma unroll
-        for (int ct = 0; ct < NCT; ++ct) {
-            const f32x4 sv = mfma4(av, w1v[ct], zero4());
-            const int j = ct * 16 + li;
-            st4_sc1(bs, j < Z ? (uint32_t)(((blk * Z + j) * 16 + 4 * q) * 4) : kOOB, sv);
+            for (int ct = 0; ct < NCT; ++ct) {
+                const f32x4 sv = mfma4(av, w1v[ct], zero4());
+                const int j = ct * 16 + li;
+                if (j < Z)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        pm[j][4 * q + r] = sv[r];
+                        pm[Z + j][4 * q + r] = sv[r] * ev[ct][r];
+                    }
+            }
+        } else {
+            const rsrc_t bs = mkbuf(a.slab_dz, (int64_t)a.L * a.Mbp * nctH * Z * 4);
+            const int64_t blk = ((int64_t)l * nrb + rbl) * nctH + by;
+#pragma unroll
+            for (int ct = 0; ct < NCT; ++ct) {
+                const f32x4 sv = mfma4(av, w1v[ct], zero4());
+                const int j = ct * 16 + li;
+                st4_sc1(bs, j < Z ? (uint32_t)(((blk * Z + j) * 16 + 4 * q) * 4) : kOOB, sv);
+            }
         }
+    }
+    if constexpr (AT) {
+        // column c < Z: S = sum_l dZ_l of latent c; c >= Z: E = sum_l dZ_l eps_l of latent c - Z
+        __syncthreads();
+        FxSlots<NCT> fx;
+        fx.add(a.acc_dz, rbl * 16, 2 * Z, pm, 32 * Z);
+        const float sl = a.sc / (float)a.L;
+#pragma unroll
+        for (int u = 0; u < NCT; ++u) {
+            float v;
+            if (!(fx.ok[u] && fx_done(fx.t[u], nctH * a.L, v))) continue;
+            const int c = fx.col[u], m = rbl * 16 + fx.row[u];
+            const bool isE = c >= Z;
+            const int j = isE ? c - Z : c;
+            const bool valid = m < a.Mb;
+            const float mu = muv[u], lv = lvv[u], sd = fexp(0.5f * lv);
+            float tm = 0.f, tv = 0.f;
+            if (a.est == EST_LA && valid) {
+                for (int s = 0; s < a.L; ++s) {
+                    const int64_t os = ((int64_t)s * a.Mbp + m) * Z + j;
+                    const float zs = a.z[os];
+                    tm += -zs;
+                    tv += 0.5f - 0.5f * zs * sd * a.eps[os];
+                }
+            }
+            float d;
+            if (!isE) d = a.est == EST_LA ? v + sl * tm : v - a.sc * mu;
+            else d = a.est == EST_LA ? v * 0.5f * sd + sl * tv : v * 0.5f * sd + a.sc * 0.5f * (1.f - fexp(lv));
+            a.dMuLv[(int64_t)m * 2 * Z + c] = valid ? d : 0.f;
+            fx_reset(fx_at(a.acc_dz, (int64_t)m * 2 * Z + c));
+        }
+        VAEB_STAMP_AT(a, sid, 2);
+        return;
     }
     VAEB_STAMP_AT(a, sid, 2);
     if (!arrive_last(a.cnt_dz + rbl, nctH * a.L, &sflag)) return;
@@ -177,7 +252,7 @@ DEV void dhd_dz_body(const PDhdT<V>& p0, int bx, int by, f32x4* red, int sid) {
 // dhd (+ dZ slabs, latent backward) tiles and the dW2 (| dW6) weight-gradient tiles in one
 // grid.  The dhd tiles are dispatched first: with the latent backward behind them they are
 // the launch's critical path (tile_wgrad_kernel, without it, puts the dW2 blocks first).
-template <int NCT, int GCH, bool VEC, int TS>
+template <int NCT, int GCH, bool VEC, int TS, bool AT>
 __global__ __launch_bounds__(512) void dhd_dz_wgrad_kernel(PDhdT<VEC> p, WGradArgs w, int ntile, int gx) {
     __shared__ float sa[kWKB][kWP];
     __shared__ float sb[kWKB][kWP];
@@ -185,7 +260,7 @@ __global__ __launch_bounds__(512) void dhd_dz_wgrad_kernel(PDhdT<VEC> p, WGradAr
     const int b0 = blockIdx.x;
     const int bid = b0 < ntile ? xcd_remap(b0, ntile) : ntile + xcd_remap(b0 - ntile, nwg);
     if (bid < ntile) {
-        dhd_dz_body<NCT, GCH, VEC>(p, bid % gx, bid / gx, reinterpret_cast<f32x4*>(&sa[0][0]), bid);
+        dhd_dz_body<NCT, GCH, VEC, AT>(p, bid % gx, bid / gx, reinterpret_cast<f32x4*>(&sa[0][0]), bid);
         return;
     }
     if (w.dbg && threadIdx.x == 0) w.dbg[bid * 8 + 0] = __builtin_amdgcn_s_memrealtime();

@@ -57,6 +57,9 @@ struct StepArgs {
     // latent slabs + per-row-block arrival counters of the folded latent phases (latent.hpp)
     float *slab_ml, *slab_dz;
     int *cnt_ml, *cnt_dz;
+    // counted fixed-point accumulators of the atomic hand-off (latent.hpp: fx_*), zero
+    // between launches: [Mbp][2Z] for [mu | lv], [Mbp][2Z] for [sum_l dZ | sum_l dZ eps]
+    uint64_t *acc_ml, *acc_dz;
     uint64_t* dbg;         // diagnostics: per-workgroup s_memrealtime stamps (null = off)
 };
 

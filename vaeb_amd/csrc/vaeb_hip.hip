@@ -128,6 +128,7 @@ struct vaeb_ctx {
     float* yacc = nullptr;        // sampled reconstruction sum (allocated on first use)
     float *slab_ml = nullptr, *slab_dz = nullptr;  // folded-latent partial slabs (latent.hpp)
     int *cnt_ml = nullptr, *cnt_dz = nullptr;      // their per-row-block arrival counters
+    uint64_t *acc_ml = nullptr, *acc_dz = nullptr; // atomic hand-off accumulators (zeroed)
     // host staging (pinned)
     int* h_ctl = nullptr;
     float* h_elbo = nullptr;
@@ -146,6 +147,7 @@ struct vaeb_ctx {
     int dz_split = 8;             // P67 column splits per row block (fused.hpp dz_dh_body; VAEB_DZ_SPLIT)
     bool fold_bwd = true;         // Z <= 32: latent backward folded into the dhd launch (VAEB_FOLD_BWD=0: P67)
     int w3_ts = 1;                // folded path's last launch: tile width / 16 (VAEB_W3_TS)
+    bool atomic_ho = true;        // folded latent hand-offs by counted atomics (VAEB_ATOMIC_HO=0: slabs)
     bool decout_2b = true;        // bf16 Bernoulli decout on 256 x 128 tiles, 2 blocks / CU (VAEB_DECOUT_2B=0: 256 x 256)
     bool bf_fuse = true;          // bf16 engine: dhd + dW2 (| dW6) in one grid (VAEB_BF_FUSE=0: two launches)
     int num_cus = 256;            // compute units of the device (hipDeviceProp_t)
@@ -210,6 +212,7 @@ StepArgs make_args(vaeb_ctx* c, int par, int Mb, int mode, const float* xbase, b
     a.nctZ = cdiv(g.Z, 16);
     a.nctD = cdiv(g.D, 16);
     a.slab_ml = c->slab_ml; a.slab_dz = c->slab_dz; a.cnt_ml = c->cnt_ml; a.cnt_dz = c->cnt_dz;
+    a.acc_ml = c->acc_ml; a.acc_dz = c->acc_dz;
     return a;
 }
 
@@ -228,6 +231,14 @@ void launch_bigk(hipStream_t s, const P& p) {
 }
 
 bool fused_latent(const vaeb_ctx* c) { return c->c.Z <= 32; }
+// The folded latent hand-offs: counted fixed-point atomics (latent.hpp fx_*) or slabs +
+// ticket + reducer.  The returning adds to one accumulator serialise at the memory side, so
+// the atomic form wins only at a small fan-in (contributors per element): Frey 560-200-2
+// (13 column tiles) 38.5 -> 32.2 us per step; MNIST 784-500-20 (32 column tiles) 44.5 ->
+// 49.3 us.  Forward fan-in: the H column tiles; backward: H column tiles x L planes.
+constexpr int kFxMaxFanIn = 16;
+bool atomic_ml(const vaeb_ctx* c) { return c->atomic_ho && cdiv(c->c.H, 16) <= kFxMaxFanIn; }
+bool atomic_dz(const vaeb_ctx* c) { return c->atomic_ho && cdiv(c->c.H, 16) * c->c.L <= kFxMaxFanIn; }
 
 // Measurement brackets: mark(id) records an event before launch slot `id`.  With
 // reps > 1 (vaeb_profile_steps) every launch of the step is issued `reps` times back to
@@ -258,21 +269,65 @@ ElboArgs base_elbo(vaeb_ctx* c, const StepArgs& a) {
     return e;
 }
 
-template <int NB, bool V1>
+template <int NB, bool V1, bool AT>
 void launch_decout_zv(hipStream_t s, dim3 grid, const StepArgs& a) {
     switch ((a.Z + 3) / 4) {
-        case 1: hipLaunchKernelGGL((decout_z_kernel<NB, 1, V1>), grid, dim3(512), 0, s, a); break;
-        case 2: hipLaunchKernelGGL((decout_z_kernel<NB, 2, V1>), grid, dim3(512), 0, s, a); break;
-        case 3: case 4: hipLaunchKernelGGL((decout_z_kernel<NB, 4, V1>), grid, dim3(512), 0, s, a); break;
-        case 5: hipLaunchKernelGGL((decout_z_kernel<NB, 5, V1>), grid, dim3(512), 0, s, a); break;
-        default: hipLaunchKernelGGL((decout_z_kernel<NB, 8, V1>), grid, dim3(512), 0, s, a); break;
+        case 1: hipLaunchKernelGGL((decout_z_kernel<NB, 1, V1, AT>), grid, dim3(512), 0, s, a); break;
+        case 2: hipLaunchKernelGGL((decout_z_kernel<NB, 2, V1, AT>), grid, dim3(512), 0, s, a); break;
+        case 3: case 4: hipLaunchKernelGGL((decout_z_kernel<NB, 4, V1, AT>), grid, dim3(512), 0, s, a); break;
+        case 5: hipLaunchKernelGGL((decout_z_kernel<NB, 5, V1, AT>), grid, dim3(512), 0, s, a); break;
+        default: hipLaunchKernelGGL((decout_z_kernel<NB, 8, V1, AT>), grid, dim3(512), 0, s, a); break;
     }
 }
-template <int NB>
+template <int NB, bool AT>
 void launch_decout_z(hipStream_t s, dim3 grid, const StepArgs& a) {
     auto al = [](const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
-    if ((a.H & 3) == 0 && al(a.W1) && al(a.b1)) launch_decout_zv<NB, true>(s, grid, a);
-    else launch_decout_zv<NB, false>(s, grid, a);
+    if ((a.H & 3) == 0 && al(a.W1) && al(a.b1)) launch_decout_zv<NB, true, AT>(s, grid, a);
+    else launch_decout_zv<NB, false, AT>(s, grid, a);
+}
+
+// dhd_dz_wgrad_kernel at compile-time NCT (latent col tiles), GCH, load width, AT
+template <int TS, bool AT>
+void launch_dhd_dz(hipStream_t s, dim3 grid, const PDhdT<true>& p5, const PDhdT<false>& p5s, const WGradArgs& w,
+                   int ntile, int gx, bool vec, bool deep) {
+    if (p5.a.Z <= 16) {
+        if (deep) {
+            if (vec) hipLaunchKernelGGL((dhd_dz_wgrad_kernel<1, 8, true, TS, AT>), grid, dim3(512), 0, s, p5, w, ntile, gx);
+            else hipLaunchKernelGGL((dhd_dz_wgrad_kernel<1, 8, false, TS, AT>), grid, dim3(512), 0, s, p5s, w, ntile, gx);
+        } else {
+            if (vec) hipLaunchKernelGGL((dhd_dz_wgrad_kernel<1, 4, true, TS, AT>), grid, dim3(512), 0, s, p5, w, ntile, gx);
+            else hipLaunchKernelGGL((dhd_dz_wgrad_kernel<1, 4, false, TS, AT>), grid, dim3(512), 0, s, p5s, w, ntile, gx);
+        }
+    } else {
+        if (deep) {
+            if (vec) hipLaunchKernelGGL((dhd_dz_wgrad_kernel<2, 8, true, TS, AT>), grid, dim3(512), 0, s, p5, w, ntile, gx);
+            else hipLaunchKernelGGL((dhd_dz_wgrad_kernel<2, 8, false, TS, AT>), grid, dim3(512), 0, s, p5s, w, ntile, gx);
+        } else {
+            if (vec) hipLaunchKernelGGL((dhd_dz_wgrad_kernel<2, 4, true, TS, AT>), grid, dim3(512), 0, s, p5, w, ntile, gx);
+            else hipLaunchKernelGGL((dhd_dz_wgrad_kernel<2, 4, false, TS, AT>), grid, dim3(512), 0, s, p5s, w, ntile, gx);
+        }
+    }
+}
+
+// enc_latent_kernel / enc_latent_fv_kernel at compile-time NCT (latent col tiles), GCH
+// (main-loop chunk group), AT (atomic hand-off)
+template <bool AT>
+void launch_enc_latent(hipStream_t s, dim3 g1, const StepArgs& a, const FvFold& fvf, bool deep) {
+    if (fvf.rows > 0) {
+        if (a.Z <= 16) {
+            if (deep) hipLaunchKernelGGL((enc_latent_fv_kernel<1, 8, AT>), g1, dim3(512), 0, s, a, fvf);
+            else hipLaunchKernelGGL((enc_latent_fv_kernel<1, 4, AT>), g1, dim3(512), 0, s, a, fvf);
+        } else {
+            if (deep) hipLaunchKernelGGL((enc_latent_fv_kernel<2, 8, AT>), g1, dim3(512), 0, s, a, fvf);
+            else hipLaunchKernelGGL((enc_latent_fv_kernel<2, 4, AT>), g1, dim3(512), 0, s, a, fvf);
+        }
+    } else if (a.Z <= 16) {
+        if (deep) hipLaunchKernelGGL((enc_latent_kernel<1, 8, AT>), g1, dim3(512), 0, s, a);
+        else hipLaunchKernelGGL((enc_latent_kernel<1, 4, AT>), g1, dim3(512), 0, s, a);
+    } else {
+        if (deep) hipLaunchKernelGGL((enc_latent_kernel<2, 8, AT>), g1, dim3(512), 0, s, a);
+        else hipLaunchKernelGGL((enc_latent_kernel<2, 4, AT>), g1, dim3(512), 0, s, a);
+    }
 }
 
 // Training minibatches with Z <= 32 fold the latent block into the wide phases
@@ -289,31 +344,24 @@ int enqueue_forward(vaeb_ctx* c, const StepArgs& a0, Prof& pr, const FvFold& fvf
     if (folded_latent(c, a)) {
         const dim3 g1(a.Mbp / 16, cdiv(a.H, 16) + fvf.rows);
         const bool deep = cdiv(cdiv(a.D, 16), 8) > 4;
+        const bool at = atomic_ml(c);
         pr.mark(16);
         REP(pr) {
-            if (fvf.rows > 0) {
-                if (a.Z <= 16) {
-                    if (deep) hipLaunchKernelGGL((enc_latent_fv_kernel<1, 8>), g1, dim3(512), 0, s, a, fvf);
-                    else hipLaunchKernelGGL((enc_latent_fv_kernel<1, 4>), g1, dim3(512), 0, s, a, fvf);
-                } else {
-                    if (deep) hipLaunchKernelGGL((enc_latent_fv_kernel<2, 8>), g1, dim3(512), 0, s, a, fvf);
-                    else hipLaunchKernelGGL((enc_latent_fv_kernel<2, 4>), g1, dim3(512), 0, s, a, fvf);
-                }
-            } else if (a.Z <= 16) {
-                if (deep) hipLaunchKernelGGL((enc_latent_kernel<1, 8>), g1, dim3(512), 0, s, a);
-                else hipLaunchKernelGGL((enc_latent_kernel<1, 4>), g1, dim3(512), 0, s, a);
-            } else {
-                if (deep) hipLaunchKernelGGL((enc_latent_kernel<2, 8>), g1, dim3(512), 0, s, a);
-                else hipLaunchKernelGGL((enc_latent_kernel<2, 4>), g1, dim3(512), 0, s, a);
-            }
+            if (at) launch_enc_latent<true>(s, g1, a, fvf, deep);
+            else launch_enc_latent<false>(s, g1, a, fvf, deep);
         }
         CHECK_LAUNCH();
         a.dbg = next_dbg(c);
         const dim3 g4(a.Me / 16, cdiv(a.D, 16));
         pr.mark(17);
         REP(pr) {
-            if (gaussian(c)) launch_decout_z<2>(s, g4, a);
-            else launch_decout_z<1>(s, g4, a);
+            if (gaussian(c)) {
+                if (at) launch_decout_z<2, true>(s, g4, a);
+                else launch_decout_z<2, false>(s, g4, a);
+            } else {
+                if (at) launch_decout_z<1, true>(s, g4, a);
+                else launch_decout_z<1, false>(s, g4, a);
+            }
         }
         CHECK_LAUNCH();
         return 0;
@@ -611,23 +659,8 @@ int enqueue_train_step(vaeb_ctx* c, int par, bool prof, bool fresh = true) {
         const bool deep = cdiv(cdiv(p5.K, 16), 8) > 4;
         pr.mark(39);
         REP(pr) {
-            if (a.Z <= 16) {
-                if (deep) {
-                    if (vec) hipLaunchKernelGGL((dhd_dz_wgrad_kernel<1, 8, true, kWTJ_P5 / 16>), grid, dim3(512), 0, s, p5, w, ntile, gx);
-                    else hipLaunchKernelGGL((dhd_dz_wgrad_kernel<1, 8, false, kWTJ_P5 / 16>), grid, dim3(512), 0, s, p5s, w, ntile, gx);
-                } else {
-                    if (vec) hipLaunchKernelGGL((dhd_dz_wgrad_kernel<1, 4, true, kWTJ_P5 / 16>), grid, dim3(512), 0, s, p5, w, ntile, gx);
-                    else hipLaunchKernelGGL((dhd_dz_wgrad_kernel<1, 4, false, kWTJ_P5 / 16>), grid, dim3(512), 0, s, p5s, w, ntile, gx);
-                }
-            } else {
-                if (deep) {
-                    if (vec) hipLaunchKernelGGL((dhd_dz_wgrad_kernel<2, 8, true, kWTJ_P5 / 16>), grid, dim3(512), 0, s, p5, w, ntile, gx);
-                    else hipLaunchKernelGGL((dhd_dz_wgrad_kernel<2, 8, false, kWTJ_P5 / 16>), grid, dim3(512), 0, s, p5s, w, ntile, gx);
-                } else {
-                    if (vec) hipLaunchKernelGGL((dhd_dz_wgrad_kernel<2, 4, true, kWTJ_P5 / 16>), grid, dim3(512), 0, s, p5, w, ntile, gx);
-                    else hipLaunchKernelGGL((dhd_dz_wgrad_kernel<2, 4, false, kWTJ_P5 / 16>), grid, dim3(512), 0, s, p5s, w, ntile, gx);
-                }
-            }
+            if (atomic_dz(c)) launch_dhd_dz<kWTJ_P5 / 16, true>(s, grid, p5, p5s, w, ntile, gx, vec, deep);
+            else launch_dhd_dz<kWTJ_P5 / 16, false>(s, grid, p5, p5s, w, ntile, gx, vec, deep);
         }
         CHECK_LAUNCH();
     } else {
@@ -875,6 +908,7 @@ int vaeb_create(const vaeb_config* cfg, vaeb_ctx** out) {
     if (const char* ts = getenv("VAEB_W3_TS")) c->w3_ts = atoi(ts) == 2 ? 2 : 1;
     if (const char* bf = getenv("VAEB_BF_FUSE")) c->bf_fuse = atoi(bf) != 0;
     if (const char* d2 = getenv("VAEB_DECOUT_2B")) c->decout_2b = atoi(d2) != 0;
+    if (const char* ah = getenv("VAEB_ATOMIC_HO")) c->atomic_ho = atoi(ah) != 0;
     if (e != hipSuccess) { delete c; return fail(VAEB_ERR_HIP, "stream/event create: %s", hipGetErrorString(e)); }
     const int64_t D = g.D, H = g.H, Z = g.Z;
     std::vector<int64_t> sz = {D * H, H * Z, H * Z, Z * H, H * D};
@@ -927,6 +961,8 @@ int vaeb_create(const vaeb_config* cfg, vaeb_ctx** out) {
         rc = rc ? rc : dalloc(&c->slab_dz, (size_t)(g.L * Bp * nctH * 32));
         rc = rc ? rc : dalloc(&c->cnt_ml, (size_t)(Bp / 16));
         rc = rc ? rc : dalloc(&c->cnt_dz, (size_t)(Bp / 16));
+        rc = rc ? rc : dalloc(&c->acc_ml, (size_t)(Bp * 2 * Z * kFxStride));
+        rc = rc ? rc : dalloc(&c->acc_dz, (size_t)(Bp * 2 * Z * kFxStride));
     }
     if (!rc && is_bf16(c)) rc = bf_alloc(c);
     if (rc) { vaeb_destroy(c); return rc; }
@@ -958,6 +994,8 @@ int vaeb_destroy(vaeb_ctx* c) {
     for (float* p : fp) if (p) hipFree(p);
     if (c->cnt_ml) hipFree(c->cnt_ml);
     if (c->cnt_dz) hipFree(c->cnt_dz);
+    if (c->acc_ml) hipFree(c->acc_ml);
+    if (c->acc_dz) hipFree(c->acc_dz);
     if (c->ictl) hipFree(c->ictl);
     if (c->step) hipFree(c->step);
     if (c->epoch) hipFree(c->epoch);
