@@ -372,22 +372,24 @@ def test_epoch_throughput_mode_matches_sync_mode():
     assert np.array_equal(res[0][1], res[1][1])
 
 
-@pytest.mark.parametrize("kw", [dict(D=560, H=200, Z=2, continuous=True), dict(D=784, H=128, Z=24, L=2)],
-                         ids=["frey2", "latent24_L2"])
+@pytest.mark.parametrize("kw", [dict(D=560, H=200, Z=2, continuous=True), dict(D=784, H=128, Z=24, L=2),
+                                dict(D=784, H=500, Z=20)], ids=["frey2", "latent24_L2", "mnist20"])
 def test_atomic_and_slab_handoffs_agree(kw, monkeypatch):
-    """The counted fixed-point atomic hand-offs (latent.hpp fx_*, chosen at fan-in <= 16)
-    against the slab + ticket + reducer form (VAEB_ATOMIC_HO=0) on the same 6 Philox steps:
-    the two sum the same partials in different arithmetic (exact integer vs ordered fp32),
-    so they agree to rounding, and each is bitwise deterministic (graph == eager)."""
+    """The folded latent hand-offs (latent.hpp) on the same 6 Philox steps: the default
+    (VAEB_ATOMIC_HO=1: counted fixed-point atomics up to fan-in 16, slabs above), the
+    ticketed atomic form (=2, A/B only) and slabs + ticket + reducer everywhere (=0).
+    They sum the same partials in different arithmetic (exact integer vs ordered fp32), so
+    they agree to rounding, and each is bitwise deterministic (graph == eager)."""
     from vaeb_amd import _lib
     cfg = O.Config(**kw)
     B = 100
     x = data_for(cfg, 8 * B)
     order = np.array([3, 1, 4, 1, 5, 7], np.int32)
     out = {}
-    for mode in ("atomic", "slab"):
+    modes = {"atomic": "1", "ticketed": "2", "slab": "0"}
+    for mode in modes:
         for use_graph in (True, False):
-            monkeypatch.setenv("VAEB_ATOMIC_HO", "1" if mode == "atomic" else "0")
+            monkeypatch.setenv("VAEB_ATOMIC_HO", modes[mode])
             ctx = _lib.Context(cfg.D, cfg.H, cfg.Z, B, L=cfg.L,
                                decoder=_lib.DEC_GAUSSIAN if cfg.continuous else _lib.DEC_BERNOULLI,
                                max_eval_rows=B, use_graph=use_graph)
@@ -399,11 +401,13 @@ def test_atomic_and_slab_handoffs_agree(kw, monkeypatch):
             s_, n_ = ctx.epoch_elbo()
             out[mode, use_graph] = (s_ / n_, ctx.get_params())
             ctx.close()
-    for mode in ("atomic", "slab"):
+    for mode in modes:
         assert out[mode, True][0] == out[mode, False][0]
         assert np.array_equal(out[mode, True][1], out[mode, False][1])
-    ea, es = out["atomic", True][0], out["slab", True][0]
-    assert abs(ea - es) <= 1e-5 * abs(es), (ea, es)
-    d = np.abs(out["atomic", True][1] - out["slab", True][1])
-    assert d.max() <= 2 * len(order) * cfg.lr          # a ~lr sign(g) step may flip where |g| ~ 1e-7
-    assert float((d > 1e-3 * cfg.lr).mean()) <= 1e-3
+    es = out["slab", True][0]
+    for mode in ("atomic", "ticketed"):
+        ea = out[mode, True][0]
+        assert abs(ea - es) <= 1e-5 * abs(es), (mode, ea, es)
+        d = np.abs(out[mode, True][1] - out["slab", True][1])
+        assert d.max() <= 2 * len(order) * cfg.lr          # a ~lr sign(g) step may flip where |g| ~ 1e-7
+        assert float((d > 1e-3 * cfg.lr).mean()) <= 1e-3

@@ -128,6 +128,42 @@ DEV uint64_t* fx_at(uint64_t* base, int64_t e) { return base + e * kFxStride; }
 // elements t and t + 512 (NS = 2 slots when Z > 16, then the first is always present), element
 // e = (column e >> 4, row e & 15).  Only the second slot's add sits in a branch, so at most
 // one wait separates the two adds (a branch around every add made hipcc wait for each).
+// HO == 2 (ticketed form): the same repacked adds without return, then the slab protocol's
+// ticket; the last arriver reads every sum once with an agent-scope exchange (read + reset).
+// The guide's producer form {8-B agent atomics both sides} with its table row 1 ticket.
+template <int NS>
+DEV void fx_add_nr(uint64_t* acc, int64_t row0, int ncol, const float (*pm)[17], int ne) {
+#pragma unroll
+    for (int u = 0; u < NS; ++u) {
+        const int e = (int)threadIdx.x + 512 * u;
+        if (e < ne) {
+            const int c = e >> 4, r = e & 15;
+            __hip_atomic_fetch_add((gu64*)fx_at(acc, (row0 + r) * ncol + c), (unsigned long long)fx_inc(pm[c][r]),
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+}
+DEV float fx_take(uint64_t* p, int n) {
+    float v;
+    fx_done(__hip_atomic_exchange((gu64*)p, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), n, v);
+    return v;
+}
+// every wave's adds performed (vmcnt 0) before the workgroup's one ticket; true in the
+// workgroup whose ticket completed `target`
+DEV bool arrive_last_all(int* cnt, int target, int* sflag) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const int old = __hip_atomic_fetch_add((gint*)cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        *sflag = (old == target - 1);
+    }
+    __syncthreads();
+    const bool last = *sflag != 0;
+    if (last && threadIdx.x == 0) __hip_atomic_store((gint*)cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // keep the reads below the ticket
+    return last;
+}
+
 template <int NS>
 struct FxSlots {
     uint64_t t[NS];
@@ -214,12 +250,13 @@ DEV void fv_stream_block(const FvFold& a, int fb, int nfb, double* sh) {
 // completes an element stores mu or lv (+ bias).  Meanwhile waves 1-7 of column tile 0
 // write the row block's eps (Philox keyed by the global row, the host buffer, or 0); z and
 // the KL / LA terms are formed by decout_z_kernel<.., AT>.
-template <int NCT, int GCH, bool FV, bool AT>
+template <int NCT, int GCH, bool FV, int HO>
 DEV void enc_latent_body(const StepArgs& a, const FvFold& fvf) {
+    constexpr bool AT = HO == 1;
     __shared__ f32x4 red[512];
     __shared__ float hs[16][20];
     __shared__ int sflag;
-    __shared__ float pm[AT ? 64 : 1][17];   // AT: the tile's [mu | lv] partials, [column][row]
+    __shared__ float pm[HO ? 64 : 1][17];   // HO: the tile's [mu | lv] partials, [column][row]
     const int nctH = FV ? (a.H + 15) >> 4 : (int)gridDim.y;   // FV: rows beyond run the stream
     if (FV && (int)blockIdx.y >= nctH) {
         fv_stream_block(fvf, (blockIdx.y - nctH) * gridDim.x + blockIdx.x, (gridDim.y - nctH) * gridDim.x,
@@ -281,7 +318,7 @@ DEV void enc_latent_body(const StepArgs& a, const FvFold& fvf) {
 #pragma unroll
         for (int s = 0; s < 4; ++s) av[s] = hs[li][4 * q + s];
         const int64_t base = ((int64_t)bx * nctH + by) * 2 * Z;
-        if constexpr (AT) {
+        if constexpr (HO != 0) {
 #pragma unroll
             for (int w = 0; w < 2 * NCT; ++w) {
                 const f32x4 sv = mfma4(av, bw[w], zero4());
@@ -334,8 +371,15 @@ DEV void enc_latent_body(const StepArgs& a, const FvFold& fvf) {
         VAEB_STAMP(a, 2);
         return;
     }
-    VAEB_STAMP(a, 2);
-    if (!arrive_last(a.cnt_ml + bx, nctH, &sflag)) return;
+    if constexpr (HO == 2) {
+        __syncthreads();
+        fx_add_nr<NCT>(a.acc_ml, m0, 2 * Z, pm, 32 * Z);
+        VAEB_STAMP(a, 2);
+        if (!arrive_last_all(a.cnt_ml + bx, nctH, &sflag)) return;
+    } else {
+        VAEB_STAMP(a, 2);
+        if (!arrive_last(a.cnt_ml + bx, nctH, &sflag)) return;
+    }
     VAEB_STAMP(a, 3);
 
     // ---- reducer (the last tile of row block bx): the element-wise operands ride the
@@ -356,9 +400,17 @@ DEV void enc_latent_body(const StepArgs& a, const FvFold& fvf) {
     // this same launch, which need not have run yet
     const int64_t grow0 = (a.order ? (int64_t)ld_launch_const(a.cursor + kCtlNext) * a.row_base_mul : 0) + a.row_base_add;
     const int64_t stp = a.step ? *a.step : 0;
+    float mu = 0.f, lv = 0.f;
+    if constexpr (HO == 2) {
+        if (n < Z) {
+            mu = fx_take(fx_at(a.acc_ml, (int64_t)m * 2 * Z + n), nctH);
+            lv = fx_take(fx_at(a.acc_ml, (int64_t)m * 2 * Z + Z + n), nctH);
+        }
+        VAEB_STAMP(a, 4);
+    }
     const int NF4 = 8 * Z;                  // float4 per slab (2Z columns x 16 rows)
     const int NP = 512 / NF4;               // slab partitions (threads >= NP * NF4 idle)
-    {
+    if constexpr (HO == 0) {
         const int f = threadIdx.x % NF4, part = threadIdx.x / NF4;
         const int64_t first = (int64_t)bx * nctH * NF4;
         constexpr int SV = 12;
@@ -374,17 +426,16 @@ DEV void enc_latent_body(const StepArgs& a, const FvFold& fvf) {
             for (int u = 0; u < SV; ++u) sum += v[u];
         }
         red[threadIdx.x] = sum;
+        __syncthreads();
+        VAEB_STAMP(a, 4);
+        auto at = [&](int c) {  // element (column c, row ml) of the summed slab
+            const int ff = (c * 16 + ml) >> 2, comp = ml & 3;
+            float v = 0.f;
+            for (int pp = 0; pp < NP; ++pp) v += red[pp * NF4 + ff][comp];
+            return v;
+        };
+        if (n < Z) { mu = at(n); lv = at(Z + n); }
     }
-    __syncthreads();
-    VAEB_STAMP(a, 4);
-    auto at = [&](int c) {  // element (column c, row ml) of the summed slab
-        const int ff = (c * 16 + ml) >> 2, comp = ml & 3;
-        float v = 0.f;
-        for (int pp = 0; pp < NP; ++pp) v += red[pp * NF4 + ff][comp];
-        return v;
-    };
-    float mu = 0.f, lv = 0.f;
-    if (n < Z) { mu = at(n); lv = at(Z + n); }
     mu = valid ? mu + b4n : 0.f;
     lv = valid ? lv + b5n : 0.f;
     const float sd = fexp(0.5f * lv);
@@ -420,13 +471,13 @@ DEV void enc_latent_body(const StepArgs& a, const FvFold& fvf) {
     }
     VAEB_STAMP(a, 5);
 }
-template <int NCT, int GCH, bool AT>
+template <int NCT, int GCH, int HO>
 __global__ __launch_bounds__(512) void enc_latent_kernel(StepArgs a) {
-    enc_latent_body<NCT, GCH, false, AT>(a, FvFold{});
+    enc_latent_body<NCT, GCH, false, HO>(a, FvFold{});
 }
-template <int NCT, int GCH, bool AT>
+template <int NCT, int GCH, int HO>
 __global__ __launch_bounds__(512) void enc_latent_fv_kernel(StepArgs a, FvFold f) {
-    enc_latent_body<NCT, GCH, true, AT>(a, f);
+    enc_latent_body<NCT, GCH, true, HO>(a, f);
 }
 
 // ----------------------------------------------------------------------------- P4'

@@ -57,11 +57,12 @@ DEV void latent_bwd_elem(const StepArgs& a, bool valid, int m, int j, float mu, 
 // dZ_l(m, j) into S(m, j) = sum_l dZ_l and dZ_l eps_l(m, j) into E(m, j) = sum_l dZ_l eps_l
 // (acc_dz; L * H/16 contributors each); the add completing S stores dMu(m, j), the one
 // completing E stores dLv(m, j).  dZ itself is not stored on this path.
-template <int NCT, int GCH, bool V, bool AT>
+template <int NCT, int GCH, bool V, int HO>
 DEV void dhd_dz_body(const PDhdT<V>& p0, int bx, int by, f32x4* red, int sid) {
+    constexpr bool AT = HO == 1;
     __shared__ float ts[16][20];
     __shared__ int sflag;
-    __shared__ float pm[AT ? 64 : 1][17];   // AT: [dZ | dZ eps] partials, [column][row]
+    __shared__ float pm[HO ? 64 : 1][17];   // HO: [dZ | dZ eps] partials, [column][row]
     PDhdT<V> p = p0;
     p.prepare();
     const StepArgs& a = p.a;
@@ -83,7 +84,7 @@ DEV void dhd_dz_body(const PDhdT<V>& p0, int bx, int by, f32x4* red, int sid) {
         const bool vh = (H & 3) == 0 && aligned16(a.W1);
 #pragma unroll
         for (int ct = 0; ct < NCT; ++ct) w1v[ct] = kc4(bw1, H, ct * 16 + li, n0 + 4 * q, Z, H, vh);
-        if constexpr (AT) {
+        if constexpr (HO != 0) {
             const rsrc_t be = mkbuf(a.eps, (int64_t)a.Me * Z * 4);
 #pragma unroll
             for (int ct = 0; ct < NCT; ++ct)
@@ -127,7 +128,7 @@ DEV void dhd_dz_body(const PDhdT<V>& p0, int bx, int by, f32x4* red, int sid) {
         f32x4 av;
 #pragma unroll
         for (int s = 0; s < 4; ++s) av[s] = ts[li][4 * q + s];
-        if constexpr (AT) {
+        if constexpr (HO != 0) {
 #pragma unroll
             for (int ct = 0; ct < NCT; ++ct) {
                 const f32x4 sv = mfma4(av, w1v[ct], zero4());
@@ -183,8 +184,15 @@ DEV void dhd_dz_body(const PDhdT<V>& p0, int bx, int by, f32x4* red, int sid) {
         VAEB_STAMP_AT(a, sid, 2);
         return;
     }
-    VAEB_STAMP_AT(a, sid, 2);
-    if (!arrive_last(a.cnt_dz + rbl, nctH * a.L, &sflag)) return;
+    if constexpr (HO == 2) {
+        __syncthreads();
+        fx_add_nr<NCT>(a.acc_dz, rbl * 16, 2 * Z, pm, 32 * Z);
+        VAEB_STAMP_AT(a, sid, 2);
+        if (!arrive_last_all(a.cnt_dz + rbl, nctH * a.L, &sflag)) return;
+    } else {
+        VAEB_STAMP_AT(a, sid, 2);
+        if (!arrive_last(a.cnt_dz + rbl, nctH * a.L, &sflag)) return;
+    }
     VAEB_STAMP_AT(a, sid, 3);
 
     // ---- reducer: latent row block rbl, all L planes.  Thread (ml, j) owns one element;
@@ -211,7 +219,15 @@ DEV void dhd_dz_body(const PDhdT<V>& p0, int bx, int by, f32x4* red, int sid) {
     const int NP = 512 / NF4;         // slab partitions (threads >= NP * NF4 idle)
     const int f = threadIdx.x % NF4, part = threadIdx.x / NF4;
     float dzsum = 0.f, dzes = 0.f;
-    for (int s = 0; s < a.L; ++s) {
+    if constexpr (HO == 2) {   // the summed S = sum_l dZ_l and E = sum_l dZ_l eps_l (dZ not stored)
+        if (j < Z) {
+            dzsum = fx_take(fx_at(a.acc_dz, (int64_t)m * 2 * Z + j), nctH * a.L);
+            dzes = fx_take(fx_at(a.acc_dz, (int64_t)m * 2 * Z + Z + j), nctH * a.L);
+        }
+        dzsum = valid ? dzsum : 0.f;
+        dzes = valid ? dzes : 0.f;
+    }
+    for (int s = 0; s < (HO == 2 ? 0 : a.L); ++s) {
         const int64_t first = ((int64_t)s * nrb + rbl) * nctH * NF4;
         constexpr int SV = 12;
         f32x4 sum = zero4();
@@ -252,7 +268,7 @@ DEV void dhd_dz_body(const PDhdT<V>& p0, int bx, int by, f32x4* red, int sid) {
 // dhd (+ dZ slabs, latent backward) tiles and the dW2 (| dW6) weight-gradient tiles in one
 // grid.  The dhd tiles are dispatched first: with the latent backward behind them they are
 // the launch's critical path (tile_wgrad_kernel, without it, puts the dW2 blocks first).
-template <int NCT, int GCH, bool VEC, int TS, bool AT>
+template <int NCT, int GCH, bool VEC, int TS, int HO>
 __global__ __launch_bounds__(512) void dhd_dz_wgrad_kernel(PDhdT<VEC> p, WGradArgs w, int ntile, int gx) {
     __shared__ float sa[kWKB][kWP];
     __shared__ float sb[kWKB][kWP];
@@ -260,7 +276,7 @@ __global__ __launch_bounds__(512) void dhd_dz_wgrad_kernel(PDhdT<VEC> p, WGradAr
     const int b0 = blockIdx.x;
     const int bid = b0 < ntile ? xcd_remap(b0, ntile) : ntile + xcd_remap(b0 - ntile, nwg);
     if (bid < ntile) {
-        dhd_dz_body<NCT, GCH, VEC, AT>(p, bid % gx, bid / gx, reinterpret_cast<f32x4*>(&sa[0][0]), bid);
+        dhd_dz_body<NCT, GCH, VEC, HO>(p, bid % gx, bid / gx, reinterpret_cast<f32x4*>(&sa[0][0]), bid);
         return;
     }
     if (w.dbg && threadIdx.x == 0) w.dbg[bid * 8 + 0] = __builtin_amdgcn_s_memrealtime();

@@ -147,7 +147,7 @@ struct vaeb_ctx {
     int dz_split = 8;             // P67 column splits per row block (fused.hpp dz_dh_body; VAEB_DZ_SPLIT)
     bool fold_bwd = true;         // Z <= 32: latent backward folded into the dhd launch (VAEB_FOLD_BWD=0: P67)
     int w3_ts = 1;                // folded path's last launch: tile width / 16 (VAEB_W3_TS)
-    bool atomic_ho = true;        // folded latent hand-offs by counted atomics (VAEB_ATOMIC_HO=0: slabs)
+    int atomic_ho = 1;            // folded latent hand-offs: 1 by fan-in (ho_mode), 0 slabs, 2 ticketed atomics
     bool decout_2b = true;        // bf16 Bernoulli decout on 256 x 128 tiles, 2 blocks / CU (VAEB_DECOUT_2B=0: 256 x 256)
     bool bf_fuse = true;          // bf16 engine: dhd + dW2 (| dW6) in one grid (VAEB_BF_FUSE=0: two launches)
     int num_cus = 256;            // compute units of the device (hipDeviceProp_t)
@@ -236,9 +236,18 @@ bool fused_latent(const vaeb_ctx* c) { return c->c.Z <= 32; }
 // the atomic form wins only at a small fan-in (contributors per element): Frey 560-200-2
 // (13 column tiles) 38.5 -> 32.2 us per step; MNIST 784-500-20 (32 column tiles) 44.5 ->
 // 49.3 us.  Forward fan-in: the H column tiles; backward: H column tiles x L planes.
+// HO = 2 (VAEB_ATOMIC_HO=2 only): the same adds without return + the slab protocol's ticket,
+// the last arriver reading each sum with one 8-B exchange -- measured slower than both
+// (MNIST 53.6 us, Frey 35.0 us): at fan-in 32 the 64-bit adds to one word serialise either
+// way.  VAEB_ATOMIC_HO=0 forces the slabs.
 constexpr int kFxMaxFanIn = 16;
-bool atomic_ml(const vaeb_ctx* c) { return c->atomic_ho && cdiv(c->c.H, 16) <= kFxMaxFanIn; }
-bool atomic_dz(const vaeb_ctx* c) { return c->atomic_ho && cdiv(c->c.H, 16) * c->c.L <= kFxMaxFanIn; }
+int ho_mode(const vaeb_ctx* c, int fan_in) {
+    if (c->atomic_ho == 0 || fan_in > 255) return 0;
+    if (c->atomic_ho == 2) return 2;
+    return fan_in <= kFxMaxFanIn ? 1 : 0;
+}
+int ho_ml(const vaeb_ctx* c) { return ho_mode(c, cdiv(c->c.H, 16)); }
+int ho_dz(const vaeb_ctx* c) { return ho_mode(c, cdiv(c->c.H, 16) * c->c.L); }
 
 // Measurement brackets: mark(id) records an event before launch slot `id`.  With
 // reps > 1 (vaeb_profile_steps) every launch of the step is issued `reps` times back to
@@ -287,46 +296,46 @@ void launch_decout_z(hipStream_t s, dim3 grid, const StepArgs& a) {
 }
 
 // dhd_dz_wgrad_kernel at compile-time NCT (latent col tiles), GCH, load width, AT
-template <int TS, bool AT>
+template <int TS, int HO>
 void launch_dhd_dz(hipStream_t s, dim3 grid, const PDhdT<true>& p5, const PDhdT<false>& p5s, const WGradArgs& w,
                    int ntile, int gx, bool vec, bool deep) {
     if (p5.a.Z <= 16) {
         if (deep) {
-            if (vec) hipLaunchKernelGGL((dhd_dz_wgrad_kernel<1, 8, true, TS, AT>), grid, dim3(512), 0, s, p5, w, ntile, gx);
-            else hipLaunchKernelGGL((dhd_dz_wgrad_kernel<1, 8, false, TS, AT>), grid, dim3(512), 0, s, p5s, w, ntile, gx);
+            if (vec) hipLaunchKernelGGL((dhd_dz_wgrad_kernel<1, 8, true, TS, HO>), grid, dim3(512), 0, s, p5, w, ntile, gx);
+            else hipLaunchKernelGGL((dhd_dz_wgrad_kernel<1, 8, false, TS, HO>), grid, dim3(512), 0, s, p5s, w, ntile, gx);
         } else {
-            if (vec) hipLaunchKernelGGL((dhd_dz_wgrad_kernel<1, 4, true, TS, AT>), grid, dim3(512), 0, s, p5, w, ntile, gx);
-            else hipLaunchKernelGGL((dhd_dz_wgrad_kernel<1, 4, false, TS, AT>), grid, dim3(512), 0, s, p5s, w, ntile, gx);
+            if (vec) hipLaunchKernelGGL((dhd_dz_wgrad_kernel<1, 4, true, TS, HO>), grid, dim3(512), 0, s, p5, w, ntile, gx);
+            else hipLaunchKernelGGL((dhd_dz_wgrad_kernel<1, 4, false, TS, HO>), grid, dim3(512), 0, s, p5s, w, ntile, gx);
         }
     } else {
         if (deep) {
-            if (vec) hipLaunchKernelGGL((dhd_dz_wgrad_kernel<2, 8, true, TS, AT>), grid, dim3(512), 0, s, p5, w, ntile, gx);
-            else hipLaunchKernelGGL((dhd_dz_wgrad_kernel<2, 8, false, TS, AT>), grid, dim3(512), 0, s, p5s, w, ntile, gx);
+            if (vec) hipLaunchKernelGGL((dhd_dz_wgrad_kernel<2, 8, true, TS, HO>), grid, dim3(512), 0, s, p5, w, ntile, gx);
+            else hipLaunchKernelGGL((dhd_dz_wgrad_kernel<2, 8, false, TS, HO>), grid, dim3(512), 0, s, p5s, w, ntile, gx);
         } else {
-            if (vec) hipLaunchKernelGGL((dhd_dz_wgrad_kernel<2, 4, true, TS, AT>), grid, dim3(512), 0, s, p5, w, ntile, gx);
-            else hipLaunchKernelGGL((dhd_dz_wgrad_kernel<2, 4, false, TS, AT>), grid, dim3(512), 0, s, p5s, w, ntile, gx);
+            if (vec) hipLaunchKernelGGL((dhd_dz_wgrad_kernel<2, 4, true, TS, HO>), grid, dim3(512), 0, s, p5, w, ntile, gx);
+            else hipLaunchKernelGGL((dhd_dz_wgrad_kernel<2, 4, false, TS, HO>), grid, dim3(512), 0, s, p5s, w, ntile, gx);
         }
     }
 }
 
 // enc_latent_kernel / enc_latent_fv_kernel at compile-time NCT (latent col tiles), GCH
 // (main-loop chunk group), AT (atomic hand-off)
-template <bool AT>
+template <int HO>
 void launch_enc_latent(hipStream_t s, dim3 g1, const StepArgs& a, const FvFold& fvf, bool deep) {
     if (fvf.rows > 0) {
         if (a.Z <= 16) {
-            if (deep) hipLaunchKernelGGL((enc_latent_fv_kernel<1, 8, AT>), g1, dim3(512), 0, s, a, fvf);
-            else hipLaunchKernelGGL((enc_latent_fv_kernel<1, 4, AT>), g1, dim3(512), 0, s, a, fvf);
+            if (deep) hipLaunchKernelGGL((enc_latent_fv_kernel<1, 8, HO>), g1, dim3(512), 0, s, a, fvf);
+            else hipLaunchKernelGGL((enc_latent_fv_kernel<1, 4, HO>), g1, dim3(512), 0, s, a, fvf);
         } else {
-            if (deep) hipLaunchKernelGGL((enc_latent_fv_kernel<2, 8, AT>), g1, dim3(512), 0, s, a, fvf);
-            else hipLaunchKernelGGL((enc_latent_fv_kernel<2, 4, AT>), g1, dim3(512), 0, s, a, fvf);
+            if (deep) hipLaunchKernelGGL((enc_latent_fv_kernel<2, 8, HO>), g1, dim3(512), 0, s, a, fvf);
+            else hipLaunchKernelGGL((enc_latent_fv_kernel<2, 4, HO>), g1, dim3(512), 0, s, a, fvf);
         }
     } else if (a.Z <= 16) {
-        if (deep) hipLaunchKernelGGL((enc_latent_kernel<1, 8, AT>), g1, dim3(512), 0, s, a);
-        else hipLaunchKernelGGL((enc_latent_kernel<1, 4, AT>), g1, dim3(512), 0, s, a);
+        if (deep) hipLaunchKernelGGL((enc_latent_kernel<1, 8, HO>), g1, dim3(512), 0, s, a);
+        else hipLaunchKernelGGL((enc_latent_kernel<1, 4, HO>), g1, dim3(512), 0, s, a);
     } else {
-        if (deep) hipLaunchKernelGGL((enc_latent_kernel<2, 8, AT>), g1, dim3(512), 0, s, a);
-        else hipLaunchKernelGGL((enc_latent_kernel<2, 4, AT>), g1, dim3(512), 0, s, a);
+        if (deep) hipLaunchKernelGGL((enc_latent_kernel<2, 8, HO>), g1, dim3(512), 0, s, a);
+        else hipLaunchKernelGGL((enc_latent_kernel<2, 4, HO>), g1, dim3(512), 0, s, a);
     }
 }
 
@@ -344,11 +353,13 @@ int enqueue_forward(vaeb_ctx* c, const StepArgs& a0, Prof& pr, const FvFold& fvf
     if (folded_latent(c, a)) {
         const dim3 g1(a.Mbp / 16, cdiv(a.H, 16) + fvf.rows);
         const bool deep = cdiv(cdiv(a.D, 16), 8) > 4;
-        const bool at = atomic_ml(c);
+        const int ho = ho_ml(c);
+        const bool at = ho == 1;
         pr.mark(16);
         REP(pr) {
-            if (at) launch_enc_latent<true>(s, g1, a, fvf, deep);
-            else launch_enc_latent<false>(s, g1, a, fvf, deep);
+            if (ho == 1) launch_enc_latent<1>(s, g1, a, fvf, deep);
+            else if (ho == 2) launch_enc_latent<2>(s, g1, a, fvf, deep);
+            else launch_enc_latent<0>(s, g1, a, fvf, deep);
         }
         CHECK_LAUNCH();
         a.dbg = next_dbg(c);
@@ -659,8 +670,11 @@ int enqueue_train_step(vaeb_ctx* c, int par, bool prof, bool fresh = true) {
         const bool deep = cdiv(cdiv(p5.K, 16), 8) > 4;
         pr.mark(39);
         REP(pr) {
-            if (atomic_dz(c)) launch_dhd_dz<kWTJ_P5 / 16, true>(s, grid, p5, p5s, w, ntile, gx, vec, deep);
-            else launch_dhd_dz<kWTJ_P5 / 16, false>(s, grid, p5, p5s, w, ntile, gx, vec, deep);
+            switch (ho_dz(c)) {
+                case 1: launch_dhd_dz<kWTJ_P5 / 16, 1>(s, grid, p5, p5s, w, ntile, gx, vec, deep); break;
+                case 2: launch_dhd_dz<kWTJ_P5 / 16, 2>(s, grid, p5, p5s, w, ntile, gx, vec, deep); break;
+                default: launch_dhd_dz<kWTJ_P5 / 16, 0>(s, grid, p5, p5s, w, ntile, gx, vec, deep); break;
+            }
         }
         CHECK_LAUNCH();
     } else {
@@ -908,7 +922,7 @@ int vaeb_create(const vaeb_config* cfg, vaeb_ctx** out) {
     if (const char* ts = getenv("VAEB_W3_TS")) c->w3_ts = atoi(ts) == 2 ? 2 : 1;
     if (const char* bf = getenv("VAEB_BF_FUSE")) c->bf_fuse = atoi(bf) != 0;
     if (const char* d2 = getenv("VAEB_DECOUT_2B")) c->decout_2b = atoi(d2) != 0;
-    if (const char* ah = getenv("VAEB_ATOMIC_HO")) c->atomic_ho = atoi(ah) != 0;
+    if (const char* ah = getenv("VAEB_ATOMIC_HO")) c->atomic_ho = atoi(ah);
     if (e != hipSuccess) { delete c; return fail(VAEB_ERR_HIP, "stream/event create: %s", hipGetErrorString(e)); }
     const int64_t D = g.D, H = g.H, Z = g.Z;
     std::vector<int64_t> sz = {D * H, H * Z, H * Z, Z * H, H * D};
