@@ -3,6 +3,8 @@ set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 bash scripts/gpu_profile_round2.sh || exit 1
+# the bench lines below read `traffic` from profiles/r2: use this run's PMC passes
+for cfg in mnist frey fv fvs synth; do cp gpurun_out/round2/$cfg/pmc_per_launch.json profiles/r2/pmc_${cfg}_per_launch.json; done
 bash scripts/gpu_mfma_busy.sh || exit 1
 mkdir -p gpurun_out/lines2
 for cfg in mnist frey fv fvs synth; do
