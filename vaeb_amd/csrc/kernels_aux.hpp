@@ -252,79 +252,69 @@ DEV f32x4 ld_w45(rsrc_t bw4, rsrc_t bw5, int Z, int H, int n, int k, bool vz) {
 
 // dA3 rows [kb, kb + kWKB) x columns [j0, j0 + 16 TS) into the B panel sb (Da3Src): wave
 // w of NWV takes the 16-row blocks w, w + NWV, ... (NR = kWKB / 16 / NWV of them); K = 2Z
-// <= 64.  load() issues every operand of all NR blocks (one round trip; a per-block load ->
-// MFMA loop cost the launch a second one), the [W4 | W5]^T slice once; form() runs the
-// MFMAs and the (1 - h^2) factor into sb.  Split so that wgrad_body can issue these loads
-// before it waits for the minibatch index its X panel needs.
+// <= 64.  Every operand of all NR blocks is issued before the first MFMA (one round trip;
+// a per-block load -> MFMA loop cost the launch a second one), the [W4 | W5]^T slice once.
 template <int NWV, int TS>
-struct Da3Panel {
-    static constexpr int NR = kWKB / 16 / NWV;
-    f32x4 bw[TS][4], av[NR][4];
-    float hv[NR][TS][4];
-    DEV void load(const Da3Src& d, int kb, int j0) {
-        const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-        const int li = lane & 15, q = lane >> 4;
-        const int Z = d.Z, H = d.H, K2 = 2 * d.Z;
-        const rsrc_t bd = mkbuf(d.dml, (int64_t)d.Mbp * K2 * 4);
-        const rsrc_t bw4 = mkbuf(d.W4, (int64_t)H * Z * 4), bw5 = mkbuf(d.W5, (int64_t)H * Z * 4);
-        const rsrc_t bh = mkbuf(d.h, (int64_t)d.Mbp * H * 4);
-        const bool vz = (Z & 3) == 0 && aligned16(d.W4) && aligned16(d.W5);
-        const bool vd = (K2 & 3) == 0 && aligned16(d.dml);
-        const int nkc = (K2 + 15) >> 4;
+DEV void da3_panel(const Da3Src& d, int kb, int j0, bool store, float (*sb)[kWP]) {
+    constexpr int NR = kWKB / 16 / NWV;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int li = lane & 15, q = lane >> 4;
+    const int Z = d.Z, H = d.H, K2 = 2 * d.Z;
+    const rsrc_t bd = mkbuf(d.dml, (int64_t)d.Mbp * K2 * 4);
+    const rsrc_t bw4 = mkbuf(d.W4, (int64_t)H * Z * 4), bw5 = mkbuf(d.W5, (int64_t)H * Z * 4);
+    const rsrc_t bh = mkbuf(d.h, (int64_t)d.Mbp * H * 4);
+    const bool vz = (Z & 3) == 0 && aligned16(d.W4) && aligned16(d.W5);
+    const bool vd = (K2 & 3) == 0 && aligned16(d.dml);
+    const int nkc = (K2 + 15) >> 4;
+    f32x4 bw[TS][4], av[NR][4], hv[NR][TS];
 #pragma unroll
-        for (int ts = 0; ts < TS; ++ts)
+    for (int ts = 0; ts < TS; ++ts)
 #pragma unroll
-            for (int c = 0; c < 4; ++c) bw[ts][c] = ld_w45(bw4, bw5, Z, c < nkc ? H : 0, j0 + 16 * ts + li, c * 16 + 4 * q, vz);
+        for (int c = 0; c < 4; ++c) bw[ts][c] = ld_w45(bw4, bw5, Z, c < nkc ? H : 0, j0 + 16 * ts + li, c * 16 + 4 * q, vz);
 #pragma unroll
-        for (int u = 0; u < NR; ++u) {
-            const int r0 = kb + 16 * (wv + NWV * u);
-            const int rl = r0 < d.Mbp ? d.Mbp : 0;   // blocks past the padded batch load nothing
+    for (int u = 0; u < NR; ++u) {
+        const int r0 = kb + 16 * (wv + NWV * u);
+        const int rl = r0 < d.Mbp ? d.Mbp : 0;   // blocks past the padded batch load nothing
 #pragma unroll
-            for (int c = 0; c < 4; ++c) av[u][c] = kc4(bd, K2, r0 + li, c * 16 + 4 * q, c < nkc ? rl : 0, K2, vd);
+        for (int c = 0; c < 4; ++c) av[u][c] = kc4(bd, K2, r0 + li, c * 16 + 4 * q, c < nkc ? rl : 0, K2, vd);
 #pragma unroll
-            for (int ts = 0; ts < TS; ++ts) {
-                const int n = j0 + 16 * ts + li;
+        for (int ts = 0; ts < TS; ++ts) {
+            const int n = j0 + 16 * ts + li;
 #pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const int mm = r0 + 4 * q + r;
-                    hv[u][ts][r] = bld(bh, (n < H && mm < d.Mb) ? (uint32_t)(mm * H + n) * 4u : kOOB);
-                }
+            for (int r = 0; r < 4; ++r) {
+                const int mm = r0 + 4 * q + r;
+                hv[u][ts][r] = bld(bh, (n < H && mm < d.Mb) ? (uint32_t)(mm * H + n) * 4u : kOOB);
             }
         }
     }
-    DEV void form(const Da3Src& d, int kb, int j0, bool store, float (*sb)[kWP]) const {
-        const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-        const int li = lane & 15, q = lane >> 4;
-        const int H = d.H, nkc = (2 * d.Z + 15) >> 4;
 #pragma unroll
-        for (int u = 0; u < NR; ++u) {
-            const int t = wv + NWV * u;
-            const int r0 = kb + 16 * t;
-            if (r0 >= d.Mbp) break;
+    for (int u = 0; u < NR; ++u) {
+        const int t = wv + NWV * u;
+        const int r0 = kb + 16 * t;
+        if (r0 >= d.Mbp) break;
 #pragma unroll
-            for (int ts = 0; ts < TS; ++ts) {
-                f32x4 acc = zero4();
+        for (int ts = 0; ts < TS; ++ts) {
+            f32x4 acc = zero4();
 #pragma unroll
-                for (int c = 0; c < 4; ++c)
-                    if (c < nkc) acc = mfma4(av[u][c], bw[ts][c], acc);
-                const int n = j0 + 16 * ts + li;
+            for (int c = 0; c < 4; ++c)
+                if (c < nkc) acc = mfma4(av[u][c], bw[ts][c], acc);
+            const int n = j0 + 16 * ts + li;
 #pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const int mm = r0 + 4 * q + r;
-                    const float v = (mm < d.Mb && n < H) ? acc[r] * (1.f - hv[u][ts][r] * hv[u][ts][r]) : 0.f;
-                    sb[16 * t + 4 * q + r][16 * ts + li] = v;
-                    if (store && n < H) d.dA3[(int64_t)mm * H + n] = v;
-                }
+            for (int r = 0; r < 4; ++r) {
+                const int mm = r0 + 4 * q + r;
+                const float v = (mm < d.Mb && n < H) ? acc[r] * (1.f - hv[u][ts][r] * hv[u][ts][r]) : 0.f;
+                sb[16 * t + 4 * q + r][16 * ts + li] = v;
+                if (store && n < H) d.dA3[(int64_t)mm * H + n] = v;
             }
         }
     }
-};
+}
 
 // One 64 x (16 TS) tile of group g (passed with a compile-time index, so its fields are
 // scalar kernel-argument loads; a dynamic index made hipcc fetch them with serialized
 // per-lane vector loads).  NWV = 4 waves (standalone launch) or 8 (a 512-thread fused
 // launch): waves w and w + 4 then take alternate K chunks and are summed through LDS.
-// DA3: the B panel is dA3, formed in the workgroup (Da3Panel) instead of loaded.
+// DA3: the B panel is dA3, formed in the workgroup (da3_panel) instead of loaded.
 template <bool VEC, int NWV, int TS, bool DA3 = false, class WA>
 DEV void wgrad_body(const WA& p, const WGroup& g, int bid, float (*sa)[kWP], float (*sb)[kWP]) {
     static_assert(NWV == 4 || NWV == 8, "wgrad: 4 or 8 waves");
@@ -340,7 +330,31 @@ DEV void wgrad_body(const WA& p, const WGroup& g, int bid, float (*sa)[kWP], flo
     const int li = lane & 15, q = lane >> 4;
     const int NT = g.N0 + g.N1;
 
-    Da3Panel<NWV, TS> d3;
+    // ---- prefetch theta / acc of this lane's 16 outputs (rows i0+16w+4q+r, cols j0+16t+li)
+    const bool upd = p.opt.update != 0;
+    const rsrc_t bth = mkbuf(p.opt.theta_in, p.P * 4), bac = mkbuf(p.opt.acc, p.P * 4);
+    uint32_t off[kWTS][4];
+    float th[kWTS][4], ac[kWTS][4];
+#pragma unroll
+    for (int t = 0; t < kWTS; ++t) {
+        const int j = j0 + 16 * t + li;
+        const bool s1 = j >= g.N0;
+        const int jj = s1 ? j - g.N0 : j;
+        const int nrow = s1 ? g.N1 : g.N0;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int i = i0 + 16 * wave + 4 * q + r;
+            const bool ok = j < NT && i <= g.rowsW;
+            const int64_t idx = (i < g.rowsW) ? (s1 ? g.offW1 : g.offW0) + (int64_t)i * nrow + jj
+                                              : (s1 ? g.offb1 : g.offb0) + jj;
+            off[t][r] = ok ? (uint32_t)idx * 4u : kOOB;
+            // unconditional loads (no branch): the waitcnt pass then sees them retired
+            // by the first panel wait instead of re-waiting after every epilogue store
+            const uint32_t lo = (upd && kh == 0) ? off[t][r] : kOOB;
+            th[t][r] = bld(bth, lo);
+            ac[t][r] = bld(bac, lo);
+        }
+    }
 
     // ---- K loop over LDS stages of kWKB rows
     const rsrc_t bb0 = mkbuf(g.b0, (int64_t)g.K * g.ld0 * 4);
@@ -350,11 +364,12 @@ DEV void wgrad_body(const WA& p, const WGroup& g, int bid, float (*sa)[kWP], flo
     f32x4 acc[kWTS];
 #pragma unroll
     for (int t = 0; t < kWTS; ++t) acc[t] = zero4();
-    constexpr int NU = (kWKB * 16) / NTH;
-    f32x4 ra[NU], rb[NU];
-    // stage the panels: element e = (row kr, float4 column c4).  All 16 loads of a thread
-    // are issued before the first LDS store (one memory round trip).
-    auto load_panels = [&](int kb) {
+    int kb = 0;
+    do {  // K >= 1 always; a do-loop keeps the pre-loop loads off the exit path
+        // stage the panels: element e = (row kr, float4 column c4).  All 16 loads of a
+        // thread are issued before the first LDS store (one memory round trip).
+        constexpr int NU = (kWKB * 16) / NTH;
+        f32x4 ra[NU], rb[NU];
 #pragma unroll
         for (int u = 0; u < NU; ++u) {
             const int e = threadIdx.x + NTH * u;
@@ -386,54 +401,7 @@ DEV void wgrad_body(const WA& p, const WGroup& g, int bid, float (*sa)[kWP], flo
                 }
             }
         }
-    };
-    // ---- prefetch theta / acc of this lane's 16 outputs (rows i0+16w+4q+r, cols j0+16t+li).
-    // vmcnt retires loads in issue order, so whichever group is issued first is waited for
-    // by the other's consumer.  The dW2 (| dW6) tiles issue their panels first (the MNIST
-    // dhd | dW2 launch 12.6 -> 11.9 us); the last launch's dW3 tiles keep theta / acc first
-    // (panels first: 10.3 -> 11.2 us -- its epilogue then waited on the later HBM reads).
-    const bool upd = p.opt.update != 0;
-    const rsrc_t bth = mkbuf(p.opt.theta_in, p.P * 4), bac = mkbuf(p.opt.acc, p.P * 4);
-    uint32_t off[kWTS][4];
-    float th[kWTS][4], ac[kWTS][4];
-    auto prefetch_opt = [&]() {
-#pragma unroll
-        for (int t = 0; t < kWTS; ++t) {
-            const int j = j0 + 16 * t + li;
-            const bool s1 = j >= g.N0;
-            const int jj = s1 ? j - g.N0 : j;
-            const int nrow = s1 ? g.N1 : g.N0;
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int i = i0 + 16 * wave + 4 * q + r;
-                const bool ok = j < NT && i <= g.rowsW;
-                const int64_t idx = (i < g.rowsW) ? (s1 ? g.offW1 : g.offW0) + (int64_t)i * nrow + jj
-                                                  : (s1 ? g.offb1 : g.offb0) + jj;
-                off[t][r] = ok ? (uint32_t)idx * 4u : kOOB;
-                // unconditional loads (no branch): one wait retires them, instead of a
-                // re-wait after every epilogue store
-                const uint32_t lo = (upd && kh == 0) ? off[t][r] : kOOB;
-                th[t][r] = bld(bth, lo);
-                ac[t][r] = bld(bac, lo);
-            }
-        }
-    };
-    if constexpr (DA3) {
-        prefetch_opt();
-        load_panels(0);
-        d3.load(p.da3, 0, j0);
-    } else {
-        load_panels(0);
-        prefetch_opt();
-    }
-
-    int kb = 0;
-    do {  // K >= 1 always; a do-loop keeps the pre-loop loads off the exit path
-        if (kb > 0) load_panels(kb);
-        if constexpr (DA3) {
-            if (kb > 0) d3.load(p.da3, kb, j0);
-            d3.form(p.da3, kb, j0, i0 == 0, sb);
-        }
+        if constexpr (DA3) da3_panel<NWV, TS>(p.da3, kb, j0, i0 == 0, sb);
 #pragma unroll
         for (int u = 0; u < NU; ++u) {
             const int e = threadIdx.x + NTH * u;
@@ -447,7 +415,6 @@ DEV void wgrad_body(const WA& p, const WGroup& g, int bid, float (*sa)[kWP], flo
             if constexpr (!DA3) *reinterpret_cast<f32x4*>(&sb[kr][4 * c4]) = rb[u];
         }
         __syncthreads();
-        if (p.dbg && threadIdx.x == 0 && kb == 0) p.dbg[bid * 8 + 2] = __builtin_amdgcn_s_memrealtime();
         const int nch = min(kWKB, g.K - kb) >> 4;
         for (int c = kh; c < nch; c += NWV / 4) {
             const int kk = 16 * c + 4 * q;

@@ -11,7 +11,7 @@
 //      sc/2 (1 - e^lv)), or the LA direct terms (VAEB.py:315-346).
 //
 // dA3 = ([dMu | dLv] [W4 | W5]^T) (1 - h^2) is then formed inside the dW3 workgroups of the
-// last launch (kernels_aux.hpp: Da3Panel), so the former dz / dh launch -- 56 workgroups
+// last launch (kernels_aux.hpp: da3_panel), so the former dz / dh launch -- 56 workgroups
 // that each recomputed dZ from 72 KB of dA1 and W1 -- and its kernel boundary are gone.
 //
 // Slab hand-off: the encoder's form (latent.hpp arrive_last and the guide rule cited
