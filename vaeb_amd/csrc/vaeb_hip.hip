@@ -150,7 +150,6 @@ struct vaeb_ctx {
     int atomic_ho = 1;            // folded latent hand-offs: 1 by fan-in (ho_mode), 0 slabs, 2 ticketed atomics
     bool decout_2b = true;        // bf16 Bernoulli decout on 256 x 128 tiles, 2 blocks / CU (VAEB_DECOUT_2B=0: 256 x 256)
     bool bf_fuse = true;          // bf16 engine: dhd + dW2 (| dW6) in one grid (VAEB_BF_FUSE=0: two launches)
-    int num_cus = 256;            // compute units of the device (hipDeviceProp_t)
     // profiling
     hipEvent_t pev[kMaxProfKernels + 1] = {};
     int prof_n = 0, prof_reps = 1;
@@ -911,11 +910,6 @@ int vaeb_create(const vaeb_config* cfg, vaeb_ctx** out) {
     if (c->c.max_eval_rows <= 0) c->c.max_eval_rows = 10000;
     hipError_t e = hipSetDevice(g.device);
     if (e != hipSuccess) { delete c; return fail(VAEB_ERR_HIP, "hipSetDevice(%d): %s", g.device, hipGetErrorString(e)); }
-    {
-        hipDeviceProp_t prop;
-        if (hipGetDeviceProperties(&prop, g.device) == hipSuccess && prop.multiProcessorCount > 0)
-            c->num_cus = prop.multiProcessorCount;
-    }
     e = hipStreamCreateWithFlags(&c->s, hipStreamNonBlocking);
     if (const char* ds = getenv("VAEB_DZ_SPLIT")) c->dz_split = atoi(ds);
     if (const char* fb = getenv("VAEB_FOLD_BWD")) c->fold_bwd = atoi(fb) != 0;
