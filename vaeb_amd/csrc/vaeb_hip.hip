@@ -141,6 +141,9 @@ struct vaeb_ctx {
     // comm
     ncclComm_t comm = nullptr;
     int rank = 0, world = 1;
+    hipStream_t s3 = nullptr;     // bf16 engine: dW2 (| dW6) + Adagrad forked beside the backward chain
+    hipEvent_t fk_ev[3] = {};     // fork after dhd, s3's work done, [dMu | dLv] ready
+    bool bf_fork = true;          // VAEB_BF_FORK=0: dW2 in the dhd grid (bf_fuse) or after it
     hipStream_t s2 = nullptr;     // DP: the gradient buckets' all-reduces and their Adagrad
     hipEvent_t dp_ev[3] = {};     // fork after dW2, bucket A reduced, bucket A updated
     bool dp_overlap = false;      // bucket A on s2 (bf16 engine; VAEB_DP_OVERLAP=0/1 overrides)
@@ -915,6 +918,7 @@ int vaeb_create(const vaeb_config* cfg, vaeb_ctx** out) {
     if (const char* fb = getenv("VAEB_FOLD_BWD")) c->fold_bwd = atoi(fb) != 0;
     if (const char* ts = getenv("VAEB_W3_TS")) c->w3_ts = atoi(ts) == 2 ? 2 : 1;
     if (const char* bf = getenv("VAEB_BF_FUSE")) c->bf_fuse = atoi(bf) != 0;
+    if (const char* bk = getenv("VAEB_BF_FORK")) c->bf_fork = atoi(bk) != 0;
     if (const char* d2 = getenv("VAEB_DECOUT_2B")) c->decout_2b = atoi(d2) != 0;
     if (const char* ah = getenv("VAEB_ATOMIC_HO")) c->atomic_ho = atoi(ah);
     if (e != hipSuccess) { delete c; return fail(VAEB_ERR_HIP, "stream/event create: %s", hipGetErrorString(e)); }
@@ -973,6 +977,13 @@ int vaeb_create(const vaeb_config* cfg, vaeb_ctx** out) {
         rc = rc ? rc : dalloc(&c->acc_dz, (size_t)(Bp * 2 * Z * kFxStride));
     }
     if (!rc && is_bf16(c)) rc = bf_alloc(c);
+    if (!rc && is_bf16(c)) {
+        if (hipStreamCreateWithFlags(&c->s3, hipStreamNonBlocking) != hipSuccess ||
+            hipEventCreateWithFlags(&c->fk_ev[0], hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&c->fk_ev[1], hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&c->fk_ev[2], hipEventDisableTiming) != hipSuccess)
+            rc = fail(VAEB_ERR_HIP, "fork stream / events");
+    }
     if (rc) { vaeb_destroy(c); return rc; }
     if (hipHostMalloc((void**)&c->h_ctl, sizeof(int) * (kCtlOrder + kOrderCap), 0) != hipSuccess ||
         hipHostMalloc((void**)&c->h_elbo, sizeof(float) * 4, 0) != hipSuccess ||
@@ -992,6 +1003,7 @@ int vaeb_destroy(vaeb_ctx* c) {
     if (!c) return 0;
     if (c->s) hipStreamSynchronize(c->s);
     if (c->s2) hipStreamSynchronize(c->s2);
+    if (c->s3) hipStreamSynchronize(c->s3);
     free_graphs(c);
     bf_free(c);
     if (c->comm) ncclCommDestroy(c->comm);
@@ -1014,6 +1026,8 @@ int vaeb_destroy(vaeb_ctx* c) {
     if (c->ctl_ev) hipEventDestroy(c->ctl_ev);
     for (auto& ev : c->pev) if (ev) hipEventDestroy(ev);
     for (auto& ev : c->dp_ev) if (ev) hipEventDestroy(ev);
+    for (auto& ev : c->fk_ev) if (ev) hipEventDestroy(ev);
+    if (c->s3) hipStreamDestroy(c->s3);
     if (c->s2) hipStreamDestroy(c->s2);
     if (c->s) hipStreamDestroy(c->s);
     delete c;
