@@ -250,39 +250,49 @@ DEV void fv_stream_block(const FvFold& a, int fb, int nfb, double* sh) {
 // completes an element stores mu or lv (+ bias).  Meanwhile waves 1-7 of column tile 0
 // write the row block's eps (Philox keyed by the global row, the host buffer, or 0); z and
 // the KL / LA terms are formed by decout_z_kernel<.., AT>.
-template <int NCT, int GCH, bool FV, int HO>
+// The encoder over CT 16-column h tiles per workgroup (wave_mainloop's NB = CT B operands).
+struct PEncCT : PEnc {
+    DEV f32x4 b4(int n, int k, int w) const { return mc4(bw, a.H, n + 16 * w, k, a.H, a.D); }
+};
+
+// CT: h column tiles per workgroup (1, or 2: half the contributors per latent element).
+template <int NCT, int GCH, bool FV, int HO, int CT = 1>
 DEV void enc_latent_body(const StepArgs& a, const FvFold& fvf) {
     constexpr bool AT = HO == 1;
-    __shared__ f32x4 red[512];
-    __shared__ float hs[16][20];
+    __shared__ f32x4 red[512 * CT];
+    __shared__ float hs[16][16 * CT + 4];
     __shared__ int sflag;
     __shared__ float pm[HO ? 64 : 1][17];   // HO: the tile's [mu | lv] partials, [column][row]
-    const int nctH = FV ? (a.H + 15) >> 4 : (int)gridDim.y;   // FV: rows beyond run the stream
+    // contributors per row block: the grid's column workgroups (FV: rows beyond run the stream)
+    const int nctH = FV ? (a.H + 16 * CT - 1) / (16 * CT) : (int)gridDim.y;
     if (FV && (int)blockIdx.y >= nctH) {
         fv_stream_block(fvf, (blockIdx.y - nctH) * gridDim.x + blockIdx.x, (gridDim.y - nctH) * gridDim.x,
                         reinterpret_cast<double*>(red));
         return;
     }
     VAEB_STAMP(a, 0);
-    PEnc p{a, nullptr, a.Mbp, a.H, a.D};
+    PEncCT p{PEnc{a, nullptr, a.Mbp, a.H, a.D}};
     p.prepare();
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int li = lane & 15, q = lane >> 4;
     const int lin = xcd_remap(blockIdx.x + blockIdx.y * gridDim.x, gridDim.x * nctH);
     const int bx = lin % gridDim.x, by = lin / gridDim.x;
-    const int m0 = bx * 16, n0 = by * 16;
+    const int m0 = bx * 16, n0 = by * 16 * CT;
     const int Z = a.Z, H = a.H;
     const rsrc_t bs = mkbuf(a.slab_ml, (int64_t)gridDim.x * nctH * 2 * Z * 16 * 4);
 
-    PEnc::Pre pre{};
-    f32x4 bw[2 * NCT];
+    PEnc::Pre pre[CT] = {};
+    f32x4 bw[CT][2 * NCT];
     if (wave == 0) {
-        pre = p.prefetch(m0, n0);
         const rsrc_t bw4 = mkbuf(a.W4, (int64_t)H * Z * 4), bw5 = mkbuf(a.W5, (int64_t)H * Z * 4);
 #pragma unroll
-        for (int ct = 0; ct < NCT; ++ct) {
-            bw[2 * ct] = mc4(bw4, Z, ct * 16 + li, n0 + 4 * q, Z, H);
-            bw[2 * ct + 1] = mc4(bw5, Z, ct * 16 + li, n0 + 4 * q, Z, H);
+        for (int c = 0; c < CT; ++c) {
+            pre[c] = p.prefetch(m0, n0 + 16 * c);
+#pragma unroll
+            for (int ct = 0; ct < NCT; ++ct) {
+                bw[c][2 * ct] = mc4(bw4, Z, ct * 16 + li, n0 + 16 * c + 4 * q, Z, H);
+                bw[c][2 * ct + 1] = mc4(bw5, Z, ct * 16 + li, n0 + 16 * c + 4 * q, Z, H);
+            }
         }
     }
     // AT: the bias of each element this thread may complete (column c: b4[c] | b5[c - Z])
@@ -296,32 +306,48 @@ DEV void enc_latent_body(const StepArgs& a, const FvFold& fvf) {
             bias[u] = bld(b4, ok && c < Z ? (uint32_t)c * 4u : kOOB) + bld(b5, ok && c >= Z ? (uint32_t)(c - Z) * 4u : kOOB);
         }
     }
-    f32x4 acc[1] = {zero4()};
-    wave_mainloop<1, 8, GCH>(p, m0 + li, n0 + li, p.K, wave, acc);
+    f32x4 acc[CT];
+#pragma unroll
+    for (int c = 0; c < CT; ++c) acc[c] = zero4();
+    wave_mainloop<CT, 8, GCH>(p, m0 + li, n0 + li, p.K, wave, acc);
     VAEB_STAMP(a, 1);
-    red[wave * 64 + lane] = acc[0];
+#pragma unroll
+    for (int c = 0; c < CT; ++c) red[(c * 8 + wave) * 64 + lane] = acc[c];
     __syncthreads();
     if (wave == 0) {
 #pragma unroll
-        for (int s = 1; s < 8; ++s) acc[0] += red[s * 64 + lane];
+        for (int c = 0; c < CT; ++c)
+#pragma unroll
+            for (int s = 1; s < 8; ++s) acc[c] += red[(c * 8 + s) * 64 + lane];
         if (a.order && bx == 0 && by == 0 && lane == 0) *a.cur_batch = a.cursor[kCtlNext];
-        const int n = n0 + li;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const int m = m0 + 4 * q + r;
-            const float hv = (m < a.Mb && n < H) ? ftanh(acc[0][r] + pre.b) : 0.f;
-            if (n < H) a.h[(int64_t)m * H + n] = hv;
-            hs[4 * q + r][li] = hv;
+        for (int c = 0; c < CT; ++c) {
+            const int n = n0 + 16 * c + li;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int m = m0 + 4 * q + r;
+                const float hv = (m < a.Mb && n < H) ? ftanh(acc[c][r] + pre[c].b) : 0.f;
+                if (n < H) a.h[(int64_t)m * H + n] = hv;
+                hs[4 * q + r][16 * c + li] = hv;
+            }
         }
-        // partial [mu|lv] of this tile: (16 x 16 h) . (16 rows of [W4|W5])
-        f32x4 av;
+        // partial [mu|lv] of this tile: (16 x 16 CT h) . (16 CT rows of [W4|W5])
+        f32x4 av[CT];
 #pragma unroll
-        for (int s = 0; s < 4; ++s) av[s] = hs[li][4 * q + s];
+        for (int c = 0; c < CT; ++c)
+#pragma unroll
+            for (int s = 0; s < 4; ++s) av[c][s] = hs[li][16 * c + 4 * q + s];
         const int64_t base = ((int64_t)bx * nctH + by) * 2 * Z;
+        auto part = [&](int w) {
+            f32x4 v = mfma4(av[0], bw[0][w], zero4());
+#pragma unroll
+            for (int c = 1; c < CT; ++c) v = mfma4(av[c], bw[c][w], v);
+            return v;
+        };
         if constexpr (HO != 0) {
 #pragma unroll
             for (int w = 0; w < 2 * NCT; ++w) {
-                const f32x4 sv = mfma4(av, bw[w], zero4());
+                const f32x4 sv = part(w);
                 const int nz = (w >> 1) * 16 + li;
                 if (nz < Z)
 #pragma unroll
@@ -330,7 +356,7 @@ DEV void enc_latent_body(const StepArgs& a, const FvFold& fvf) {
         } else {
 #pragma unroll
             for (int w = 0; w < 2 * NCT; ++w) {
-                const f32x4 sv = mfma4(av, bw[w], zero4());
+                const f32x4 sv = part(w);
                 const int nz = (w >> 1) * 16 + li;  // latent column of this lane
                 st4_sc1(bs, nz < Z ? (uint32_t)(((base + (w & 1) * Z + nz) * 16 + 4 * q) * 4) : kOOB, sv);
             }
@@ -471,13 +497,13 @@ DEV void enc_latent_body(const StepArgs& a, const FvFold& fvf) {
     }
     VAEB_STAMP(a, 5);
 }
-template <int NCT, int GCH, int HO>
+template <int NCT, int GCH, int HO, int CT>
 __global__ __launch_bounds__(512) void enc_latent_kernel(StepArgs a) {
-    enc_latent_body<NCT, GCH, false, HO>(a, FvFold{});
+    enc_latent_body<NCT, GCH, false, HO, CT>(a, FvFold{});
 }
-template <int NCT, int GCH, int HO>
+template <int NCT, int GCH, int HO, int CT>
 __global__ __launch_bounds__(512) void enc_latent_fv_kernel(StepArgs a, FvFold f) {
-    enc_latent_body<NCT, GCH, true, HO>(a, f);
+    enc_latent_body<NCT, GCH, true, HO, CT>(a, f);
 }
 
 // ----------------------------------------------------------------------------- P4'

@@ -151,6 +151,7 @@ struct vaeb_ctx {
     bool fold_bwd = true;         // Z <= 32: latent backward folded into the dhd launch (VAEB_FOLD_BWD=0: P67)
     int w3_ts = 1;                // folded path's last launch: tile width / 16 (VAEB_W3_TS)
     int atomic_ho = 1;            // folded latent hand-offs: 1 by fan-in (ho_mode), 0 slabs, 2 ticketed atomics
+    int enc_ct = 0;               // encoder h column tiles per workgroup: 0 auto, VAEB_ENC_CT=1|2 forces
     bool decout_2b = true;        // bf16 Bernoulli decout on 256 x 128 tiles, 2 blocks / CU (VAEB_DECOUT_2B=0: 256 x 256)
     bool bf_fuse = true;          // bf16 engine: dhd + dW2 (| dW6) in one grid (VAEB_BF_FUSE=0: two launches)
     // profiling
@@ -248,7 +249,7 @@ int ho_mode(const vaeb_ctx* c, int fan_in) {
     if (c->atomic_ho == 2) return 2;
     return fan_in <= kFxMaxFanIn ? 1 : 0;
 }
-int ho_ml(const vaeb_ctx* c) { return ho_mode(c, cdiv(c->c.H, 16)); }
+int ho_ml(const vaeb_ctx* c, int ct) { return ho_mode(c, cdiv(c->c.H, 16 * ct)); }
 int ho_dz(const vaeb_ctx* c) { return ho_mode(c, cdiv(c->c.H, 16) * c->c.L); }
 
 // Measurement brackets: mark(id) records an event before launch slot `id`.  With
@@ -322,23 +323,28 @@ void launch_dhd_dz(hipStream_t s, dim3 grid, const PDhdT<true>& p5, const PDhdT<
 
 // enc_latent_kernel / enc_latent_fv_kernel at compile-time NCT (latent col tiles), GCH
 // (main-loop chunk group), AT (atomic hand-off)
-template <int HO>
-void launch_enc_latent(hipStream_t s, dim3 g1, const StepArgs& a, const FvFold& fvf, bool deep) {
+template <int HO, int CT>
+void launch_enc_latent_ct(hipStream_t s, dim3 g1, const StepArgs& a, const FvFold& fvf, bool deep) {
     if (fvf.rows > 0) {
         if (a.Z <= 16) {
-            if (deep) hipLaunchKernelGGL((enc_latent_fv_kernel<1, 8, HO>), g1, dim3(512), 0, s, a, fvf);
-            else hipLaunchKernelGGL((enc_latent_fv_kernel<1, 4, HO>), g1, dim3(512), 0, s, a, fvf);
+            if (deep) hipLaunchKernelGGL((enc_latent_fv_kernel<1, 8, HO, CT>), g1, dim3(512), 0, s, a, fvf);
+            else hipLaunchKernelGGL((enc_latent_fv_kernel<1, 4, HO, CT>), g1, dim3(512), 0, s, a, fvf);
         } else {
-            if (deep) hipLaunchKernelGGL((enc_latent_fv_kernel<2, 8, HO>), g1, dim3(512), 0, s, a, fvf);
-            else hipLaunchKernelGGL((enc_latent_fv_kernel<2, 4, HO>), g1, dim3(512), 0, s, a, fvf);
+            if (deep) hipLaunchKernelGGL((enc_latent_fv_kernel<2, 8, HO, CT>), g1, dim3(512), 0, s, a, fvf);
+            else hipLaunchKernelGGL((enc_latent_fv_kernel<2, 4, HO, CT>), g1, dim3(512), 0, s, a, fvf);
         }
     } else if (a.Z <= 16) {
-        if (deep) hipLaunchKernelGGL((enc_latent_kernel<1, 8, HO>), g1, dim3(512), 0, s, a);
-        else hipLaunchKernelGGL((enc_latent_kernel<1, 4, HO>), g1, dim3(512), 0, s, a);
+        if (deep) hipLaunchKernelGGL((enc_latent_kernel<1, 8, HO, CT>), g1, dim3(512), 0, s, a);
+        else hipLaunchKernelGGL((enc_latent_kernel<1, 4, HO, CT>), g1, dim3(512), 0, s, a);
     } else {
-        if (deep) hipLaunchKernelGGL((enc_latent_kernel<2, 8, HO>), g1, dim3(512), 0, s, a);
-        else hipLaunchKernelGGL((enc_latent_kernel<2, 4, HO>), g1, dim3(512), 0, s, a);
+        if (deep) hipLaunchKernelGGL((enc_latent_kernel<2, 8, HO, CT>), g1, dim3(512), 0, s, a);
+        else hipLaunchKernelGGL((enc_latent_kernel<2, 4, HO, CT>), g1, dim3(512), 0, s, a);
     }
+}
+template <int HO>
+void launch_enc_latent(hipStream_t s, dim3 g1, const StepArgs& a, const FvFold& fvf, bool deep, int ct) {
+    if (ct == 2) launch_enc_latent_ct<HO, 2>(s, g1, a, fvf, deep);
+    else launch_enc_latent_ct<HO, 1>(s, g1, a, fvf, deep);
 }
 
 // Training minibatches with Z <= 32 fold the latent block into the wide phases
@@ -353,15 +359,19 @@ int enqueue_forward(vaeb_ctx* c, const StepArgs& a0, Prof& pr, const FvFold& fvf
     StepArgs a = a0;
     a.dbg = next_dbg(c);
     if (folded_latent(c, a)) {
-        const dim3 g1(a.Mbp / 16, cdiv(a.H, 16) + fvf.rows);
+        // auto: two column tiles per workgroup when the literal-FV stream shares the launch
+        // (FV 27.75 -> 27.4 us: fewer encoder tiles beside the stream blocks), else one
+        // (MNIST 44.6 either way, Frey 32.2 vs 34.0 us)
+        const int ct = c->enc_ct ? c->enc_ct : (fvf.rows > 0 ? 2 : 1);
+        const dim3 g1(a.Mbp / 16, cdiv(a.H, 16 * ct) + fvf.rows);
         const bool deep = cdiv(cdiv(a.D, 16), 8) > 4;
-        const int ho = ho_ml(c);
+        const int ho = ho_ml(c, ct);
         const bool at = ho == 1;
         pr.mark(16);
         REP(pr) {
-            if (ho == 1) launch_enc_latent<1>(s, g1, a, fvf, deep);
-            else if (ho == 2) launch_enc_latent<2>(s, g1, a, fvf, deep);
-            else launch_enc_latent<0>(s, g1, a, fvf, deep);
+            if (ho == 1) launch_enc_latent<1>(s, g1, a, fvf, deep, ct);
+            else if (ho == 2) launch_enc_latent<2>(s, g1, a, fvf, deep, ct);
+            else launch_enc_latent<0>(s, g1, a, fvf, deep, ct);
         }
         CHECK_LAUNCH();
         a.dbg = next_dbg(c);
@@ -920,6 +930,7 @@ int vaeb_create(const vaeb_config* cfg, vaeb_ctx** out) {
     if (const char* bf = getenv("VAEB_BF_FUSE")) c->bf_fuse = atoi(bf) != 0;
     if (const char* bk = getenv("VAEB_BF_FORK")) c->bf_fork = atoi(bk) != 0;
     if (const char* d2 = getenv("VAEB_DECOUT_2B")) c->decout_2b = atoi(d2) != 0;
+    if (const char* ec = getenv("VAEB_ENC_CT")) c->enc_ct = atoi(ec) == 2 ? 2 : 1;
     if (const char* ah = getenv("VAEB_ATOMIC_HO")) c->atomic_ho = atoi(ah);
     if (e != hipSuccess) { delete c; return fail(VAEB_ERR_HIP, "stream/event create: %s", hipGetErrorString(e)); }
     const int64_t D = g.D, H = g.H, Z = g.Z;
