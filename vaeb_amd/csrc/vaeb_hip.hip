@@ -144,6 +144,7 @@ struct vaeb_ctx {
     hipStream_t s3 = nullptr;     // bf16 engine: dW2 (| dW6) + Adagrad forked beside the backward chain
     hipEvent_t fk_ev[3] = {};     // fork after dhd, s3's work done, [dMu | dLv] ready
     bool bf_fork = true;          // VAEB_BF_FORK=0: dW2 in the dhd grid (bf_fuse) or after it
+    bool w3_256 = true;           // forked step: dW3 on 256 x 256 tiles beside dW2 (VAEB_BF_W3_256=0: 256 x 128)
     hipStream_t s2 = nullptr;     // DP: the gradient buckets' all-reduces and their Adagrad
     hipEvent_t dp_ev[3] = {};     // fork after dW2, bucket A reduced, bucket A updated
     bool dp_overlap = false;      // bucket A on s2 (bf16 engine; VAEB_DP_OVERLAP=0/1 overrides)
@@ -929,6 +930,7 @@ int vaeb_create(const vaeb_config* cfg, vaeb_ctx** out) {
     if (const char* ts = getenv("VAEB_W3_TS")) c->w3_ts = atoi(ts) == 2 ? 2 : 1;
     if (const char* bf = getenv("VAEB_BF_FUSE")) c->bf_fuse = atoi(bf) != 0;
     if (const char* bk = getenv("VAEB_BF_FORK")) c->bf_fork = atoi(bk) != 0;
+    if (const char* w3 = getenv("VAEB_BF_W3_256")) c->w3_256 = atoi(w3) != 0;
     if (const char* d2 = getenv("VAEB_DECOUT_2B")) c->decout_2b = atoi(d2) != 0;
     if (const char* ec = getenv("VAEB_ENC_CT")) c->enc_ct = atoi(ec) == 2 ? 2 : 1;
     if (const char* ah = getenv("VAEB_ATOMIC_HO")) c->atomic_ho = atoi(ah);
