@@ -486,8 +486,8 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WGradArgs p) {
 }
 
 // The folded latent backward's last launch: dW3 (dA3 formed in the workgroup) | dW4 | dW5
-// | dW1, and the ELBO workgroup first.
-template <bool VEC, int TS>
+// | dW1, and the ELBO workgroup first.  VM: bit g = group g's panels take 16-byte loads.
+template <int VM, int TS>
 __global__ __launch_bounds__(256) void wgrad3_kernel(WGradArgs3 p) {
     __shared__ float sa[kWKB][kWP];
     __shared__ float sb[kWKB][kWP];
@@ -501,9 +501,9 @@ __global__ __launch_bounds__(256) void wgrad3_kernel(WGradArgs3 p) {
         elbo_reduce(p.elbo, reinterpret_cast<double*>(&sa[0][0]));
         return;
     }
-    if (bid >= p.g[2].wg_begin) wgrad_body<VEC, 4, TS>(p, p.g[2], bid, sa, sb);
-    else if (bid >= p.g[1].wg_begin) wgrad_body<VEC, 4, TS>(p, p.g[1], bid, sa, sb);
-    else wgrad_body<VEC, 4, TS, true>(p, p.g[0], bid, sa, sb);
+    if (bid >= p.g[2].wg_begin) wgrad_body<(VM & 4) != 0, 4, TS>(p, p.g[2], bid, sa, sb);
+    else if (bid >= p.g[1].wg_begin) wgrad_body<(VM & 2) != 0, 4, TS>(p, p.g[1], bid, sa, sb);
+    else wgrad_body<(VM & 1) != 0, 4, TS, true>(p, p.g[0], bid, sa, sb);
 }
 
 // ----------------------------------------------------------------- DP optimizer

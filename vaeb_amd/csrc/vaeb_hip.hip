@@ -16,6 +16,7 @@
 #include <cstring>
 #include <string>
 #include <vector>
+#include <type_traits>
 
 #include "../../include/vaeb_diag.h"   // includes vaeb_hip.h
 #include "hfuse.hpp"
@@ -151,6 +152,7 @@ struct vaeb_ctx {
     int dz_split = 8;             // P67 column splits per row block (fused.hpp dz_dh_body; VAEB_DZ_SPLIT)
     bool fold_bwd = true;         // Z <= 32: latent backward folded into the dhd launch (VAEB_FOLD_BWD=0: P67)
     int w3_ts = 1;                // folded path's last launch: tile width / 16 (VAEB_W3_TS)
+    bool w3_gvec = true;          // ... 16-byte panel loads decided per group (VAEB_W3_GVEC)
     int atomic_ho = 1;            // folded latent hand-offs: 1 by fan-in (ho_mode), 0 slabs, 2 ticketed atomics
     int enc_ct = 0;               // encoder h column tiles per workgroup: 0 auto, VAEB_ENC_CT=1|2 forces
     bool decout_2b = true;        // bf16 Bernoulli decout on 256 x 128 tiles, 2 blocks / CU (VAEB_DECOUT_2B=0: 256 x 256)
@@ -453,7 +455,7 @@ constexpr int kWTJ_W = 16;     // standalone launches: dW3 | dW45 (+ ELBO), non-
 // launch (+ the ELBO workgroup when e != nullptr).  *vec: 16-byte panel loads are legal.
 template <class WA>
 int prep_wgrad(vaeb_ctx* c, const WGroup* groups, int n, const OptArgs& opt, const ElboArgs* e, const StepArgs& a,
-               int base, WA& w, bool& vec, int tw) {
+               int base, WA& w, bool& vec, int tw, int* vmask = nullptr) {
     w = WA{};
     int begin = base;
     constexpr int kMaxG = (int)(sizeof(w.g) / sizeof(w.g[0]));
@@ -476,12 +478,15 @@ int prep_wgrad(vaeb_ctx* c, const WGroup* groups, int n, const OptArgs& opt, con
     // 16-byte panel loads need every panel row aligned with widths % 4 == 0 (the
     // activation buffers are hipMalloc'd; X rows are D floats apart)
     vec = true;
+    if (vmask) *vmask = 0;
     auto al = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
     for (int gi = 0; gi < n; ++gi) {
         const WGroup& G = w.g[gi];
-        vec = vec && (G.ld_at % 4 == 0) && (G.rowsW % 4 == 0) && (G.at_is_x ? al(a.xbase) : al(G.at)) &&
-              (G.ld0 % 4 == 0) && (G.N0 % 4 == 0) && al(G.b0) &&
-              (G.N1 == 0 || ((G.ld1 % 4 == 0) && (G.N1 % 4 == 0) && al(G.b1)));
+        const bool gv = (G.ld_at % 4 == 0) && (G.rowsW % 4 == 0) && (G.at_is_x ? al(a.xbase) : al(G.at)) &&
+                        (G.ld0 % 4 == 0) && (G.N0 % 4 == 0) && al(G.b0) &&
+                        (G.N1 == 0 || ((G.ld1 % 4 == 0) && (G.N1 % 4 == 0) && al(G.b1)));
+        vec = vec && gv;
+        if (vmask && gv) *vmask |= 1 << gi;
     }
     return 0;
 }
@@ -495,16 +500,23 @@ int launch_wgrad(vaeb_ctx* c, hipStream_t s, const WGroup* groups, int n, const 
         if (n != 3) return fail(VAEB_ERR_ARG, "internal: the dA3-forming launch takes three groups");
         WGradArgs3 w;
         const int tw = c->w3_ts * 16;
-        if (int rc = prep_wgrad(c, groups, n, opt, e, a, 0, w, vec, tw)) return rc;
+        int vm = 0;   // 16-byte panel loads per group (Frey: dW3 yes, dW4 | dW5 and dW1 not)
+        if (int rc = prep_wgrad(c, groups, n, opt, e, a, 0, w, vec, tw, &vm)) return rc;
         w.da3 = *da3;
+        if (!c->w3_gvec) vm = vec ? 7 : 0;
         const dim3 grid(w.total_wgs + (e ? 1 : 0));
-        if (tw == 32) {
-            if (vec) hipLaunchKernelGGL((wgrad3_kernel<true, 2>), grid, dim3(256), 0, s, w);
-            else hipLaunchKernelGGL((wgrad3_kernel<false, 2>), grid, dim3(256), 0, s, w);
-        } else {
-            if (vec) hipLaunchKernelGGL((wgrad3_kernel<true, 1>), grid, dim3(256), 0, s, w);
-            else hipLaunchKernelGGL((wgrad3_kernel<false, 1>), grid, dim3(256), 0, s, w);
-        }
+        auto go = [&](auto ts) {
+            constexpr int TS = decltype(ts)::value;
+            switch (vm) {
+                case 7: hipLaunchKernelGGL((wgrad3_kernel<7, TS>), grid, dim3(256), 0, s, w); break;
+                case 1: hipLaunchKernelGGL((wgrad3_kernel<1, TS>), grid, dim3(256), 0, s, w); break;
+                case 3: hipLaunchKernelGGL((wgrad3_kernel<3, TS>), grid, dim3(256), 0, s, w); break;
+                case 5: hipLaunchKernelGGL((wgrad3_kernel<5, TS>), grid, dim3(256), 0, s, w); break;
+                default: hipLaunchKernelGGL((wgrad3_kernel<0, TS>), grid, dim3(256), 0, s, w); break;
+            }
+        };
+        if (tw == 32) go(std::integral_constant<int, 2>{});
+        else go(std::integral_constant<int, 1>{});
     } else {
         WGradArgs w;
         if (int rc = prep_wgrad(c, groups, n, opt, e, a, 0, w, vec, kWTJ_W)) return rc;
@@ -928,6 +940,7 @@ int vaeb_create(const vaeb_config* cfg, vaeb_ctx** out) {
     if (const char* ds = getenv("VAEB_DZ_SPLIT")) c->dz_split = atoi(ds);
     if (const char* fb = getenv("VAEB_FOLD_BWD")) c->fold_bwd = atoi(fb) != 0;
     if (const char* ts = getenv("VAEB_W3_TS")) c->w3_ts = atoi(ts) == 2 ? 2 : 1;
+    if (const char* gv = getenv("VAEB_W3_GVEC")) c->w3_gvec = atoi(gv) != 0;
     if (const char* bf = getenv("VAEB_BF_FUSE")) c->bf_fuse = atoi(bf) != 0;
     if (const char* bk = getenv("VAEB_BF_FORK")) c->bf_fork = atoi(bk) != 0;
     if (const char* w3 = getenv("VAEB_BF_W3_256")) c->w3_256 = atoi(w3) != 0;
