@@ -108,3 +108,19 @@ def test_vaeb_class_fv_weight_sampling_extension():
         assert not np.array_equal(fvp[0], theta[0])
         m.close()
     assert runs[0][0] == runs[1][0] and np.array_equal(runs[0][1], runs[1][1])
+
+
+def test_vaeb_optimizer_plugin_binds_the_engine_rule():
+    """inf=AdaGrad(eta) (degenerate-vae/infalg.py contract): eta becomes the engine's step
+    size, and the accumulators construct() hands out are views of the engine's arena."""
+    from vaeb_amd.infalg import AdaGrad
+    from vaeb_amd.model import VAEB
+    x = O.synthetic_mnist(n=400)
+    a = VAEB(x, False, 500, 20, 100, 1, 0.01, False, False, inf=AdaGrad(0.03))
+    b = VAEB(x, False, 500, 20, 100, 1, 0.03, False, False)
+    assert a.update(0) == b.update(0)
+    assert all(np.array_equal(p.get_value(), q.get_value()) for p, q in zip(a.params, b.params))
+    acc = a.updates[0][0]
+    assert np.array_equal(acc.get_value(), a.ADA[0])
+    acc.set_value(np.zeros_like(a.ADA[0]))
+    assert not a.ADA[0].any() and a.ADA[1].any()

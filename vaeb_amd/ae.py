@@ -14,7 +14,7 @@ from __future__ import annotations
 import numpy as np
 
 from . import _lib
-from .infalg import AdaGrad
+from .infalg import AdaGrad, bind_updates
 
 _ACT_NAMES = {"tanh": "tanh", "sigmoid": "sigmoid", "logistic": "sigmoid", "relu": "relu"}
 
@@ -66,6 +66,22 @@ class SharedParam:
         return f"SharedParam({self.name}, {self.shape})"
 
 
+class _AccArena:
+    """Owner of the AdaGrad accumulators `inf.construct` hands out (views of the engine's
+    accumulator arena, one slice per SharedParam)."""
+
+    def __init__(self, ctx):
+        self.ctx = ctx
+
+    def _acc_get(self, p):
+        return self.ctx.get_adagrad_state()[p.offset:p.offset + p.size].reshape(p.shape).copy()
+
+    def _acc_set(self, p, value):
+        flat = self.ctx.get_adagrad_state()
+        flat[p.offset:p.offset + p.size] = value.ravel()
+        self.ctx.set_adagrad_state(flat)
+
+
 def ConstructAE(Xtr, Denc=(500,), Dz=20, Ddec=(500,), f="tanh", s2=1.0, inf=None, otype="binary",
                 max_batch=None, device=0):
     """ae.py:41-117.  Returns (train, reconstruct, encode, decode, theta)."""
@@ -85,6 +101,10 @@ def ConstructAE(Xtr, Denc=(500,), Dz=20, Ddec=(500,), f="tanh", s2=1.0, inf=None
     ctx.set_params(np.concatenate([t.ravel() for t in theta0]))
     offs = np.cumsum([0] + [int(np.prod(s)) for _, s in shapes])
     theta = [SharedParam(ctx, n, s, int(o)) for (n, s), o in zip(shapes, offs[:-1])]
+    # ae.py:80: updates = inf.construct(logjoint, theta), bound to the engine's fused rule
+    arena = _AccArena(ctx)
+    updates = inf.construct(arena, theta)
+    bind_updates(arena, theta, updates)
 
     def train(idx):
         return ctx.train(np.asarray(idx, np.int32))

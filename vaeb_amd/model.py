@@ -12,6 +12,7 @@ import numpy as np
 
 from . import _lib
 from . import pickle_static
+from .infalg import AdaGrad, bind_updates
 
 PARAM_NAMES_BERNOULLI = ["W3", "W4", "W5", "W1", "W2", "b3", "b4", "b5", "b1", "b2"]
 PARAM_NAMES_GAUSSIAN = ["W3", "W4", "W5", "W1", "W2", "W6", "b3", "b4", "b5", "b1", "b2", "b6"]
@@ -96,8 +97,11 @@ class VAEB:
     def __init__(self, x_train, continuous, hidden_units, latent_size, batch_size, L, learning_rate,
                  genericEstimator, fullVariational, params=None, prng=None, sigmaInit=None, *,
                  device=0, rng="philox", seed=10, objective="sum_prior", use_graph=True, max_eval_rows=10000,
-                 B_global=None, row_offset=0, fv_sample=False):
+                 B_global=None, row_offset=0, fv_sample=False, inf=None):
         x_train = np.asarray(x_train, np.float32)
+        if inf is not None:
+            # optimizer plug-in (degenerate-vae/infalg.py contract): its eta is the step size
+            learning_rate = inf.eta
         self.N, self.input_size = x_train.shape
         self.n_hidden_units = hidden_units
         self.n_latent = latent_size
@@ -134,6 +138,10 @@ class VAEB:
             arrs = [np.asarray(_as_array(p), np.float32).reshape(s) for p, (_, s) in zip(params, self._shapes)]
         self._ctx.set_params(np.concatenate([a.ravel() for a in arrs]))
         self.params = [SharedParam(self, i, n, s) for i, (n, s) in enumerate(self._shapes)]
+        # the update list of VAEB.getUpdates (VAEB.py:426-444) in the infalg.construct form,
+        # bound to the fused Adagrad epilogues of the engine
+        self.updates = (inf or AdaGrad(learning_rate)).construct(self, self.params)
+        bind_updates(self, self.params, self.updates)
         if self.fullVariational:
             # VAEB.py:120-125: mu_theta = theta, sigma_theta = 1e-3; Adagrad state zero (:178-182)
             flat = np.concatenate([a.ravel() for a in arrs])
@@ -182,6 +190,20 @@ class VAEB:
             out.append(acc[o:o + n].reshape(s))
             o += n
         return out
+
+    def _acc_slice(self, param):
+        o = sum(int(np.prod(s)) for _, s in self._shapes[:param._i])
+        return o, o + int(np.prod(param.shape))
+
+    def _acc_get(self, param):
+        a, b = self._acc_slice(param)
+        return self._ctx.get_adagrad_state()[a:b].reshape(param.shape).copy()
+
+    def _acc_set(self, param, value):
+        a, b = self._acc_slice(param)
+        flat = self._ctx.get_adagrad_state()
+        flat[a:b] = value.ravel()
+        self._ctx.set_adagrad_state(flat)
 
     # ------------------------------------------------------------------ the operators
     def update(self, index):
