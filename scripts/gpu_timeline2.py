@@ -3,6 +3,9 @@ one eager MNIST 784-500-20 step (10 ns ticks from the launch's first workgroup s
 import os
 import sys
 
+# the stamps exist only in the VAEB_TIMELINE build (__graft_entry__.build_variant('tl', 'VAEB_TIMELINE'))
+os.environ.setdefault("VAEB_LIB_VARIANT", "tl")
+
 import numpy as np
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))

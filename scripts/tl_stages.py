@@ -4,6 +4,9 @@ the workgroups that wrote it."""
 import os
 import sys
 
+# the stamps exist only in the VAEB_TIMELINE build (__graft_entry__.build_variant('tl', 'VAEB_TIMELINE'))
+os.environ.setdefault("VAEB_LIB_VARIANT", "tl")
+
 import numpy as np
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))

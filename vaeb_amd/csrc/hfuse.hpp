@@ -24,7 +24,7 @@ __global__ __launch_bounds__(512) void tile_wgrad_kernel(P p0, WGradArgs w, int 
     // XCDs, each XCD's share contiguous in tile order
     // the weight-gradient blocks take the low block indices (dispatched first: their
     // Adagrad epilogue makes them the longer pole; dhd | dW2 8.55 vs 9.12 us)
-    const int nwg = (int)gridDim.x - ntile;
+    const int nwg = w.total_wgs - ntile;   // grid = w.total_wgs
     const int b0 = (int)blockIdx.x < nwg ? (int)blockIdx.x + ntile : (int)blockIdx.x - nwg;
     const int bid = b0 < ntile ? xcd_remap(b0, ntile) : ntile + xcd_remap(b0 - ntile, nwg);
     if (bid < ntile) {
@@ -33,7 +33,7 @@ __global__ __launch_bounds__(512) void tile_wgrad_kernel(P p0, WGradArgs w, int 
         tile_body<WM, WN, KS, NB, GCH, P>(p, bid % gx, bid / gx);
         return;
     }
-    if (w.dbg && threadIdx.x == 0) w.dbg[bid * 8 + 0] = __builtin_amdgcn_s_memrealtime();
+    if (VAEB_DBG_ON(w.dbg) && threadIdx.x == 0) w.dbg[bid * 8 + 0] = __builtin_amdgcn_s_memrealtime();
     wgrad_body<VEC, 8, TS>(w, w.g[0], bid, sa, sb);
 }
 
@@ -51,7 +51,7 @@ __global__ __launch_bounds__(512) void dz_dh_wgrad_kernel(StepArgs a, WGradArgs 
         dz_dh_body<NCT>(a, (bid % nrb) * 16, bid / nrb, nrow / nrb);
         return;
     }
-    if (w.dbg && threadIdx.x == 0) w.dbg[bid * 8 + 0] = __builtin_amdgcn_s_memrealtime();
+    if (VAEB_DBG_ON(w.dbg) && threadIdx.x == 0) w.dbg[bid * 8 + 0] = __builtin_amdgcn_s_memrealtime();
     wgrad_body<VEC, 8, TS>(w, w.g[0], bid, sa, sb);
 }
 

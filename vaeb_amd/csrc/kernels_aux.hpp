@@ -442,7 +442,7 @@ DEV void wgrad_body(const WA& p, const WGroup& g, int bid, float (*sa)[kWP], flo
 #pragma unroll
         for (int t = 0; t < kWTS; ++t) acc[t] += red[(wave * 4 + t) * 64 + lane];
     }
-    if (p.dbg && threadIdx.x == 0) p.dbg[bid * 8 + 1] = __builtin_amdgcn_s_memrealtime();
+    if (VAEB_DBG_ON(p.dbg) && threadIdx.x == 0) p.dbg[bid * 8 + 1] = __builtin_amdgcn_s_memrealtime();
 
     // ---- epilogue: out-of-range byte offsets make masked buffer stores no-ops
     const rsrc_t bto = mkbuf(p.opt.theta_out, p.P * 4), bgr = mkbuf(p.opt.grad, p.P * 4);
@@ -459,7 +459,7 @@ DEV void wgrad_body(const WA& p, const WGroup& g, int bid, float (*sa)[kWP], flo
                 bst_opt(bto, off[t][r], nt);
             }
         }
-    if (p.dbg && threadIdx.x == 0) p.dbg[bid * 8 + 3] = __builtin_amdgcn_s_memrealtime();
+    if (VAEB_DBG_ON(p.dbg) && threadIdx.x == 0) p.dbg[bid * 8 + 3] = __builtin_amdgcn_s_memrealtime();
 }
 
 template <bool VEC, int TS>
@@ -476,7 +476,7 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WGradArgs p) {
         bid = blockIdx.x == 0 ? p.total_wgs : xcd_remap((int)blockIdx.x - 1, p.total_wgs);
     else
         bid = (int)blockIdx.x < p.total_wgs ? xcd_remap(blockIdx.x, p.total_wgs) : (int)blockIdx.x;
-    if (p.dbg && threadIdx.x == 0) p.dbg[bid * 8 + 0] = __builtin_amdgcn_s_memrealtime();
+    if (VAEB_DBG_ON(p.dbg) && threadIdx.x == 0) p.dbg[bid * 8 + 0] = __builtin_amdgcn_s_memrealtime();
     if (bid >= p.total_wgs) {  // the extra workgroup: ELBO of this step
         elbo_reduce(p.elbo, reinterpret_cast<double*>(&sa[0][0]));
         return;
@@ -496,7 +496,7 @@ __global__ __launch_bounds__(256) void wgrad3_kernel(WGradArgs3 p) {
         bid = blockIdx.x == 0 ? p.total_wgs : xcd_remap((int)blockIdx.x - 1, p.total_wgs);
     else
         bid = xcd_remap(blockIdx.x, p.total_wgs);
-    if (p.dbg && threadIdx.x == 0) p.dbg[bid * 8 + 0] = __builtin_amdgcn_s_memrealtime();
+    if (VAEB_DBG_ON(p.dbg) && threadIdx.x == 0) p.dbg[bid * 8 + 0] = __builtin_amdgcn_s_memrealtime();
     if (bid >= p.total_wgs) {
         elbo_reduce(p.elbo, reinterpret_cast<double*>(&sa[0][0]));
         return;

@@ -264,10 +264,12 @@ DEV void enc_latent_body(const StepArgs& a, const FvFold& fvf) {
     __shared__ int sflag;
     __shared__ float pm[HO ? 64 : 1][17];   // HO: the tile's [mu | lv] partials, [column][row]
     // contributors per row block: the grid's column workgroups (FV: rows beyond run the stream)
-    const int nctH = FV ? (a.H + 16 * CT - 1) / (16 * CT) : (int)gridDim.y;
+    // (grid extents from the arguments, not gridDim: reading the implicit arguments put one
+    // more dependent scalar round trip ahead of every workgroup's first operand load)
+    const int nctH = (a.H + 16 * CT - 1) / (16 * CT);
+    const int gxE = a.Mbp >> 4;   // grid: (Mbp / 16, nctH (+ FV stream rows))
     if (FV && (int)blockIdx.y >= nctH) {
-        fv_stream_block(fvf, (blockIdx.y - nctH) * gridDim.x + blockIdx.x, (gridDim.y - nctH) * gridDim.x,
-                        reinterpret_cast<double*>(red));
+        fv_stream_block(fvf, (blockIdx.y - nctH) * gxE + blockIdx.x, fvf.rows * gxE, reinterpret_cast<double*>(red));
         return;
     }
     VAEB_STAMP(a, 0);
@@ -275,11 +277,11 @@ DEV void enc_latent_body(const StepArgs& a, const FvFold& fvf) {
     p.prepare();
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int li = lane & 15, q = lane >> 4;
-    const int lin = xcd_remap(blockIdx.x + blockIdx.y * gridDim.x, gridDim.x * nctH);
-    const int bx = lin % gridDim.x, by = lin / gridDim.x;
+    const int lin = xcd_remap(blockIdx.x + blockIdx.y * gxE, gxE * nctH);
+    const int bx = lin % gxE, by = lin / gxE;
     const int m0 = bx * 16, n0 = by * 16 * CT;
     const int Z = a.Z, H = a.H;
-    const rsrc_t bs = mkbuf(a.slab_ml, (int64_t)gridDim.x * nctH * 2 * Z * 16 * 4);
+    const rsrc_t bs = mkbuf(a.slab_ml, (int64_t)gxE * nctH * 2 * Z * 16 * 4);
 
     PEnc::Pre pre[CT] = {};
     f32x4 bw[CT][2 * NCT];
@@ -528,8 +530,9 @@ __global__ __launch_bounds__(512, 4) void decout_z_kernel(StepArgs a) {
     p.prepare_at(nullptr);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int li = lane & 15, q = lane >> 4;
-    const int lin = xcd_remap(blockIdx.x + blockIdx.y * gridDim.x, gridDim.x * gridDim.y);
-    const int bxr = lin % gridDim.x, byr = lin / gridDim.x;
+    const int gx = a.Me >> 4, gy = (a.D + 15) >> 4;   // the grid (no implicit-argument load)
+    const int lin = xcd_remap(blockIdx.x + blockIdx.y * gx, gx * gy);
+    const int bxr = lin % gx, byr = lin / gx;
     const int m0 = bxr * 16, n0 = byr * 16;
     const int Z = a.Z, H = a.H;
     const bool col0 = byr == 0;

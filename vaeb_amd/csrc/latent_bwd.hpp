@@ -272,14 +272,14 @@ template <int NCT, int GCH, bool VEC, int TS, int HO>
 __global__ __launch_bounds__(512) void dhd_dz_wgrad_kernel(PDhdT<VEC> p, WGradArgs w, int ntile, int gx) {
     __shared__ float sa[kWKB][kWP];
     __shared__ float sb[kWKB][kWP];
-    const int nwg = (int)gridDim.x - ntile;
+    const int nwg = w.total_wgs - ntile;   // grid = w.total_wgs (no implicit-argument load)
     const int b0 = blockIdx.x;
     const int bid = b0 < ntile ? xcd_remap(b0, ntile) : ntile + xcd_remap(b0 - ntile, nwg);
     if (bid < ntile) {
         dhd_dz_body<NCT, GCH, VEC, HO>(p, bid % gx, bid / gx, reinterpret_cast<f32x4*>(&sa[0][0]), bid);
         return;
     }
-    if (w.dbg && threadIdx.x == 0) w.dbg[bid * 8 + 0] = __builtin_amdgcn_s_memrealtime();
+    if (VAEB_DBG_ON(w.dbg) && threadIdx.x == 0) w.dbg[bid * 8 + 0] = __builtin_amdgcn_s_memrealtime();
     wgrad_body<VEC, 8, TS>(w, w.g[0], bid, sa, sb);
 }
 

@@ -233,6 +233,200 @@ __global__ __launch_bounds__(256) void latent_bwd_kernel(LatentArgs a) {
         a.colpart[(int64_t)blockIdx.x * Z2 + c] = ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
 }
 
+// ---------------------------------------------------------------- 16-byte forms
+// The two latent kernels above move ~50 MB each at config 5 (B = 8192, Z = 128): the
+// split-K slabs dominate.  With one 4-byte element per lane they ran at 2-3 TB/s; these
+// forms (Z % 4 == 0, 16-B aligned operands; the host checks) give each lane four
+// consecutive latent columns, so every slab / mu / lv / eps access is one 16-byte load, and
+// latent_bwd_v4 owns BOTH outputs of a latent index (dMu at column j, dLv at Z + j), so
+// each dZ slab element is read once instead of twice.  Same arithmetic, same slab order.
+DEV void st_bf16x4(bf16_t* p, f32x4 v) {
+    const uint32_t lo = f2bf(v[0]) | (f2bf(v[1]) << 16), hi = f2bf(v[2]) | (f2bf(v[3]) << 16);
+    *reinterpret_cast<uint2*>(p) = make_uint2(lo, hi);
+}
+
+// Fixed-order sum of n slab float4s (8 loads per round trip), added to init.
+DEV f32x4 slab_sum4(rsrc_t b, uint32_t off, uint32_t stride, int n, bool ok, f32x4 init) {
+    f32x4 acc = init;
+    for (int s0 = 0; s0 < n; s0 += 8) {
+        f32x4 v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = bld4(b, (ok && s0 + u < n) ? off + (uint32_t)(s0 + u) * stride : kOOB);
+#pragma unroll
+        for (int u = 0; u < 8; ++u) acc += v[u];
+    }
+    return acc;
+}
+
+// latent_fwd_kernel, 16-byte form: a wave owns two rows (lanes 0-31, 32-63), a lane four
+// latent columns per pass (j0 = 4 lane', + 128 per pass).  Grid ceil(M / 8), 256 threads.
+__global__ __launch_bounds__(256) void latent_fwd_v4_kernel(LatentArgs a) {
+    const int lane = threadIdx.x & 63, hl = lane & 31;
+    const int m = blockIdx.x * 8 + (threadIdx.x >> 5);
+    const bool rok = m < a.M;
+    const int Z = a.Z, Z2 = 2 * Z;
+    const int64_t brow = a.rows.order ? (int64_t)a.rows.order[*a.rows.cursor] : 0;
+    const int64_t grow = brow * a.row_base_mul + a.row_base_add + m;
+    const uint64_t c23 = philox_c23(*a.step, a.domain);
+    const rsrc_t bsl = mkbuf(a.ml_slab, (int64_t)a.nslab * a.M * Z2 * 4);
+    const rsrc_t bb4 = mkbuf(a.b4, (int64_t)Z * 4), bb5 = mkbuf(a.b5, (int64_t)Z * 4);
+    const uint32_t sstride = (uint32_t)a.M * Z2 * 4u;
+    float kl = 0.f;
+    float la[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};   // LA: L <= 8 on this path
+    for (int j = 4 * hl; j < Z; j += 128) {
+        const bool ok = rok;
+        const uint32_t o = ((uint32_t)m * Z2 + j) * 4u;
+        const f32x4 b4v = bld4(bb4, (uint32_t)j * 4u), b5v = bld4(bb5, (uint32_t)j * 4u);
+        const f32x4 mu = slab_sum4(bsl, o, sstride, a.nslab, ok, b4v);
+        const f32x4 lv = slab_sum4(bsl, o + Z * 4u, sstride, a.nslab, ok, b5v);
+        if (!ok) continue;
+        *reinterpret_cast<f32x4*>(a.mu + (int64_t)m * Z + j) = mu;
+        *reinterpret_cast<f32x4*>(a.lv + (int64_t)m * Z + j) = lv;
+        f32x4 sd;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            sd[k] = fexp(0.5f * lv[k]);
+            kl += 0.5f * (1.f + lv[k] - mu[k] * mu[k] - fexp(lv[k]));
+        }
+        for (int l = 0; l < a.L; ++l) {
+            f32x4 e = zero4();
+            if (a.mode != MODE_RECON) {
+                if (a.eps_mode == 0) {
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) e[k] = philox_normal(a.seed, (uint32_t)grow, (uint32_t)(l * Z + j + k), c23);
+                } else {
+                    e = *reinterpret_cast<const f32x4*>(a.eps_in + ((int64_t)l * a.eps_in_ld + m) * Z + j);
+                }
+            }
+            f32x4 z;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) z[k] = mu[k] + sd[k] * e[k];
+            const int64_t oz = ((int64_t)l * a.M + m) * Z + j;
+            *reinterpret_cast<f32x4*>(a.eps + oz) = e;
+            st_bf16x4(a.z + oz, z);
+            if (a.est == EST_LA && l < 8) {
+#pragma unroll
+                for (int k = 0; k < 4; ++k) la[l] += -0.5f * z[k] * z[k] + 0.5f * lv[k] + 0.5f * e[k] * e[k];
+            }
+        }
+    }
+    // row sums over the 32 lanes of the half-wave
+    if (a.est == EST_LA) {
+        for (int l = 0; l < a.L && l < 8; ++l) {
+            float v = la[l];
+#pragma unroll
+            for (int o = 16; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+            if (hl == 0 && rok) a.kl_part[(int64_t)l * a.M + m] = v;
+        }
+    } else {
+#pragma unroll
+        for (int o = 16; o > 0; o >>= 1) kl += __shfl_xor(kl, o, 64);
+        if (hl == 0 && rok) a.kl_part[m] = kl;
+    }
+}
+
+// latent_bwd_kernel, 16-byte form: block (16-row block, 128 latent columns), 256 threads =
+// 8 row slots x 32 lanes of 4 columns; a thread owns rows rs and rs + 8 and BOTH outputs of
+// its columns.  Column partials for b4 / b5: per row slot (rows rs + rs + 8), then the 8
+// slots in order.
+__global__ __launch_bounds__(256) void latent_bwd_v4_kernel(LatentArgs a) {
+    __shared__ float red[8][256];
+    const int Z = a.Z, Z2 = 2 * Z;
+    const int rs = threadIdx.x >> 5, cl = threadIdx.x & 31;
+    const int j = blockIdx.y * 128 + 4 * cl;
+    const bool jok = j < Z;
+    const int LMZ = a.L * a.M * Z;
+    const float sl = a.sc / (float)a.L;
+    const rsrc_t bdz = mkbuf(a.dz_slab, (int64_t)a.ndz * LMZ * 4);
+    const rsrc_t bmu = mkbuf(a.mu, (int64_t)a.M * Z * 4), blv = mkbuf(a.lv, (int64_t)a.M * Z * 4);
+    const rsrc_t bep = mkbuf(a.eps, (int64_t)LMZ * 4);
+    int mr[2];
+    bool ok[2];
+    f32x4 mu[2], lv[2];
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+        mr[r] = blockIdx.x * kLbRows + rs + 8 * r;
+        ok[r] = jok && mr[r] < a.M;
+        const uint32_t o = ok[r] ? (uint32_t)(mr[r] * Z + j) * 4u : kOOB;
+        mu[r] = bld4(bmu, o);
+        lv[r] = bld4(blv, o);
+    }
+    f32x4 g[2] = {zero4(), zero4()}, gv[2] = {zero4(), zero4()}, tm[2] = {zero4(), zero4()}, tv[2] = {zero4(), zero4()};
+    for (int l = 0; l < a.L; ++l) {
+        f32x4 e[2], dz[2];
+        const uint32_t sstride = (uint32_t)LMZ * 4u;
+#pragma unroll
+        for (int r = 0; r < 2; ++r) {
+            const uint32_t ol = (uint32_t)((l * a.M + mr[r]) * Z + j) * 4u;
+            e[r] = bld4(bep, ok[r] ? ol : kOOB);
+            dz[r] = zero4();
+        }
+        // both rows' slab loads together, 8 slabs per round trip
+        for (int s0 = 0; s0 < a.ndz; s0 += 8) {
+            f32x4 v[2][8];
+#pragma unroll
+            for (int r = 0; r < 2; ++r)
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    const uint32_t ol = (uint32_t)((l * a.M + mr[r]) * Z + j) * 4u + (uint32_t)(s0 + u) * sstride;
+                    v[r][u] = bld4(bdz, (ok[r] && s0 + u < a.ndz) ? ol : kOOB);
+                }
+#pragma unroll
+            for (int r = 0; r < 2; ++r)
+#pragma unroll
+                for (int u = 0; u < 8; ++u) dz[r] += v[r][u];
+        }
+#pragma unroll
+        for (int r = 0; r < 2; ++r)
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const float sd = fexp(0.5f * lv[r][k]);
+                const float z = mu[r][k] + sd * e[r][k];
+                g[r][k] += dz[r][k];
+                gv[r][k] += dz[r][k] * 0.5f * sd * e[r][k];
+                if (a.est == EST_LA) {
+                    tm[r][k] += -z;
+                    tv[r][k] += 0.5f - 0.5f * z * sd * e[r][k];
+                }
+            }
+    }
+    f32x4 cm = zero4(), cv = zero4();
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+        f32x4 dm, dl;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            if (a.est == EST_LA) {
+                dm[k] = g[r][k] + sl * tm[r][k];
+                dl[k] = gv[r][k] + sl * tv[r][k];
+            } else {
+                dm[k] = g[r][k] - a.sc * mu[r][k];
+                dl[k] = gv[r][k] + a.sc * 0.5f * (1.f - fexp(lv[r][k]));
+            }
+        }
+        if (ok[r]) {
+            st_bf16x4(a.dmulv + (int64_t)mr[r] * Z2 + j, dm);
+            st_bf16x4(a.dmulv + (int64_t)mr[r] * Z2 + Z + j, dl);
+            cm += dm;
+            cv += dl;
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        red[rs][4 * cl + k] = cm[k];
+        red[rs][128 + 4 * cl + k] = cv[k];
+    }
+    __syncthreads();
+    const int t = threadIdx.x;
+    const int jc = blockIdx.y * 128 + (t & 127);
+    if (jc < Z) {
+        float s = red[0][t];
+#pragma unroll
+        for (int q = 1; q < 8; ++q) s += red[q][t];
+        a.colpart[(int64_t)blockIdx.x * Z2 + (t < 128 ? jc : Z + jc)] = s;
+    }
+}
+
 // Split-K weight gradients: sum the slabs in fixed order, then the optimizer rule.
 struct WReduceArgs {
     const float* slab; int nslab; int M, N;   // slabs [nslab][M][N]
@@ -322,13 +516,23 @@ __global__ __launch_bounds__(256) void bias_opt_kernel(BiasArgs b) {
     float v = 0.f;
     if (ok) {
         const BiasSeg& g = b.seg[s];
+        // 32 loads in flight per round trip (one round at 128 partial rows), accumulated
+        // into 8 running sums: row w + 4k + 32i goes to sum k in increasing i
         float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-        int r = w;
-        for (; r + 28 < g.nrb; r += 32) {
+        // (per-lane pointers: a 64-column block can straddle two segments, so no
+        // wave-uniform buffer descriptor; rows past the end re-read the last row, masked)
+        const float* pp = g.part + e;
+        for (int r0 = w; r0 < g.nrb; r0 += 128) {
+            float v[32];
 #pragma unroll
-            for (int u = 0; u < 8; ++u) acc[u] += g.part[(int64_t)(r + 4 * u) * g.N + e];
+            for (int u = 0; u < 32; ++u) {
+                const int r = r0 + 4 * u;
+                const float x = pp[(int64_t)min(r, g.nrb - 1) * g.N];
+                v[u] = r < g.nrb ? x : 0.f;
+            }
+#pragma unroll
+            for (int u = 0; u < 32; ++u) acc[u & 7] += v[u];
         }
-        for (; r < g.nrb; r += 4) acc[0] += g.part[(int64_t)r * g.N + e];
 #pragma unroll
         for (int u = 0; u < 8; ++u) v += acc[u];
     }

@@ -28,9 +28,17 @@
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 // Diagnostics: wave 0 of each workgroup records a 100 MHz timestamp in slot `slot`.
+// Compiled in only with -DVAEB_TIMELINE (the `tl` library variant, __graft_entry__
+// .build_variant): in the product build the stamp branches are dead code, so no kernel
+// starts with a dependent load of its debug pointer ahead of its operand loads.
+#ifdef VAEB_TIMELINE
+#define VAEB_DBG_ON(p) ((p) != nullptr)
+#else
+#define VAEB_DBG_ON(p) false
+#endif
 #define VAEB_STAMP(A, slot)                                                               \
     do {                                                                                  \
-        if ((A).dbg && threadIdx.x == 0)                                                  \
+        if (VAEB_DBG_ON((A).dbg) && threadIdx.x == 0)                                     \
             (A).dbg[(blockIdx.x + (uint64_t)blockIdx.y * gridDim.x) * 8 + (slot)] =       \
                 __builtin_amdgcn_s_memrealtime();                                         \
     } while (0)
@@ -39,7 +47,7 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 // logical id so their slots do not collide.
 #define VAEB_STAMP_AT(A, idx, slot)                                                       \
     do {                                                                                  \
-        if ((A).dbg && threadIdx.x == 0)                                                  \
+        if (VAEB_DBG_ON((A).dbg) && threadIdx.x == 0)                                     \
             (A).dbg[(uint64_t)(idx) * 8 + (slot)] = __builtin_amdgcn_s_memrealtime();     \
     } while (0)
 
@@ -47,7 +55,7 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 // so the stamp marks when its loads have actually landed (debug launches only).
 #define VAEB_STAMP_SYNC(A, slot)                                                          \
     do {                                                                                  \
-        if ((A).dbg) {                                                                    \
+        if (VAEB_DBG_ON((A).dbg)) {                                                       \
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");                              \
             if (threadIdx.x == 0)                                                         \
                 (A).dbg[(blockIdx.x + (uint64_t)blockIdx.y * gridDim.x) * 8 + (slot)] =   \
@@ -223,7 +231,7 @@ template <int WM, int WN, int KS, int NB, int GCH, class P>
 DEV void tile_body(P& p, int bx, int by) {
     constexpr int NW = WM * WN * KS;
     const int lin = bx + by * (int)gridDim.x;  // 1-D fused grids have gridDim.y == 1 and by == 0
-    if (p.a.dbg && threadIdx.x == 0) p.a.dbg[(uint64_t)lin * 8 + 6] = __builtin_amdgcn_s_memtime();
+    if (VAEB_DBG_ON(p.a.dbg) && threadIdx.x == 0) p.a.dbg[(uint64_t)lin * 8 + 6] = __builtin_amdgcn_s_memtime();
     p.prepare();
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
@@ -243,7 +251,7 @@ DEV void tile_body(P& p, int bx, int by) {
     if (m0 >= p.M || n0 >= p.N) return;
     p.epilogue(m0, n0, acc, pre);
     VAEB_STAMP(p.a, 3);
-    if (p.a.dbg && threadIdx.x == 0) p.a.dbg[(uint64_t)lin * 8 + 7] = __builtin_amdgcn_s_memtime();
+    if (VAEB_DBG_ON(p.a.dbg) && threadIdx.x == 0) p.a.dbg[(uint64_t)lin * 8 + 7] = __builtin_amdgcn_s_memtime();
 }
 
 template <int WM, int WN, int KS, int NB, int GCH, class P>

@@ -143,7 +143,7 @@ struct vaeb_ctx {
     ncclComm_t comm = nullptr;
     int rank = 0, world = 1;
     hipStream_t s3 = nullptr;     // bf16 engine: dW2 (| dW6) + Adagrad forked beside the backward chain
-    hipEvent_t fk_ev[3] = {};     // fork after dhd, s3's work done, [dMu | dLv] ready
+    hipEvent_t fk_ev[4] = {};     // fork after dhd, s3's work done, [dMu | dLv] ready, ELBO partials
     bool bf_fork = true;          // VAEB_BF_FORK=0: dW2 in the dhd grid (bf_fuse) or after it
     bool w3_256 = true;           // forked step: dW3 on 256 x 256 tiles beside dW2 (VAEB_BF_W3_256=0: 256 x 128)
     hipStream_t s2 = nullptr;     // DP: the gradient buckets' all-reduces and their Adagrad
@@ -154,6 +154,7 @@ struct vaeb_ctx {
     int w3_ts = 1;                // folded path's last launch: tile width / 16 (VAEB_W3_TS)
     bool w3_gvec = true;          // ... 16-byte panel loads decided per group (VAEB_W3_GVEC)
     int atomic_ho = 1;            // folded latent hand-offs: 1 by fan-in (ho_mode), 0 slabs, 2 ticketed atomics
+    bool bf_lat4 = true;          // bf16 engine: 16-byte latent kernels where shapes allow (VAEB_BF_LAT4)
     int enc_ct = 0;               // encoder h column tiles per workgroup: 0 auto, VAEB_ENC_CT=1|2 forces
     bool decout_2b = true;        // bf16 Bernoulli decout on 256 x 128 tiles, 2 blocks / CU (VAEB_DECOUT_2B=0: 256 x 256)
     bool bf_fuse = true;          // bf16 engine: dhd + dW2 (| dW6) in one grid (VAEB_BF_FUSE=0: two launches)
@@ -346,7 +347,8 @@ void launch_enc_latent_ct(hipStream_t s, dim3 g1, const StepArgs& a, const FvFol
 }
 template <int HO>
 void launch_enc_latent(hipStream_t s, dim3 g1, const StepArgs& a, const FvFold& fvf, bool deep, int ct) {
-    if (ct == 2) launch_enc_latent_ct<HO, 2>(s, g1, a, fvf, deep);
+    if (ct == 4) launch_enc_latent_ct<HO, 4>(s, g1, a, fvf, deep);
+    else if (ct == 2) launch_enc_latent_ct<HO, 2>(s, g1, a, fvf, deep);
     else launch_enc_latent_ct<HO, 1>(s, g1, a, fvf, deep);
 }
 
@@ -945,8 +947,9 @@ int vaeb_create(const vaeb_config* cfg, vaeb_ctx** out) {
     if (const char* bk = getenv("VAEB_BF_FORK")) c->bf_fork = atoi(bk) != 0;
     if (const char* w3 = getenv("VAEB_BF_W3_256")) c->w3_256 = atoi(w3) != 0;
     if (const char* d2 = getenv("VAEB_DECOUT_2B")) c->decout_2b = atoi(d2) != 0;
-    if (const char* ec = getenv("VAEB_ENC_CT")) c->enc_ct = atoi(ec) == 2 ? 2 : 1;
+    if (const char* ec = getenv("VAEB_ENC_CT")) { const int v = atoi(ec); c->enc_ct = (v == 2 || v == 4) ? v : 1; }
     if (const char* ah = getenv("VAEB_ATOMIC_HO")) c->atomic_ho = atoi(ah);
+    if (const char* l4 = getenv("VAEB_BF_LAT4")) c->bf_lat4 = atoi(l4) != 0;
     if (e != hipSuccess) { delete c; return fail(VAEB_ERR_HIP, "stream/event create: %s", hipGetErrorString(e)); }
     const int64_t D = g.D, H = g.H, Z = g.Z;
     std::vector<int64_t> sz = {D * H, H * Z, H * Z, Z * H, H * D};
@@ -1007,7 +1010,8 @@ int vaeb_create(const vaeb_config* cfg, vaeb_ctx** out) {
         if (hipStreamCreateWithFlags(&c->s3, hipStreamNonBlocking) != hipSuccess ||
             hipEventCreateWithFlags(&c->fk_ev[0], hipEventDisableTiming) != hipSuccess ||
             hipEventCreateWithFlags(&c->fk_ev[1], hipEventDisableTiming) != hipSuccess ||
-            hipEventCreateWithFlags(&c->fk_ev[2], hipEventDisableTiming) != hipSuccess)
+            hipEventCreateWithFlags(&c->fk_ev[2], hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&c->fk_ev[3], hipEventDisableTiming) != hipSuccess)
             rc = fail(VAEB_ERR_HIP, "fork stream / events");
     }
     if (rc) { vaeb_destroy(c); return rc; }
