@@ -377,7 +377,8 @@ def test_epoch_throughput_mode_matches_sync_mode():
 def test_atomic_and_slab_handoffs_agree(kw, monkeypatch):
     """The folded latent hand-offs (latent.hpp) on the same 6 Philox steps: the default
     (VAEB_ATOMIC_HO=1: counted fixed-point atomics up to fan-in 16, slabs above), the
-    ticketed atomic form (=2, A/B only) and slabs + ticket + reducer everywhere (=0).
+    ticketed atomic form (=2, A/B only), slabs + ticket + reducer everywhere (=0) and the
+    encoder slabs summed by the decoder launch (VAEB_ENC_RED=1).
     They sum the same partials in different arithmetic (exact integer vs ordered fp32), so
     they agree to rounding, and each is bitwise deterministic (graph == eager)."""
     from vaeb_amd import _lib
@@ -386,10 +387,12 @@ def test_atomic_and_slab_handoffs_agree(kw, monkeypatch):
     x = data_for(cfg, 8 * B)
     order = np.array([3, 1, 4, 1, 5, 7], np.int32)
     out = {}
-    modes = {"atomic": "1", "ticketed": "2", "slab": "0"}
+    # "decred": VAEB_ENC_RED=1, the encoder's slabs summed by every decoder workgroup
+    modes = {"atomic": ("1", "0"), "ticketed": ("2", "0"), "slab": ("0", "0"), "decred": ("1", "1")}
     for mode in modes:
         for use_graph in (True, False):
-            monkeypatch.setenv("VAEB_ATOMIC_HO", modes[mode])
+            monkeypatch.setenv("VAEB_ATOMIC_HO", modes[mode][0])
+            monkeypatch.setenv("VAEB_ENC_RED", modes[mode][1])
             ctx = _lib.Context(cfg.D, cfg.H, cfg.Z, B, L=cfg.L,
                                decoder=_lib.DEC_GAUSSIAN if cfg.continuous else _lib.DEC_BERNOULLI,
                                max_eval_rows=B, use_graph=use_graph)
@@ -405,7 +408,7 @@ def test_atomic_and_slab_handoffs_agree(kw, monkeypatch):
         assert out[mode, True][0] == out[mode, False][0]
         assert np.array_equal(out[mode, True][1], out[mode, False][1])
     es = out["slab", True][0]
-    for mode in ("atomic", "ticketed"):
+    for mode in ("atomic", "ticketed", "decred"):
         ea = out[mode, True][0]
         assert abs(ea - es) <= 1e-5 * abs(es), (mode, ea, es)
         d = np.abs(out[mode, True][1] - out["slab", True][1])

@@ -262,7 +262,7 @@ DEV void enc_latent_body(const StepArgs& a, const FvFold& fvf) {
     __shared__ f32x4 red[512 * CT];
     __shared__ float hs[16][16 * CT + 4];
     __shared__ int sflag;
-    __shared__ float pm[HO ? 64 : 1][17];   // HO: the tile's [mu | lv] partials, [column][row]
+    __shared__ float pm[(HO == 1 || HO == 2) ? 64 : 1][17];   // the tile's [mu | lv] partials, [column][row]
     // contributors per row block: the grid's column workgroups (FV: rows beyond run the stream)
     // (grid extents from the arguments, not gridDim: reading the implicit arguments put one
     // more dependent scalar round trip ahead of every workgroup's first operand load)
@@ -346,7 +346,7 @@ DEV void enc_latent_body(const StepArgs& a, const FvFold& fvf) {
             for (int c = 1; c < CT; ++c) v = mfma4(av[c], bw[c][w], v);
             return v;
         };
-        if constexpr (HO != 0) {
+        if constexpr (HO == 1 || HO == 2) {
 #pragma unroll
             for (int w = 0; w < 2 * NCT; ++w) {
                 const f32x4 sv = part(w);
@@ -354,6 +354,16 @@ DEV void enc_latent_body(const StepArgs& a, const FvFold& fvf) {
                 if (nz < Z)
 #pragma unroll
                     for (int r = 0; r < 4; ++r) pm[(w & 1) * Z + nz][4 * q + r] = sv[r];
+            }
+        } else if constexpr (HO == 3) {
+            // the decoder launch sums the slabs (decout_z_kernel<.., ZM = 2>): plain stores,
+            // made visible by the kernel boundary
+#pragma unroll
+            for (int w = 0; w < 2 * NCT; ++w) {
+                const f32x4 sv = part(w);
+                const int nz = (w >> 1) * 16 + li;
+                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, sv), bs,
+                                                       nz < Z ? (uint32_t)(((base + (w & 1) * Z + nz) * 16 + 4 * q) * 4) : kOOB, 0, 0);
             }
         } else {
 #pragma unroll
@@ -363,6 +373,10 @@ DEV void enc_latent_body(const StepArgs& a, const FvFold& fvf) {
                 st4_sc1(bs, nz < Z ? (uint32_t)(((base + (w & 1) * Z + nz) * 16 + 4 * q) * 4) : kOOB, sv);
             }
         }
+    }
+    if constexpr (HO == 3) {
+        VAEB_STAMP(a, 2);
+        return;
     }
     if constexpr (AT) {
         __syncthreads();
@@ -523,8 +537,13 @@ __global__ __launch_bounds__(512) void enc_latent_fv_kernel(StepArgs a, FvFold f
 // AT (atomic hand-off, enc_latent_body<.., AT>): z = mu + exp(lv / 2) eps is formed here
 // from mu, lv and eps (all written by the encoder launch), and column tile 0 stores z and
 // the row's KL (LB / FV, plane 0) or LA partial for the backward and the ELBO.
-template <int NB, int ZS, bool V1, bool AT>
+// ZM: 0 = z read from memory; 1 = AT (z formed from mu, lv, eps that the encoder launch
+// wrote); 2 = the encoder's CT = 2 partial [mu | lv] slabs (enc_latent_body<.., HO = 3, 2>,
+// ceil(H / 32) per row block) summed here in fixed order, + bias, eps drawn here, and column
+// tile 0 stores mu, lv, eps, z and the KL / LA terms for the backward and the ELBO.
+template <int NB, int ZS, bool V1, int ZM>
 __global__ __launch_bounds__(512, 4) void decout_z_kernel(StepArgs a) {
+    constexpr bool AT = ZM != 0;
     VAEB_STAMP(a, 0);
     PDecOut p{a, nullptr, a.Me, a.D, a.H};
     p.prepare_at(nullptr);
@@ -540,6 +559,38 @@ __global__ __launch_bounds__(512, 4) void decout_z_kernel(StepArgs a) {
     const rsrc_t bw1 = mkbuf(a.W1, (int64_t)Z * H * 4);
     const rsrc_t bb1 = mkbuf(a.b1, (int64_t)H * 4);
     constexpr bool v1 = V1;
+    PDecOut::Pre pre{};
+    f32x4 acc[NB];
+#pragma unroll
+    for (int w = 0; w < NB; ++w) acc[w] = zero4();
+    // W1^T rows kb + 4 li + (0..3) at latent 4t + q; b1 at kb + 16 q + 4 r + (0..3); W2 rows
+    // kb + 16 q + 4 r + u.  ZM 0 / 1: the first block's loads are issued BEFORE the z
+    // prologue (whose own loads -- z, or mu / lv / eps -- they do not depend on), so both
+    // round trips overlap (MNIST ZM 0 decout 10.5 -> 10.2 us); a block past H reads zeros.
+    // ZM 2 keeps them in the loop: beside its 16 slab float4s in flight they pushed the
+    // kernel past 128 VGPRs (spills at 4 blocks / CU; at 2 blocks / CU 87 of MNIST's 343
+    // workgroups waited for a second round: 12.7 -> 15.7 us).
+    f32x4 w1v[ZS], b1v[4];
+    float w2b[4][4][NB];
+    auto load_block = [&](int kb) {
+#pragma unroll
+        for (int t = 0; t < ZS; ++t) {
+            const int c = 4 * t + q, k = kb + 4 * li;
+            w1v[t] = kc4(bw1, H, c, k, Z, H, v1);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) b1v[r] = kc4(bb1, 0, 0, kb + 16 * q + 4 * r, 1, H, v1);
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+#pragma unroll
+                for (int w = 0; w < NB; ++w) {
+                    const int k = kb + 16 * q + 4 * r + u;
+                    w2b[u][r][w] = p.b1(n0 + li, k, w);
+                }
+    };
+    if constexpr (ZM != 2) load_block(64 * wave);
     float zb[ZS];
     if constexpr (!AT) {
         const rsrc_t bz = mkbuf(a.z, (int64_t)a.Me * Z * 4);
@@ -550,15 +601,60 @@ __global__ __launch_bounds__(512, 4) void decout_z_kernel(StepArgs a) {
         // and eps of one element (coalesced), the waves then read their fragments from LDS
         __shared__ float zs[16][33];
         __shared__ float gs[16][33];
+        __shared__ float msum[ZM == 2 ? 64 : 1][17];   // ZM 2: summed [mu | lv] slab, [column][row]
         const int per = 16 * Z;
         const int l = m0 / a.Mbp;                 // a 16-row block never straddles two planes
         const int i0 = m0 - l * a.Mbp;
+        if constexpr (ZM == 2) {
+            // thread (c, mq) sums float4 (column c, rows 4 mq .. 4 mq + 3) of the row block's
+            // nct slabs, contributor order, 16 loads per round trip
+            const int nct = (H + 31) >> 5, nf4 = 8 * Z;
+            const rsrc_t bsl = mkbuf(a.slab_ml, (int64_t)(a.Mbp >> 4) * nct * nf4 * 16);
+            if ((int)threadIdx.x < nf4) {
+                const int64_t first = (int64_t)(i0 >> 4) * nct * nf4 + threadIdx.x;
+                f32x4 sum = zero4();
+                for (int c0 = 0; c0 < nct; c0 += 16) {
+                    f32x4 v[16];
+#pragma unroll
+                    for (int u = 0; u < 16; ++u)
+                        v[u] = bld4(bsl, c0 + u < nct ? (uint32_t)((first + (int64_t)(c0 + u) * nf4) * 16) : kOOB);
+#pragma unroll
+                    for (int u = 0; u < 16; ++u) sum += v[u];
+                }
+                const int c = threadIdx.x >> 2, mq = threadIdx.x & 3;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) msum[c][4 * mq + k] = sum[k];
+            }
+            __syncthreads();
+        }
         if ((int)threadIdx.x < per) {
             const int ml = threadIdx.x / Z, j = threadIdx.x - ml * Z;
             const int i = i0 + ml;
-            const float mu = a.mu[(int64_t)i * Z + j], lv = a.lv[(int64_t)i * Z + j];
-            const float e = a.eps[((int64_t)l * a.Mbp + i) * Z + j];
             const bool rv = i < a.Mb;
+            float mu, lv, e;
+            if constexpr (ZM == 2) {
+                mu = rv ? msum[j][ml] + a.b4[j] : 0.f;
+                lv = rv ? msum[Z + j][ml] + a.b5[j] : 0.f;
+                // eps as the encoder's reducer draws it (Philox keyed by the global row)
+                const int64_t grow0 =
+                    (a.order ? (int64_t)ld_launch_const(a.cursor + kCtlNext) * a.row_base_mul : 0) + a.row_base_add;
+                e = 0.f;
+                if (rv) {
+                    if (a.eps_mode == 0) e = philox_normal(a.seed, (uint32_t)(grow0 + i), (uint32_t)(l * Z + j), philox_c23(a.step ? *a.step : 0, a.domain));
+                    else if (a.eps_mode == 1) e = a.eps_in[((int64_t)l * a.eps_in_ld + i) * Z + j];
+                }
+                if (col0) {
+                    a.eps[((int64_t)l * a.Mbp + i) * Z + j] = e;
+                    if (l == 0) {
+                        a.mu[(int64_t)i * Z + j] = mu;
+                        a.lv[(int64_t)i * Z + j] = lv;
+                    }
+                }
+            } else {
+                mu = a.mu[(int64_t)i * Z + j];
+                lv = a.lv[(int64_t)i * Z + j];
+                e = a.eps[((int64_t)l * a.Mbp + i) * Z + j];
+            }
             const float z = rv ? mu + fexp(0.5f * lv) * e : 0.f;
             zs[ml][j] = z;
             if (col0) {
@@ -585,30 +681,8 @@ __global__ __launch_bounds__(512, 4) void decout_z_kernel(StepArgs a) {
             for (int n = 0; n < a.nctZ; ++n) dst[n] = n == 0 ? f : 0.f;
         }
     }
-    PDecOut::Pre pre{};
-    f32x4 acc[NB];
-#pragma unroll
-    for (int w = 0; w < NB; ++w) acc[w] = zero4();
     for (int kb = 64 * wave; kb < H; kb += 64 * 8) {
-        // W1^T rows kb + 4 li + (0..3) at latent 4t + q; b1 at kb + 16 q + 4 r + (0..3)
-        f32x4 w1v[ZS], b1v[4];
-        float w2b[4][4][NB];
-#pragma unroll
-        for (int t = 0; t < ZS; ++t) {
-            const int c = 4 * t + q, k = kb + 4 * li;
-            w1v[t] = kc4(bw1, H, c, k, Z, H, v1);
-        }
-#pragma unroll
-        for (int r = 0; r < 4; ++r) b1v[r] = kc4(bb1, 0, 0, kb + 16 * q + 4 * r, 1, H, v1);
-#pragma unroll
-        for (int u = 0; u < 4; ++u)
-#pragma unroll
-            for (int r = 0; r < 4; ++r)
-#pragma unroll
-                for (int w = 0; w < NB; ++w) {
-                    const int k = kb + 16 * q + 4 * r + u;
-                    w2b[u][r][w] = p.b1(n0 + li, k, w);
-                }
+        if (ZM == 2 || kb != 64 * wave) load_block(kb);
         if (kb == 0) {   // wave 0, first block: its loads are in flight
             p.x = x_rows(a);
             pre = p.prefetch(m0, n0);

@@ -154,6 +154,7 @@ struct vaeb_ctx {
     int w3_ts = 1;                // folded path's last launch: tile width / 16 (VAEB_W3_TS)
     bool w3_gvec = true;          // ... 16-byte panel loads decided per group (VAEB_W3_GVEC)
     int atomic_ho = 1;            // folded latent hand-offs: 1 by fan-in (ho_mode), 0 slabs, 2 ticketed atomics
+    int enc_red = -1;             // encoder slabs summed by the decoder launch: -1 auto, VAEB_ENC_RED=0|1
     bool bf_lat4 = true;          // bf16 engine: 16-byte latent kernels where shapes allow (VAEB_BF_LAT4)
     int enc_ct = 0;               // encoder h column tiles per workgroup: 0 auto, VAEB_ENC_CT=1|2 forces
     bool decout_2b = true;        // bf16 Bernoulli decout on 256 x 128 tiles, 2 blocks / CU (VAEB_DECOUT_2B=0: 256 x 256)
@@ -285,7 +286,7 @@ ElboArgs base_elbo(vaeb_ctx* c, const StepArgs& a) {
     return e;
 }
 
-template <int NB, bool V1, bool AT>
+template <int NB, bool V1, int AT>
 void launch_decout_zv(hipStream_t s, dim3 grid, const StepArgs& a) {
     switch ((a.Z + 3) / 4) {
         case 1: hipLaunchKernelGGL((decout_z_kernel<NB, 1, V1, AT>), grid, dim3(512), 0, s, a); break;
@@ -295,7 +296,7 @@ void launch_decout_zv(hipStream_t s, dim3 grid, const StepArgs& a) {
         default: hipLaunchKernelGGL((decout_z_kernel<NB, 8, V1, AT>), grid, dim3(512), 0, s, a); break;
     }
 }
-template <int NB, bool AT>
+template <int NB, int AT>
 void launch_decout_z(hipStream_t s, dim3 grid, const StepArgs& a) {
     auto al = [](const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
     if ((a.H & 3) == 0 && al(a.W1) && al(a.b1)) launch_decout_zv<NB, true, AT>(s, grid, a);
@@ -347,6 +348,16 @@ void launch_enc_latent_ct(hipStream_t s, dim3 g1, const StepArgs& a, const FvFol
 }
 template <int HO>
 void launch_enc_latent(hipStream_t s, dim3 g1, const StepArgs& a, const FvFold& fvf, bool deep, int ct) {
+    if constexpr (HO == 3) {   // slabs summed by the decoder launch: CT = 2 only, no FV stream
+        if (a.Z <= 16) {
+            if (deep) hipLaunchKernelGGL((enc_latent_kernel<1, 8, 3, 2>), g1, dim3(512), 0, s, a);
+            else hipLaunchKernelGGL((enc_latent_kernel<1, 4, 3, 2>), g1, dim3(512), 0, s, a);
+        } else {
+            if (deep) hipLaunchKernelGGL((enc_latent_kernel<2, 8, 3, 2>), g1, dim3(512), 0, s, a);
+            else hipLaunchKernelGGL((enc_latent_kernel<2, 4, 3, 2>), g1, dim3(512), 0, s, a);
+        }
+        return;
+    }
     if (ct == 4) launch_enc_latent_ct<HO, 4>(s, g1, a, fvf, deep);
     else if (ct == 2) launch_enc_latent_ct<HO, 2>(s, g1, a, fvf, deep);
     else launch_enc_latent_ct<HO, 1>(s, g1, a, fvf, deep);
@@ -367,14 +378,21 @@ int enqueue_forward(vaeb_ctx* c, const StepArgs& a0, Prof& pr, const FvFold& fvf
         // auto: two column tiles per workgroup when the literal-FV stream shares the launch
         // (FV 27.75 -> 27.4 us: fewer encoder tiles beside the stream blocks), else one
         // (MNIST 44.6 either way, Frey 32.2 vs 34.0 us)
-        const int ct = c->enc_ct ? c->enc_ct : (fvf.rows > 0 ? 2 : 1);
+        // VAEB_ENC_RED=1: no hand-off in the encoder launch at all -- its CT = 2 tiles store
+        // partial [mu | lv] slabs and end; every decoder workgroup sums its row block's
+        // ceil(H / 32) slabs (decout_z_kernel<.., ZM = 2>)
+        // auto: where the slab + ticket form would be chosen (fan-in > 16; MNIST 784-500-20
+        // 43.8 -> 42.5 us); at a small fan-in the counted atomics stay (Frey 30.8 vs 32.7 us)
+        const bool red = (c->enc_red < 0 ? ho_ml(c, 1) == 0 : c->enc_red == 1) && fvf.rows == 0 && cdiv(a.H, 32) <= 32;
+        const int ct = red ? 2 : (c->enc_ct ? c->enc_ct : (fvf.rows > 0 ? 2 : 1));
         const dim3 g1(a.Mbp / 16, cdiv(a.H, 16 * ct) + fvf.rows);
         const bool deep = cdiv(cdiv(a.D, 16), 8) > 4;
-        const int ho = ho_ml(c, ct);
-        const bool at = ho == 1;
+        const int ho = red ? 3 : ho_ml(c, ct);
+        const int at = red ? 2 : (ho == 1 ? 1 : 0);
         pr.mark(16);
         REP(pr) {
-            if (ho == 1) launch_enc_latent<1>(s, g1, a, fvf, deep, ct);
+            if (ho == 3) launch_enc_latent<3>(s, g1, a, fvf, deep, ct);
+            else if (ho == 1) launch_enc_latent<1>(s, g1, a, fvf, deep, ct);
             else if (ho == 2) launch_enc_latent<2>(s, g1, a, fvf, deep, ct);
             else launch_enc_latent<0>(s, g1, a, fvf, deep, ct);
         }
@@ -384,11 +402,13 @@ int enqueue_forward(vaeb_ctx* c, const StepArgs& a0, Prof& pr, const FvFold& fvf
         pr.mark(17);
         REP(pr) {
             if (gaussian(c)) {
-                if (at) launch_decout_z<2, true>(s, g4, a);
-                else launch_decout_z<2, false>(s, g4, a);
+                if (at == 2) launch_decout_z<2, 2>(s, g4, a);
+                else if (at == 1) launch_decout_z<2, 1>(s, g4, a);
+                else launch_decout_z<2, 0>(s, g4, a);
             } else {
-                if (at) launch_decout_z<1, true>(s, g4, a);
-                else launch_decout_z<1, false>(s, g4, a);
+                if (at == 2) launch_decout_z<1, 2>(s, g4, a);
+                else if (at == 1) launch_decout_z<1, 1>(s, g4, a);
+                else launch_decout_z<1, 0>(s, g4, a);
             }
         }
         CHECK_LAUNCH();
@@ -950,6 +970,7 @@ int vaeb_create(const vaeb_config* cfg, vaeb_ctx** out) {
     if (const char* ec = getenv("VAEB_ENC_CT")) { const int v = atoi(ec); c->enc_ct = (v == 2 || v == 4) ? v : 1; }
     if (const char* ah = getenv("VAEB_ATOMIC_HO")) c->atomic_ho = atoi(ah);
     if (const char* l4 = getenv("VAEB_BF_LAT4")) c->bf_lat4 = atoi(l4) != 0;
+    if (const char* er = getenv("VAEB_ENC_RED")) c->enc_red = atoi(er) != 0 ? 1 : 0;
     if (e != hipSuccess) { delete c; return fail(VAEB_ERR_HIP, "stream/event create: %s", hipGetErrorString(e)); }
     const int64_t D = g.D, H = g.H, Z = g.Z;
     std::vector<int64_t> sz = {D * H, H * Z, H * Z, Z * H, H * D};
