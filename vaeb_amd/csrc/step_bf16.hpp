@@ -496,6 +496,7 @@ struct BiasSeg {
 };
 struct BiasArgs {
     BiasSeg seg[4]; int nseg;
+    int segblk[4];                        // blocks per segment: ceil(N / 64)
     int total;                            // sum of the segments' N
     Opt opt;
     ElboArgs elbo;
@@ -508,39 +509,35 @@ __global__ __launch_bounds__(256) void bias_opt_kernel(BiasArgs b) {
     }
     __shared__ float red[4][64];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    int e = blockIdx.x * 64 + lane;
-    const bool ok = e < b.total;
-    int s = 0;
-    if (ok)
-        while (s < b.nseg - 1 && e >= b.seg[s].N) { e -= b.seg[s].N; ++s; }
-    float v = 0.f;
-    if (ok) {
-        const BiasSeg& g = b.seg[s];
-        // 32 loads in flight per round trip (one round at 128 partial rows), accumulated
-        // into 8 running sums: row w + 4k + 32i goes to sum k in increasing i
-        float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-        // (per-lane pointers: a 64-column block can straddle two segments, so no
-        // wave-uniform buffer descriptor; rows past the end re-read the last row, masked)
-        const float* pp = g.part + e;
-        for (int r0 = w; r0 < g.nrb; r0 += 128) {
-            float v[32];
+    // blocks never straddle segments (segblk: ceil(N / 64) blocks per segment), so the
+    // segment and its partials' buffer descriptor are block-uniform
+    int bid = blockIdx.x, s = 0;
+    while (s < b.nseg - 1 && bid >= b.segblk[s]) { bid -= b.segblk[s]; ++s; }
+    const BiasSeg& g = b.seg[s];
+    const int e = bid * 64 + lane;
+    const bool ok = e < g.N;
+    // 32 loads in flight per round trip (one round at 128 partial rows), accumulated into 8
+    // running sums: row w + 4k + 32i goes to sum k in increasing i
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    const rsrc_t bp = mkbuf(g.part, (int64_t)g.nrb * g.N * 4);
+    for (int r0 = w; r0 < g.nrb; r0 += 128) {
+        float v[32];
 #pragma unroll
-            for (int u = 0; u < 32; ++u) {
-                const int r = r0 + 4 * u;
-                const float x = pp[(int64_t)min(r, g.nrb - 1) * g.N];
-                v[u] = r < g.nrb ? x : 0.f;
-            }
-#pragma unroll
-            for (int u = 0; u < 32; ++u) acc[u & 7] += v[u];
+        for (int u = 0; u < 32; ++u) {
+            const int r = r0 + 4 * u;
+            v[u] = bld(bp, (ok && r < g.nrb) ? (uint32_t)((int64_t)r * g.N + e) * 4u : kOOB);
         }
 #pragma unroll
-        for (int u = 0; u < 8; ++u) v += acc[u];
+        for (int u = 0; u < 32; ++u) acc[u & 7] += v[u];
     }
+    float v = 0.f;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v += acc[u];
     red[w][lane] = v;
     __syncthreads();
     if (w == 0 && ok) {
         const float t = ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
-        b.opt.apply(b.seg[s].map.at(0, e), -1, t);
+        b.opt.apply(g.map.at(0, e), -1, t);
     }
 }
 

@@ -157,6 +157,8 @@ struct vaeb_ctx {
     int enc_red = -1;             // encoder slabs summed by the decoder launch: -1 auto, VAEB_ENC_RED=0|1
     bool bf_lat4 = true;          // bf16 engine: 16-byte latent kernels where shapes allow (VAEB_BF_LAT4)
     int enc_ct = 0;               // encoder h column tiles per workgroup: 0 auto, VAEB_ENC_CT=1|2 forces
+    bool enc_2b = false;          // bf16 enc on 256 x 128 tiles, 2 blocks / CU (VAEB_BF_ENC2B)
+    bool dhd_2b = false;          // bf16 forked dhd on 256 x 128 tiles, 2 blocks / CU (VAEB_BF_DHD2B)
     bool decout_2b = true;        // bf16 Bernoulli decout on 256 x 128 tiles, 2 blocks / CU (VAEB_DECOUT_2B=0: 256 x 256)
     bool bf_fuse = true;          // bf16 engine: dhd + dW2 (| dW6) in one grid (VAEB_BF_FUSE=0: two launches)
     // profiling
@@ -967,6 +969,8 @@ int vaeb_create(const vaeb_config* cfg, vaeb_ctx** out) {
     if (const char* bk = getenv("VAEB_BF_FORK")) c->bf_fork = atoi(bk) != 0;
     if (const char* w3 = getenv("VAEB_BF_W3_256")) c->w3_256 = atoi(w3) != 0;
     if (const char* d2 = getenv("VAEB_DECOUT_2B")) c->decout_2b = atoi(d2) != 0;
+    if (const char* e2 = getenv("VAEB_BF_ENC2B")) c->enc_2b = atoi(e2) != 0;
+    if (const char* h2 = getenv("VAEB_BF_DHD2B")) c->dhd_2b = atoi(h2) != 0;
     if (const char* ec = getenv("VAEB_ENC_CT")) { const int v = atoi(ec); c->enc_ct = (v == 2 || v == 4) ? v : 1; }
     if (const char* ah = getenv("VAEB_ATOMIC_HO")) c->atomic_ho = atoi(ah);
     if (const char* l4 = getenv("VAEB_BF_LAT4")) c->bf_lat4 = atoi(l4) != 0;
