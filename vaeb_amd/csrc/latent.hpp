@@ -26,6 +26,7 @@
 // block's 80 KB of slabs, and at ~90 GB/s of L2->CU bandwidth per CU that cost more
 // (15.7 us decoder launch) than the arrival round trip here.
 #pragma once
+#include <type_traits>
 #include "fused.hpp"
 
 namespace vaeb {
@@ -541,25 +542,49 @@ __global__ __launch_bounds__(512) void enc_latent_fv_kernel(StepArgs a, FvFold f
 // wrote); 2 = the encoder's CT = 2 partial [mu | lv] slabs (enc_latent_body<.., HO = 3, 2>,
 // ceil(H / 32) per row block) summed here in fixed order, + bias, eps drawn here, and column
 // tile 0 stores mu, lv, eps, z and the KL / LA terms for the backward and the ELBO.
-template <int NB, int ZS, bool V1, int ZM>
-__global__ __launch_bounds__(512, 4) void decout_z_kernel(StepArgs a) {
+// C2 (Bernoulli only, NB = 2): each workgroup owns TWO 16-column output tiles (the B
+// operand's second slot is W2's next 16 columns): half the workgroups, each recomputing hd
+// and (ZM 2) summing the encoder slabs once for 32 columns.
+struct PDecOutC2 : PDecOut {
+    DEV float b1(int n, int k, int w) const { return PDecOut::b1(n + 16 * w, k, 0); }
+    struct Pre { PDecOut::Pre t[2]; };
+    DEV Pre prefetch(int m0, int n0) const { return Pre{{PDecOut::prefetch(m0, n0), PDecOut::prefetch(m0, n0 + 16)}}; }
+    template <int NB>
+    DEV void epilogue(int m0, int n0, const f32x4 (&acc)[NB], const Pre& pre) const {
+#pragma unroll
+        for (int w = 0; w < 2; ++w) {
+            if (n0 + 16 * w >= a.D) break;   // the last pair's second tile past D: no partial slot
+            const f32x4 one[1] = {acc[w]};
+            PDecOut::epilogue<1>(m0, n0 + 16 * w, one, pre.t[w]);
+        }
+    }
+};
+
+// (C2 holds twice the W2 operands: up to 256 VGPRs, so no spills; MNIST's 175 two-tile
+// workgroups need one per CU anyway)
+template <int NB, int ZS, bool V1, int ZM, bool C2 = false>
+__global__ __launch_bounds__(512, C2 ? 2 : 4) void decout_z_kernel(StepArgs a) {
     constexpr bool AT = ZM != 0;
+    constexpr int CW = C2 ? 32 : 16;   // output columns per workgroup
+    static_assert(!C2 || NB == 2, "two Bernoulli column tiles ride the NB = 2 slots");
+    using PD = std::conditional_t<C2, PDecOutC2, PDecOut>;
     VAEB_STAMP(a, 0);
-    PDecOut p{a, nullptr, a.Me, a.D, a.H};
+    PD p{};
+    static_cast<PDecOut&>(p) = PDecOut{a, nullptr, a.Me, a.D, a.H};
     p.prepare_at(nullptr);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int li = lane & 15, q = lane >> 4;
-    const int gx = a.Me >> 4, gy = (a.D + 15) >> 4;   // the grid (no implicit-argument load)
+    const int gx = a.Me >> 4, gy = (a.D + CW - 1) / CW;   // the grid (no implicit-argument load)
     const int lin = xcd_remap(blockIdx.x + blockIdx.y * gx, gx * gy);
     const int bxr = lin % gx, byr = lin / gx;
-    const int m0 = bxr * 16, n0 = byr * 16;
+    const int m0 = bxr * 16, n0 = byr * CW;
     const int Z = a.Z, H = a.H;
     const bool col0 = byr == 0;
     const bool rowok = ((m0 + li) % a.Mbp) < a.Mb;
     const rsrc_t bw1 = mkbuf(a.W1, (int64_t)Z * H * 4);
     const rsrc_t bb1 = mkbuf(a.b1, (int64_t)H * 4);
     constexpr bool v1 = V1;
-    PDecOut::Pre pre{};
+    typename PD::Pre pre{};
     f32x4 acc[NB];
 #pragma unroll
     for (int w = 0; w < NB; ++w) acc[w] = zero4();

@@ -154,6 +154,7 @@ struct vaeb_ctx {
     int w3_ts = 1;                // folded path's last launch: tile width / 16 (VAEB_W3_TS)
     bool w3_gvec = true;          // ... 16-byte panel loads decided per group (VAEB_W3_GVEC)
     int atomic_ho = 1;            // folded latent hand-offs: 1 by fan-in (ho_mode), 0 slabs, 2 ticketed atomics
+    int decout_c2 = 0;            // Bernoulli decoder, 2 column tiles per workgroup: -1 auto, VAEB_DECOUT_C2=0|1
     int enc_red = -1;             // encoder slabs summed by the decoder launch: -1 auto, VAEB_ENC_RED=0|1
     bool bf_lat4 = true;          // bf16 engine: 16-byte latent kernels where shapes allow (VAEB_BF_LAT4)
     int enc_ct = 0;               // encoder h column tiles per workgroup: 0 auto, VAEB_ENC_CT=1|2 forces
@@ -288,21 +289,22 @@ ElboArgs base_elbo(vaeb_ctx* c, const StepArgs& a) {
     return e;
 }
 
-template <int NB, bool V1, int AT>
+template <int NB, bool V1, int AT, bool C2>
 void launch_decout_zv(hipStream_t s, dim3 grid, const StepArgs& a) {
     switch ((a.Z + 3) / 4) {
-        case 1: hipLaunchKernelGGL((decout_z_kernel<NB, 1, V1, AT>), grid, dim3(512), 0, s, a); break;
-        case 2: hipLaunchKernelGGL((decout_z_kernel<NB, 2, V1, AT>), grid, dim3(512), 0, s, a); break;
-        case 3: case 4: hipLaunchKernelGGL((decout_z_kernel<NB, 4, V1, AT>), grid, dim3(512), 0, s, a); break;
-        case 5: hipLaunchKernelGGL((decout_z_kernel<NB, 5, V1, AT>), grid, dim3(512), 0, s, a); break;
-        default: hipLaunchKernelGGL((decout_z_kernel<NB, 8, V1, AT>), grid, dim3(512), 0, s, a); break;
+        case 1: hipLaunchKernelGGL((decout_z_kernel<NB, 1, V1, AT, C2>), grid, dim3(512), 0, s, a); break;
+        case 2: hipLaunchKernelGGL((decout_z_kernel<NB, 2, V1, AT, C2>), grid, dim3(512), 0, s, a); break;
+        case 3: case 4: hipLaunchKernelGGL((decout_z_kernel<NB, 4, V1, AT, C2>), grid, dim3(512), 0, s, a); break;
+        case 5: hipLaunchKernelGGL((decout_z_kernel<NB, 5, V1, AT, C2>), grid, dim3(512), 0, s, a); break;
+        default: hipLaunchKernelGGL((decout_z_kernel<NB, 8, V1, AT, C2>), grid, dim3(512), 0, s, a); break;
     }
 }
-template <int NB, int AT>
+// C2: Bernoulli decoder with two 16-column tiles per workgroup (grid y = ceil(D / 32))
+template <int NB, int AT, bool C2 = false>
 void launch_decout_z(hipStream_t s, dim3 grid, const StepArgs& a) {
     auto al = [](const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
-    if ((a.H & 3) == 0 && al(a.W1) && al(a.b1)) launch_decout_zv<NB, true, AT>(s, grid, a);
-    else launch_decout_zv<NB, false, AT>(s, grid, a);
+    if ((a.H & 3) == 0 && al(a.W1) && al(a.b1)) launch_decout_zv<NB, true, AT, C2>(s, grid, a);
+    else launch_decout_zv<NB, false, AT, C2>(s, grid, a);
 }
 
 // dhd_dz_wgrad_kernel at compile-time NCT (latent col tiles), GCH, load width, AT
@@ -400,10 +402,16 @@ int enqueue_forward(vaeb_ctx* c, const StepArgs& a0, Prof& pr, const FvFold& fvf
         }
         CHECK_LAUNCH();
         a.dbg = next_dbg(c);
-        const dim3 g4(a.Me / 16, cdiv(a.D, 16));
+        // Bernoulli decoder with two column tiles per workgroup (VAEB_DECOUT_C2)
+        const bool c2 = !gaussian(c) && (c->decout_c2 < 0 ? at == 2 : c->decout_c2 == 1);
+        const dim3 g4(a.Me / 16, cdiv(a.D, c2 ? 32 : 16));
         pr.mark(17);
         REP(pr) {
-            if (gaussian(c)) {
+            if (c2) {
+                if (at == 2) launch_decout_z<2, 2, true>(s, g4, a);
+                else if (at == 1) launch_decout_z<2, 1, true>(s, g4, a);
+                else launch_decout_z<2, 0, true>(s, g4, a);
+            } else if (gaussian(c)) {
                 if (at == 2) launch_decout_z<2, 2>(s, g4, a);
                 else if (at == 1) launch_decout_z<2, 1>(s, g4, a);
                 else launch_decout_z<2, 0>(s, g4, a);
@@ -975,6 +983,7 @@ int vaeb_create(const vaeb_config* cfg, vaeb_ctx** out) {
     if (const char* ah = getenv("VAEB_ATOMIC_HO")) c->atomic_ho = atoi(ah);
     if (const char* l4 = getenv("VAEB_BF_LAT4")) c->bf_lat4 = atoi(l4) != 0;
     if (const char* er = getenv("VAEB_ENC_RED")) c->enc_red = atoi(er) != 0 ? 1 : 0;
+    if (const char* c2 = getenv("VAEB_DECOUT_C2")) c->decout_c2 = atoi(c2) != 0 ? 1 : 0;
     if (e != hipSuccess) { delete c; return fail(VAEB_ERR_HIP, "stream/event create: %s", hipGetErrorString(e)); }
     const int64_t D = g.D, H = g.H, Z = g.Z;
     std::vector<int64_t> sz = {D * H, H * Z, H * Z, Z * H, H * D};
