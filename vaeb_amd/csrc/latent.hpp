@@ -630,6 +630,21 @@ __global__ __launch_bounds__(512, C2 ? 2 : 4) void decout_z_kernel(StepArgs a) {
         const int per = 16 * Z;
         const int l = m0 / a.Mbp;                 // a 16-row block never straddles two planes
         const int i0 = m0 - l * a.Mbp;
+        // ZM 2: the element phase's own operands (b4 / b5 of its latent column, the step
+        // counter, the host eps) are loaded BEFORE the slab round trip, so the element phase
+        // after the barrier starts from registers (they were dependent loads behind it)
+        float b4p = 0.f, b5p = 0.f, epre = 0.f;
+        int64_t stp = 0, grow0p = 0;
+        if constexpr (ZM == 2) {
+            if ((int)threadIdx.x < per) {
+                const int ml = threadIdx.x / Z, j = threadIdx.x - ml * Z;
+                b4p = a.b4[j];
+                b5p = a.b5[j];
+                if (a.eps_mode == 1 && i0 + ml < a.Mb) epre = a.eps_in[((int64_t)l * a.eps_in_ld + i0 + ml) * Z + j];
+            }
+            stp = a.step ? *a.step : 0;
+            grow0p = (a.order ? (int64_t)ld_launch_const(a.cursor + kCtlNext) * a.row_base_mul : 0) + a.row_base_add;
+        }
         if constexpr (ZM == 2) {
             // thread (c, mq) sums float4 (column c, rows 4 mq .. 4 mq + 3) of the row block's
             // nct slabs, contributor order, 16 loads per round trip
@@ -658,15 +673,13 @@ __global__ __launch_bounds__(512, C2 ? 2 : 4) void decout_z_kernel(StepArgs a) {
             const bool rv = i < a.Mb;
             float mu, lv, e;
             if constexpr (ZM == 2) {
-                mu = rv ? msum[j][ml] + a.b4[j] : 0.f;
-                lv = rv ? msum[Z + j][ml] + a.b5[j] : 0.f;
+                mu = rv ? msum[j][ml] + b4p : 0.f;
+                lv = rv ? msum[Z + j][ml] + b5p : 0.f;
                 // eps as the encoder's reducer draws it (Philox keyed by the global row)
-                const int64_t grow0 =
-                    (a.order ? (int64_t)ld_launch_const(a.cursor + kCtlNext) * a.row_base_mul : 0) + a.row_base_add;
                 e = 0.f;
                 if (rv) {
-                    if (a.eps_mode == 0) e = philox_normal(a.seed, (uint32_t)(grow0 + i), (uint32_t)(l * Z + j), philox_c23(a.step ? *a.step : 0, a.domain));
-                    else if (a.eps_mode == 1) e = a.eps_in[((int64_t)l * a.eps_in_ld + i) * Z + j];
+                    if (a.eps_mode == 0) e = philox_normal(a.seed, (uint32_t)(grow0p + i), (uint32_t)(l * Z + j), philox_c23(stp, a.domain));
+                    else if (a.eps_mode == 1) e = epre;
                 }
                 if (col0) {
                     a.eps[((int64_t)l * a.Mbp + i) * Z + j] = e;
