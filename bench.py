@@ -321,12 +321,30 @@ def make_context(C, D, H, Z, B, Bg, row_off, local, args, gauss, bf16, dist, ran
     return ctx
 
 
-def timed_run(ctx, order, warmup, steps, dist):
-    """W untimed steps, then exactly K steps between barrier + stream sync; max over ranks."""
+def graph_check(ctx, dist, world):
+    """How every rank's steps run (vaeb_graph_status), gathered to all ranks.  With world > 1
+    a rank whose graph capture fell back to eager launches ends the run on EVERY rank with a
+    non-zero exit: an eager multi-rank step is not the configuration that was tested (the
+    library itself also refuses that fallback at world > 1; this covers any other path)."""
+    st = list(ctx.graph_status())
+    allst = [st]
+    if dist:
+        allst = [None] * world
+        dist.all_gather_object(allst, st)
+    bad = [(r, m) for r, (mode, m) in enumerate(allst) if mode == "eager_fallback"]
+    if bad and world > 1:
+        raise SystemExit(f"graph capture fell back to eager launches on rank(s) {[r for r, _ in bad]}: {bad[0][1]}")
+    return [mode for mode, _ in allst]
+
+
+def timed_run(ctx, order, warmup, steps, dist, world=1):
+    """W untimed steps, then exactly K steps between barrier + stream sync; max over ranks.
+    Returns (seconds, the graph mode of each rank after the warmup)."""
     warm_order, timed_order = order(warmup), order(steps)   # host work done before the GPU runs
     ctx.update_many(warm_order)
     ctx.synchronize()
     ctx.epoch_elbo()
+    modes = graph_check(ctx, dist, world)
     if dist:
         dist.barrier()
     ctx.synchronize()
@@ -342,7 +360,20 @@ def timed_run(ctx, order, warmup, steps, dist):
         t = torch.tensor([el], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
-    return el
+    return el, modes
+
+
+def comm_record(ctx, dist, world):
+    """Per rank: the RCCL version, the overlap choice and the collective algorithm / protocol
+    requested through the environment (RCCL picks per call when unset: "auto")."""
+    info = dict(ctx.comm_info())
+    info["algo"] = os.environ.get("NCCL_ALGO", "auto")
+    info["proto"] = os.environ.get("NCCL_PROTO", "auto")
+    if not dist:
+        return [info]
+    out = [None] * world
+    dist.all_gather_object(out, info)
+    return out
 
 
 def main(argv=None):
@@ -418,8 +449,9 @@ def main(argv=None):
             return np.array(out[:n], np.int32)
         return order
 
-    el = timed_run(ctx, orders(N // Bg), warmup, steps, dist)
+    el, graph_modes = timed_run(ctx, orders(N // Bg), warmup, steps, dist, world)
     elbo_sum, nsteps = ctx.epoch_elbo()
+    comm = comm_record(ctx, dist, world)
 
     # per-kernel device time (HIP events on the context's stream), after the timed region
     prof = ctx.profile_steps(50 if not bf16 else 5)
@@ -457,6 +489,8 @@ def main(argv=None):
         "config": {"workload": C["workload"], "global_batch": Bg, "batch_per_gpu": B, "seq_len": None,
                    "parallelism": f"dp{world}"},
         "elbo": elbo_sum / max(nsteps, 1),
+        "graph": graph_modes,              # per rank: how the timed steps ran (vaeb_graph_status)
+        "comm": comm,                      # per rank: RCCL version, overlap, algorithm / protocol
         "step_tflops": sflops / (el / steps) / 1e12,
         "kernels_ms": {k: round(v, 5) for k, v in prof},
         "roofline": {"bound": bound, "kernel": dom[0], "achieved": achieved, "peak": peak,
@@ -472,7 +506,7 @@ def main(argv=None):
         ctx2.set_data(x)
         ctx2.set_params(theta0)
         ctx2.set_eps_mode(0, seed=10)
-        el2 = timed_run(ctx2, orders(N // Bgs), warmup, steps, dist)
+        el2, _ = timed_run(ctx2, orders(N // Bgs), warmup, steps, dist, world)
         ctx2.close()
         res["strong"] = {"value": Bgs * steps / el2, "ms_per_step": el2 / steps * 1e3, "global_batch": Bgs,
                          "rows_per_gpu": [row_split(Bn, world, r, "strong")[0] for r in range(world)]}

@@ -21,6 +21,23 @@ extern "C" {
 int vaeb_profile_steps(vaeb_ctx* ctx, int32_t n_steps, float* out_ms_per_kernel,
                        int32_t* out_kernel_ids, int32_t max_kernels, int32_t* out_n_kernels);
 int vaeb_kernel_name(int32_t kernel_id, char* out, int32_t cap);
+
+/* How the context's steps run: graphs disabled by the config, not captured yet (the first
+ * vaeb_update / vaeb_update_many captures them), replaying captured graphs, or eager launches
+ * after a failed capture (msg: the failure; with a communicator of > 1 ranks a failed capture
+ * is an error of the call instead, never a silent fallback). */
+enum vaeb_graph_mode { VAEB_GRAPH_OFF = 0, VAEB_GRAPH_NOT_CAPTURED = 1, VAEB_GRAPH_REPLAY = 2,
+                       VAEB_GRAPH_EAGER_FALLBACK = 3 };
+int vaeb_graph_status(vaeb_ctx* ctx, int32_t* mode, char* msg, int32_t cap);
+/* Diagnostics: vaeb_update_many bracketed by events on the context's stream (after a stream
+ * sync): the GPU time from the call's first enqueued work to its last, and the host time
+ * the call itself took to enqueue (graph launches, the order upload). */
+int vaeb_time_update_many(vaeb_ctx* ctx, const int32_t* batch_indices, int32_t n, float* out_gpu_ms,
+                          double* out_enqueue_ms);
+/* Data-parallel configuration: the RCCL version (ncclGetVersion), whether bucket A's
+ * all-reduce + Adagrad overlap the backward on a second stream (-1: no communicator), and
+ * the communicator's world size (1 without one). */
+int vaeb_comm_info(vaeb_ctx* ctx, int32_t* rccl_version, int32_t* dp_overlap, int32_t* world);
 /* Diagnostics: one eager step with a 100 MHz s_memrealtime stamp per workgroup at the
  * stage boundaries of every launch; out = [launch][1024 workgroups][8 slots]. */
 int vaeb_debug_timeline(vaeb_ctx* ctx, int32_t batch_index, uint64_t* out, int64_t cap,

@@ -38,7 +38,11 @@ enum vaeb_dtype     { VAEB_DTYPE_F32 = 0,      /* fp32 MFMA, the reference's flo
                       VAEB_DTYPE_BF16 = 1 };   /* bf16 MFMA operands, fp32 accumulation and fp32
                                                   master weights / Adagrad state (BASELINE config 5) */
 enum vaeb_status    { VAEB_OK = 0, VAEB_ERR_ARG = -1, VAEB_ERR_HIP = -2, VAEB_ERR_STATE = -3,
-                      VAEB_ERR_COMM = -4, VAEB_ERR_NOMEM = -5 };
+                      VAEB_ERR_COMM = -4, VAEB_ERR_NOMEM = -5,
+                      VAEB_ERR_NUMERIC = -6 };  /* a step's values left the fixed-point latent hand-off's
+                                                   range (NaN / inf / |partial| >= 2^17): those latent
+                                                   values were set to NaN; reported by the next
+                                                   vaeb_update / vaeb_epoch_elbo, then cleared */
 
 typedef struct vaeb_config {
     int32_t D;            /* input size (784 MNIST, 560 Frey)                         */
@@ -119,6 +123,15 @@ int vaeb_reconstruct(vaeb_ctx* ctx, const float* x, int64_t n, float* out_y);
  * (Philox validation streams 1..n_samples, or in host eps mode rows [s*n, (s+1)*n) of the
  * pushed eps, which must hold n * n_samples rows).  Writes [n x D]. */
 int vaeb_reconstruct_sampled(vaeb_ctx* ctx, const float* x, int64_t n, int32_t n_samples, float* out_y);
+/* As vaeb_reconstruct_sampled, plus (Gaussian decoder, fp32 contexts; NULL to skip) the
+ * decoder's log-sigma head hd W6 + b6 averaged over the same samples (VAEB.py:275-290): the
+ * reference's closing draw is y + exp(out_lv) * N(0, 1) per pixel (VAEB.py:293-297). */
+int vaeb_reconstruct_full(vaeb_ctx* ctx, const float* x, int64_t n, int32_t n_samples, float* out_y,
+                          float* out_lv);
+/* The decoder from given latents (freyFace.py:173-187 `image(z)`, compiled as `freyFace` at
+ * :237-245): z [n x Z] -> mean [n x D] (sigmoid(tanh(z W1 + b1) W2 + b2)) and, for the Gaussian
+ * decoder, the log-sigma head [n x D] (out_lv; NULL to skip).  fp32 contexts. */
+int vaeb_decode(vaeb_ctx* ctx, const float* z, int64_t n, float* out_mu, float* out_lv);
 
 /* Data parallel (one ctx per rank): the library owns an RCCL communicator; the 128-byte
  * unique id is produced on rank 0 and broadcast by the host (e.g. torch.distributed). */

@@ -307,6 +307,39 @@ def reconstruct(params, x, eps, cfg: Config):
     return y / dt.type(eps.shape[0])
 
 
+def decode(params, z, cfg: Config):
+    """The decoder from given latents: freyFace.py:173-187 `image(z)` (compiled as `freyFace`,
+    :237-245) / VAEB.decoder (VAEB.py:253-265).  Returns (mu, log_sigma); log_sigma is None
+    for the Bernoulli decoder."""
+    p = _unpack(params, cfg)
+    dt = p["W1"].dtype
+    hd = np.tanh(np.asarray(z, dt) @ p["W1"] + p["b1"])
+    mu = sigmoid(hd @ p["W2"] + p["b2"])
+    return mu, (hd @ p["W6"] + p["b6"] if cfg.continuous else None)
+
+
+def reconstruct_full(params, x, eps, cfg: Config):
+    """VAEB.reconstruct (VAEB.py:267-291) up to its closing draw: (y_mu, y_log_sigma), each
+    the decoder output at z = mu (eps None) or the mean over the S draws of eps [S, B, Z]
+    (:279-290).  The reference then returns N(y_mu, exp(y_log_sigma)^2 I) (:293-297)."""
+    p = _unpack(params, cfg)
+    dt = p["W3"].dtype
+    x = np.asarray(x, dt)
+    h = np.tanh(x @ p["W3"] + p["b3"])
+    mu = h @ p["W4"] + p["b4"]
+    lv = h @ p["W5"] + p["b5"]
+    if eps is None:
+        return decode(params, mu, cfg)
+    eps = np.asarray(eps, dt)
+    ym, yl = 0, 0
+    for s in range(eps.shape[0]):
+        m, l = decode(params, mu + np.exp(dt.type(0.5) * lv) * eps[s], cfg)
+        ym = ym + m
+        yl = yl + (l if l is not None else 0)
+    S = dt.type(eps.shape[0])
+    return ym / S, (yl / S if cfg.continuous else None)
+
+
 # ---------------------------------------------------------------- full variational
 def fv_theta_prior(mu_list, sig_list):
     """VAEB.py:359-363: sum over params of 1/2 sum(1 + log sigma^2 - mu^2 - sigma^2)."""

@@ -17,8 +17,14 @@ The JPEG round trip quantises and blurs every pixel (and the sample carries the 
 noise), so the pin is statistical: tests compare mean |y - y_ref| against the same
 statistic for mismatched (input, output) pairs.
 
+The num_samples = 20 pass of the same loop (reconstruction.py:21-34) saved
+`..._image_20_{i}_original.jpg` (the same 8 inputs) and `..._image_20_{i}_sample.jpg`:
+model.reconstruct(x_i, 20), i.e. the decoder outputs averaged over 20 posterior draws
+z = mu + exp(lv / 2) eps (VAEB.py:271-291), then the closing draw.
+
 Stored: for each z in (2, 10, 20): the 12 parameters flattened in file (= reference) order,
-x_orig [8, 560] and y_sample [8, 560] (float32).
+x_orig [8, 560], y_sample [8, 560] (num_samples = 0) and y_sample20 [8, 560]
+(num_samples = 20) (float32).
 """
 import os
 import sys
@@ -50,6 +56,10 @@ def main():
                                         for i in range(8)])
         out[f"y_sample_z{z}"] = np.stack([jpg_to_x(os.path.join(REF, f"continuous_{z}__image_0_{i}_sample.jpg"))
                                           for i in range(8)])
+        x20 = np.stack([jpg_to_x(os.path.join(REF, f"continuous_{z}__image_20_{i}_original.jpg")) for i in range(8)])
+        assert np.array_equal(x20, out[f"x_orig_z{z}"]), "both passes save the same 8 inputs"
+        out[f"y_sample20_z{z}"] = np.stack([jpg_to_x(os.path.join(REF, f"continuous_{z}__image_20_{i}_sample.jpg"))
+                                            for i in range(8)])
         print(f"z={z}: {out[f'theta_z{z}'].size} parameters, header {hdr}")
     np.savez_compressed(os.path.join(HERE, "recon_frey.npz"), **out)
 

@@ -59,19 +59,33 @@ class FakeCtx:
     def profile_steps(self, n):
         return [("p1_enc_latent", 0.012), ("p4_decout_z", 0.010)]
 
+    def graph_status(self):
+        if os.environ.get("FAKE_GRAPH_FAIL_RANK") == os.environ.get("RANK"):
+            return "eager_fallback", "hipStreamEndCapture: operation not permitted when stream is capturing"
+        return "replay", ""
+
+    def comm_info(self):
+        return {"rccl_version": 22700, "dp_overlap": self.world > 1, "world": self.world}
+
     def close(self):
         pass
 
 
-def _rank(rank, world, port, q):
+def _rank(rank, world, port, q, fail_rank=None):
     os.environ.update(RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1",
                       MASTER_PORT=str(port))
+    if fail_rank is not None:
+        os.environ["FAKE_GRAPH_FAIL_RANK"] = str(fail_rank)
     import bench
     from vaeb_amd import _lib
     _lib.Context = FakeCtx
     buf = io.StringIO()
-    with redirect_stdout(buf):
-        bench.main(["--gpus", str(world), "--steps", "40", "--warmup", "4", "--no-cpu-baseline"])
+    try:
+        with redirect_stdout(buf):
+            bench.main(["--gpus", str(world), "--steps", "40", "--warmup", "4", "--no-cpu-baseline"])
+    except SystemExit as e:
+        q.put((rank, "exit", str(e.code)))
+        raise
     q.put((rank, FakeCtx.made, buf.getvalue()))
 
 
@@ -95,6 +109,28 @@ def test_bench_two_ranks_weak_and_strong():
     assert res[1][0][1]["B"] == 50 and res[1][0][1]["B_global"] == 100 and res[1][0][1]["row_offset"] == 50
     line = json.loads(res[0][1].strip().splitlines()[-1])
     assert line["n_gpus"] == 2 and line["scaling"] == "weak" and line["config"]["global_batch"] == 200
+    assert line["graph"] == ["replay", "replay"]
+    assert [c["dp_overlap"] for c in line["comm"]] == [True, True] and line["comm"][1]["algo"] == "auto"
     assert line["strong"]["rows_per_gpu"] == [50, 50] and line["strong"]["global_batch"] == 100
     assert line["value"] == pytest.approx(200 * 40 / (line["ms_per_step"] * 40 / 1e3), rel=1e-6)
     assert res[1][1].strip() == ""   # only rank 0 prints
+
+
+def test_bench_fails_on_every_rank_when_one_rank_falls_back_to_eager():
+    """at world > 1 a graph capture that fell back to eager launches must never
+    be silent.  Rank 1's context reports the fallback after the warmup; bench gathers every
+    rank's graph mode and all ranks exit non-zero (none is left waiting in a collective)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 29900 + (os.getpid() + 250) % 500
+    ps = [ctx.Process(target=_rank, args=(r, 2, port, q, 1)) for r in range(2)]
+    for p in ps:
+        p.start()
+    got = {}
+    for _ in range(2):
+        r, kind, msg = q.get(timeout=120)
+        got[r] = (kind, msg)
+    for p in ps:
+        p.join(60)
+    assert all(p.exitcode not in (0, None) for p in ps), [p.exitcode for p in ps]
+    assert all(k == "exit" and "rank(s) [1]" in m for k, m in got.values()), got

@@ -48,13 +48,16 @@ def test_vaeb_class_theano_rng_mode_is_reproducible():
     assert r[0] == r[1]
 
 
-@pytest.mark.parametrize("continuous,use_graph", [(False, True), (True, True), (False, False)])
-def test_dp_path_world1_matches_fused_path(continuous, use_graph):
-    """The data-parallel path (gradients stored; bucket A = W2 [| W6] all-reduced and
-    updated on the second stream while the backward continues, bucket B + SGVB after it)
-    at world size 1 against the fused-optimizer path: Bernoulli / Gaussian decoder,
-    graph-replayed and eager."""
+@pytest.mark.parametrize("continuous,use_graph,overlap", [(False, True, "1"), (True, True, "1"), (False, False, "1"),
+                                                         (False, True, "0"), (True, True, "0")])
+def test_dp_path_world1_matches_fused_path(continuous, use_graph, overlap, monkeypatch):
+    """The data-parallel path (gradients stored; with VAEB_DP_OVERLAP=1 -- the default at
+    world > 1 -- bucket A = W2 [| W6] all-reduced and updated on the second stream while the
+    backward continues, bucket B + SGVB after it; with 0 -- the fp32 default at world 1 --
+    one all-reduce and one optimizer launch) at world size 1 against the fused-optimizer
+    path: Bernoulli / Gaussian decoder, graph-replayed and eager."""
     from vaeb_amd import _lib
+    monkeypatch.setenv("VAEB_DP_OVERLAP", overlap)
     cfg = O.Config(D=560, H=200, Z=2, continuous=True) if continuous else O.Config(D=784, H=500, Z=20)
     x = O.synthetic_frey(n=2000) if continuous else O.synthetic_mnist(n=2000)
     order = np.random.default_rng(1).permutation(20).astype(np.int32)
@@ -64,11 +67,13 @@ def test_dp_path_world1_matches_fused_path(continuous, use_graph):
                            decoder=_lib.DEC_GAUSSIAN if continuous else _lib.DEC_BERNOULLI)
         if use_comm:
             ctx.comm_init(_lib.Context.comm_unique_id(), 0, 1)
+            assert ctx.comm_info()["dp_overlap"] == (overlap == "1")
         ctx.set_data(x)
         ctx.set_params(O.flatten(O.init_params(cfg)))
         ctx.set_eps_mode(_lib.EPS_PHILOX, 10)
         ctx.set_step(0)
         ctx.update_many(order)
+        assert ctx.graph_status()[0] == ("replay" if use_graph else "off")
         s, n = ctx.epoch_elbo()
         outs.append((s, ctx.get_params(), ctx.get_adagrad_state()))
         ctx.close()

@@ -247,3 +247,36 @@ def test_bf16_dp_path_world1_matches_fused_optimizer():
     assert abs(outs[0][0] - outs[1][0]) <= 1e-5 * abs(outs[0][0]), (outs[0][0], outs[1][0])
     assert np.abs(outs[0][1] - outs[1][1]).max() <= 1e-5
     assert rel(outs[1][2], outs[0][2]) <= 1e-4
+
+
+def test_bf16_forked_and_single_stream_steps_agree(monkeypatch):
+    """the forked bf16 step (dW1, dW2 | dW6 and dW4 | dW5 on a second stream
+    beside the dz -> [dMu | dLv] -> dh -> dW3 chain, joined by events inside the graph) and
+    the single-stream step (VAEB_BF_FORK=0: dhd and dW2 in one grid) compute the same
+    products with the same K order, so 10 Philox steps agree to 1e-6 in every parameter and
+    the ELBO -- this pins the cross-stream ordering independently of the golden tolerances;
+    graph replay and eager launches agree bitwise for each form."""
+    from vaeb_amd import _lib
+    cfg = O.Config(D=512, H=256, Z=32)
+    B = 512
+    x = (np.random.default_rng(4).random((6 * B, cfg.D)) < 0.4).astype(np.float32)
+    order = np.array([3, 1, 4, 1, 5, 0, 2, 5, 3, 4], np.int32)
+    out = {}
+    for fork in ("1", "0"):
+        for use_graph in (True, False):
+            monkeypatch.setenv("VAEB_BF_FORK", fork)
+            ctx = _lib.Context(cfg.D, cfg.H, cfg.Z, B, max_eval_rows=B, dtype=_lib.DTYPE_BF16, use_graph=use_graph)
+            ctx.set_data(x)
+            ctx.set_params(O.flatten(O.init_params(cfg)))
+            ctx.set_eps_mode(_lib.EPS_PHILOX, 10)
+            ctx.set_step(0)
+            ctx.update_many(order)
+            s_, n_ = ctx.epoch_elbo()
+            out[fork, use_graph] = (s_ / n_, ctx.get_params(), ctx.get_adagrad_state())
+            ctx.close()
+    for fork in ("1", "0"):
+        a, b = out[fork, True], out[fork, False]
+        assert a[0] == b[0] and np.array_equal(a[1], b[1]) and np.array_equal(a[2], b[2])
+    f, u = out["1", True], out["0", True]
+    assert abs(f[0] - u[0]) <= 1e-6 * abs(u[0])
+    assert np.abs(f[1] - u[1]).max() <= 1e-6 and np.abs(f[2] - u[2]).max() <= 1e-6 * max(1.0, np.abs(u[2]).max())

@@ -132,11 +132,11 @@ def test_native_checkpoint_resume_is_bit_identical(tmp_path):
     order = np.random.default_rng(8).integers(0, 15, 61).astype(np.int32)
     theta0 = O.flatten(O.init_params(cfg))
 
-    def fresh():
-        c = _lib.Context(560, 200, 2, 100, decoder=_lib.DEC_GAUSSIAN, max_eval_rows=100)
+    def fresh(seed=10, objective=_lib.OBJ_SUM_PRIOR):
+        c = _lib.Context(560, 200, 2, 100, decoder=_lib.DEC_GAUSSIAN, max_eval_rows=100, objective=objective)
         c.set_data(x)
         c.set_params(theta0)
-        c.set_eps_mode(_lib.EPS_PHILOX, 10)
+        c.set_eps_mode(_lib.EPS_PHILOX, seed)
         c.set_step(0)
         return c
 
@@ -149,8 +149,10 @@ def test_native_checkpoint_resume_is_bit_identical(tmp_path):
     ea = a.epoch_elbo()
     pa, acc_a, sa = a.get_params(), a.get_adagrad_state(), a.get_step()
     a.close()
-    b = fresh()
-    b.update_many(order[:3])             # diverge first: the load must overwrite everything
+    # another seed, with its steps already captured as graphs: the load must overwrite
+    # everything, the captured seed included
+    b = fresh(seed=77)
+    b.update_many(order[:3])
     b.checkpoint_load(f)
     assert b.get_step() == 29
     b.epoch_elbo()
@@ -164,6 +166,11 @@ def test_native_checkpoint_resume_is_bit_identical(tmp_path):
     with pytest.raises(_lib.VaebError, match="checkpoint"):
         c.checkpoint_load(f)
     c.close()
+    # ... and so is one written under another objective
+    d = fresh(objective=_lib.OBJ_MEAN_MAP)
+    with pytest.raises(_lib.VaebError, match="objective"):
+        d.checkpoint_load(f)
+    d.close()
 
 
 @pytest.mark.parametrize("eps_mode", ["host", "philox"])

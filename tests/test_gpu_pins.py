@@ -101,3 +101,84 @@ def test_reconstruction_pin_against_reference_images(recon, z):
     if z >= 10:   # each reference output is nearest to its own input's reconstruction
         M = np.abs(y[None, :, :] - y_ref[:, None, :]).mean(-1)
         assert np.array_equal(M.argmin(1), np.arange(8))
+
+
+def _hip_ctx(theta, z):
+    from vaeb_amd import _lib
+    ctx = _lib.Context(560, 200, z, 100, decoder=_lib.DEC_GAUSSIAN, max_eval_rows=64)
+    ctx.set_params(theta)
+    return ctx
+
+
+def _hip_pairs(recon, zs, S, b5_add=0.0):
+    """(y0, yE, yr0, yr20) per model from the HIP path: vaeb_reconstruct (z = mu) and
+    vaeb_reconstruct_sampled over S Philox posterior draws."""
+    pairs = []
+    for z in zs:
+        cfg = O.Config(D=560, H=200, Z=z, continuous=True)
+        theta = recon[f"theta_z{z}"].copy()
+        sl = O.unflatten(np.arange(theta.size), cfg)[8]   # b5's arena slots
+        theta[sl] += np.float32(b5_add)
+        ctx = _hip_ctx(theta, z)
+        x = recon[f"x_orig_z{z}"]
+        pairs.append((ctx.reconstruct(x), ctx.reconstruct_sampled(x, S), recon[f"y_sample_z{z}"],
+                      recon[f"y_sample20_z{z}"]))
+        ctx.close()
+    return pairs
+
+
+def test_sampled_reconstruction_pin_against_reference_images(recon):
+    """reconstruction_res/continuous_{z}__image_20_{i}_sample.jpg (reconstruction.py:21-34:
+    reconstruct(x_i, 20), VAEB.py:271-291) on the HIP path: vaeb_reconstruct_full agrees with
+    the oracle on the same injected draws (mean and log-sigma head, 1e-5); the Philox 20-draw
+    reconstruction matches the reference's to the JPEG's resolution while a wrong model
+    misses; and the curvature shift of the HIP posterior spread exp(lv / 2) matches the
+    reference's (pinstats.lv_head_beta, beta consistent with 1) while b5 + 2 fails by > 4
+    standard errors (a spread too narrow is not discriminated, tests/test_oracle_pins.py)."""
+    from pinstats import lv_head_beta
+    from vaeb_amd import _lib
+    for z in (2, 10, 20):
+        cfg = O.Config(D=560, H=200, Z=z, continuous=True)
+        theta, x, yr20 = recon[f"theta_z{z}"], recon[f"x_orig_z{z}"], recon[f"y_sample20_z{z}"]
+        ctx = _hip_ctx(theta, z)
+        eps = np.random.default_rng(z).standard_normal((20, 8, z)).astype(np.float32)
+        ctx.set_eps_mode(_lib.EPS_HOST)
+        ctx.push_eps(eps.reshape(1, 160, z))
+        y, ls = ctx.reconstruct_full(x, 20)
+        ref_y, ref_ls = O.reconstruct_full(O.unflatten(theta.astype(np.float64), cfg), x.astype(np.float64),
+                                           eps.astype(np.float64), cfg)
+        assert np.abs(y - ref_y).max() <= 1e-5 and np.abs(ls - ref_ls).max() <= 1e-4
+        ctx.set_eps_mode(_lib.EPS_PHILOX, 10)
+        y20 = ctx.reconstruct_sampled(x, 20)
+        ctx.close()
+        assert np.abs(y20 - yr20).mean() <= 0.021
+        z2 = 2 if z != 2 else 20
+        w = _hip_ctx(recon[f"theta_z{z2}"], z2)
+        assert np.abs(w.reconstruct_sampled(x, 20) - yr20).mean() >= 0.025
+        w.close()
+    beta, se = lv_head_beta(_hip_pairs(recon, (10, 20), 4000))
+    assert abs(beta - 1.0) < 2.5 * se, (beta, se)
+    beta_c, se_c = lv_head_beta(_hip_pairs(recon, (10, 20), 4000, b5_add=2.0))
+    assert (1.0 - beta_c) > 4.0 * se_c, (beta_c, se_c)
+
+
+def test_manifold_decode_pin_against_reference_faces():
+    """freyFaces/FREY{ii}{jj}.jpg (freyFace.py:352-367, modelFrey.pkl; fixture
+    tests/golden/frey_manifold.npz) through vaeb_decode: mean and log-sigma head within 1e-5
+    of the oracle's decoder, every face matched to the JPEG's resolution and nearest to its
+    own grid point; the transposed grid and another trained model miss."""
+    from pinstats import manifold_match
+    f = np.load(os.path.join(GOLD, "frey_manifold.npz"))
+    cfg = O.Config(D=560, H=200, Z=2, continuous=True)
+    ctx = _hip_ctx(f["theta"], 2)
+    mu, ls = ctx.decode(f["z"])
+    muT, _ = ctx.decode(f["z"][:, ::-1])
+    ctx.close()
+    rm, rl = O.decode(O.unflatten(f["theta"].astype(np.float64), cfg), f["z"].astype(np.float64), cfg)
+    assert np.abs(mu - rm).max() <= 1e-5 and np.abs(ls - rl).max() <= 1e-4
+    d, own = manifold_match(mu, f["faces"])
+    assert d <= 0.020 and own == 1.0, (d, own)
+    assert np.abs(muT - f["faces"]).mean() >= 0.05
+    w = _hip_ctx(np.load(os.path.join(GOLD, "recon_frey.npz"))["theta_z2"], 2)
+    assert np.abs(w.decode(f["z"])[0] - f["faces"]).mean() >= 0.08
+    w.close()

@@ -375,10 +375,10 @@ def test_epoch_throughput_mode_matches_sync_mode():
 @pytest.mark.parametrize("kw", [dict(D=560, H=200, Z=2, continuous=True), dict(D=784, H=128, Z=24, L=2),
                                 dict(D=784, H=500, Z=20)], ids=["frey2", "latent24_L2", "mnist20"])
 def test_atomic_and_slab_handoffs_agree(kw, monkeypatch):
-    """The folded latent hand-offs (latent.hpp) on the same 6 Philox steps: the default
-    (VAEB_ATOMIC_HO=1: counted fixed-point atomics up to fan-in 16, slabs above), the
-    ticketed atomic form (=2, A/B only), slabs + ticket + reducer everywhere (=0) and the
-    encoder slabs summed by the decoder launch (VAEB_ENC_RED=1).
+    """Every fp32 step form a switch can select, on the same 6 Philox steps: the default
+    (VAEB_ATOMIC_HO=1: counted fixed-point atomics up to fan-in 16, slabs above), slabs +
+    ticket + reducer everywhere (=0), the encoder slabs summed by the decoder launch
+    (VAEB_ENC_RED=1) and the unfolded latent backward (VAEB_FOLD_BWD=0: the P67 launches).
     They sum the same partials in different arithmetic (exact integer vs ordered fp32), so
     they agree to rounding, and each is bitwise deterministic (graph == eager)."""
     from vaeb_amd import _lib
@@ -388,11 +388,13 @@ def test_atomic_and_slab_handoffs_agree(kw, monkeypatch):
     order = np.array([3, 1, 4, 1, 5, 7], np.int32)
     out = {}
     # "decred": VAEB_ENC_RED=1, the encoder's slabs summed by every decoder workgroup
-    modes = {"atomic": ("1", "0"), "ticketed": ("2", "0"), "slab": ("0", "0"), "decred": ("1", "1")}
+    modes = {"atomic": ("1", "0", "1"), "slab": ("0", "0", "1"), "decred": ("1", "1", "1"),
+             "unfolded": ("1", "0", "0")}
     for mode in modes:
         for use_graph in (True, False):
             monkeypatch.setenv("VAEB_ATOMIC_HO", modes[mode][0])
             monkeypatch.setenv("VAEB_ENC_RED", modes[mode][1])
+            monkeypatch.setenv("VAEB_FOLD_BWD", modes[mode][2])
             ctx = _lib.Context(cfg.D, cfg.H, cfg.Z, B, L=cfg.L,
                                decoder=_lib.DEC_GAUSSIAN if cfg.continuous else _lib.DEC_BERNOULLI,
                                max_eval_rows=B, use_graph=use_graph)
@@ -408,9 +410,48 @@ def test_atomic_and_slab_handoffs_agree(kw, monkeypatch):
         assert out[mode, True][0] == out[mode, False][0]
         assert np.array_equal(out[mode, True][1], out[mode, False][1])
     es = out["slab", True][0]
-    for mode in ("atomic", "ticketed", "decred"):
+    for mode in ("atomic", "decred", "unfolded"):
         ea = out[mode, True][0]
         assert abs(ea - es) <= 1e-5 * abs(es), (mode, ea, es)
         d = np.abs(out[mode, True][1] - out["slab", True][1])
         assert d.max() <= 2 * len(order) * cfg.lr          # a ~lr sign(g) step may flip where |g| ~ 1e-7
         assert float((d > 1e-3 * cfg.lr).mean()) <= 1e-3
+
+
+def test_fixed_point_handoff_overflow_is_reported_not_silent():
+    """The counted fixed-point hand-off (latent.hpp fx_inc) at Frey 560-200-2 (fan-in 13, the
+    atomic form): an encoder partial beyond its range -- here every W4 entry 1e3, so the mu
+    partials reach ~1e4 * 16 hidden units -- or a NaN weight poisons the latent elements
+    instead of wrapping into the count field.  The step reports VAEB_ERR_NUMERIC with NaN
+    values (as the slab form's NaN propagation would), and a context restored to sane
+    parameters steps cleanly again (the accumulators were reset by their completers)."""
+    from vaeb_amd import _lib
+    cfg = O.Config(D=560, H=200, Z=2, continuous=True)
+    x = O.synthetic_frey(n=300)
+    theta0 = O.flatten(O.init_params(cfg))
+    ctx = _lib.Context(560, 200, 2, 100, decoder=_lib.DEC_GAUSSIAN, max_eval_rows=100)
+    ctx.set_data(x)
+    ctx.set_params(theta0)
+    ctx.set_eps_mode(_lib.EPS_PHILOX, 10)
+    good = ctx.update(0)
+    assert np.isfinite(good)
+    sl = O.unflatten(np.arange(theta0.size), cfg)
+    for poison in ("huge", "nan"):
+        bad = theta0.copy()
+        bad[sl[0].ravel()] = 1.0                 # W3: h saturates at +-1
+        bad[sl[1].ravel()] = 1e4 if poison == "huge" else np.nan   # W4: mu partials ~ 1e4 x 16 > 2^17
+        ctx.set_params(bad)
+        with pytest.raises(_lib.VaebError, match="fixed-point"):
+            ctx.update(1)
+        assert np.isnan(ctx.activation("mu", 100 * 2)).any()
+        # the asynchronous form reports at vaeb_epoch_elbo
+        ctx.set_params(bad)
+        ctx.update_many(np.array([1, 2], np.int32))
+        with pytest.raises(_lib.VaebError, match="fixed-point"):
+            ctx.epoch_elbo()
+        ctx.set_params(theta0)
+        ctx.set_adagrad_state(np.zeros_like(theta0))   # the poisoned steps' NaN gradients reached it
+        v = ctx.update(0)
+        assert np.isfinite(v) and abs(v - good) < 0.05 * abs(good)
+        assert ctx.epoch_elbo()[1] >= 1
+    ctx.close()

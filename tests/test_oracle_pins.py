@@ -153,3 +153,67 @@ def test_fullbayes_init_draw_order():
         assert not np.array_equal(p[0], O.init_params(cfg)[0])
         q = initial_params_fullbayes(9, 6, 3, cont)
         assert all(np.array_equal(a, b) for a, b in zip(p, q))
+
+
+def _recon_pairs(f, zs, S, b5_add=0.0, seed=7):
+    """(y0, yE, yr0, yr20) per model: the oracle's decoder mean at z = mu and its mean over S
+    posterior draws, next to the reference's saved num_samples = 0 / 20 outputs."""
+    pairs = []
+    for z in zs:
+        cfg = O.Config(D=560, H=200, Z=z, continuous=True)
+        p = O.unflatten(f[f"theta_z{z}"].astype(np.float64).copy(), cfg)
+        p[8] = p[8] + b5_add   # b5: the encoder's log-variance bias
+        x = f[f"x_orig_z{z}"].astype(np.float64)
+        eps = np.random.default_rng(seed).standard_normal((S, x.shape[0], z))
+        pairs.append((O.reconstruct(p, x, None, cfg), O.reconstruct(p, x, eps, cfg),
+                      f[f"y_sample_z{z}"], f[f"y_sample20_z{z}"]))
+    return pairs
+
+
+def test_oracle_sampled_reconstruction_pins_the_posterior_spread():
+    """reconstruction_res/continuous_{10,20}__image_20_{i}_sample.jpg (reconstruction.py:21-34:
+    model.reconstruct(x_i, 20), VAEB.py:271-291) against the restated sampled path: the
+    20-draw reconstructions match to the JPEG's resolution (a wrong model does not), and the
+    reference's (20-draw - mean) difference has the curvature shift of the restated posterior
+    spread exp(lv / 2) (tests/pinstats.lv_head_beta: beta consistent with 1), which a
+    log-variance head shifted by b5 + 2 fails by > 4 standard errors.  Not discriminated: a
+    spread too NARROW (b5 - 2 gives beta ~ 9 +- 5) -- the shift then vanishes into the noise."""
+    from pinstats import lv_head_beta
+    f = np.load(os.path.join(os.path.dirname(__file__), "golden", "recon_frey.npz"))
+    for z in (2, 10, 20):
+        cfg = O.Config(D=560, H=200, Z=z, continuous=True)
+        x = f[f"x_orig_z{z}"].astype(np.float64)
+        eps = np.random.default_rng(z).standard_normal((20, x.shape[0], z))
+        y20 = O.reconstruct(O.unflatten(f[f"theta_z{z}"].astype(np.float64), cfg), x, eps, cfg)
+        assert np.abs(y20 - f[f"y_sample20_z{z}"]).mean() <= 0.021
+        z2 = 2 if z != 2 else 20
+        cfg2 = O.Config(D=560, H=200, Z=z2, continuous=True)
+        y2 = O.reconstruct(O.unflatten(f[f"theta_z{z2}"].astype(np.float64), cfg2), x, eps[..., :z2] if z2 <= z else
+                           np.random.default_rng(z).standard_normal((20, x.shape[0], z2)), cfg2)
+        assert np.abs(y2 - f[f"y_sample20_z{z}"]).mean() >= 0.025
+    beta, se = lv_head_beta(_recon_pairs(f, (10, 20), 4000))
+    assert abs(beta - 1.0) < 2.5 * se, (beta, se)
+    beta_c, se_c = lv_head_beta(_recon_pairs(f, (10, 20), 4000, b5_add=2.0))
+    assert (1.0 - beta_c) > 4.0 * se_c, (beta_c, se_c)
+
+
+def test_oracle_manifold_matches_reference_faces():
+    """freyFaces/FREY{ii}{jj}.jpg (freyFace.py:352-367: modelFrey.pkl decoded at z =
+    [Phi^-1((ii + .9) / 10), Phi^-1((jj + .9) / 10)], then a N(mu, exp(log_sigma)^2) draw;
+    fixture tests/golden/frey_manifold.npz): the restated decoder (freyFace.py:173-187) gives
+    every face to the JPEG's resolution and each face is nearest to its own grid point; the
+    transposed grid and another trained model miss.  The draw's own noise, exp(log_sigma),
+    is ~0.009 per pixel -- below the JPEG's ~0.017."""
+    from pinstats import manifold_match
+    f = np.load(os.path.join(os.path.dirname(__file__), "golden", "frey_manifold.npz"))
+    cfg = O.Config(D=560, H=200, Z=2, continuous=True)
+    p = O.unflatten(f["theta"].astype(np.float64), cfg)
+    mu, ls = O.decode(p, f["z"].astype(np.float64), cfg)
+    d, own = manifold_match(mu, f["faces"])
+    assert d <= 0.020 and own == 1.0, (d, own)
+    assert 0.002 < np.exp(ls).mean() < 0.02
+    muT, _ = O.decode(p, f["z"][:, ::-1].astype(np.float64), cfg)
+    assert np.abs(muT - f["faces"]).mean() >= 0.05
+    g = np.load(os.path.join(os.path.dirname(__file__), "golden", "recon_frey.npz"))
+    mu2, _ = O.decode(O.unflatten(g["theta_z2"].astype(np.float64), cfg), f["z"].astype(np.float64), cfg)
+    assert np.abs(mu2 - f["faces"]).mean() >= 0.08

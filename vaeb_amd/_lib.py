@@ -31,6 +31,7 @@ EXPORTS = [
     "vaeb_get_adagrad_state", "vaeb_set_fv_state", "vaeb_get_fv_state", "vaeb_set_eps_mode",
     "vaeb_push_eps", "vaeb_set_step", "vaeb_get_step", "vaeb_update", "vaeb_update_async", "vaeb_update_many",
     "vaeb_epoch_elbo", "vaeb_synchronize", "vaeb_validate", "vaeb_reconstruct", "vaeb_reconstruct_sampled",
+    "vaeb_reconstruct_full", "vaeb_decode",
     "vaeb_comm_unique_id", "vaeb_comm_init", "vaeb_comm_count", "vaeb_set_valid_data", "vaeb_validate_resident",
     "vaeb_checkpoint_save", "vaeb_checkpoint_load", "vaeb_get_grads", "vaeb_get_activation", "vaeb_push_fv_noise",
     "vaeb_ae_create", "vaeb_ae_destroy", "vaeb_ae_num_params", "vaeb_ae_set_data", "vaeb_ae_set_params",
@@ -38,7 +39,8 @@ EXPORTS = [
     "vaeb_ae_train_many", "vaeb_ae_reconstruct", "vaeb_ae_encode", "vaeb_ae_decode",
 ]
 DIAG_EXPORTS = ["vaeb_profile_steps", "vaeb_kernel_name", "vaeb_debug_timeline", "vaeb_test_gemm_bf16",
-                "vaeb_bench_gemm_bf16"]
+                "vaeb_bench_gemm_bf16", "vaeb_graph_status", "vaeb_comm_info", "vaeb_time_update_many"]
+GRAPH_MODES = {0: "off", 1: "not_captured", 2: "replay", 3: "eager_fallback"}
 AE_MAX_LAYERS = 8
 AE_BINARY, AE_CONT = 0, 1
 ACT = {"tanh": 0, "sigmoid": 1, "relu": 2}
@@ -82,6 +84,11 @@ def load():
         return _lib
     if not os.path.exists(LIB_PATH):
         raise VaebError(f"{LIB_PATH} not found: build it with `python -c 'import __graft_entry__ as g; g.build()'`")
+    if not os.environ.get("VAEB_LIB_VARIANT"):
+        from ._buildinfo import check_stamp
+        why = check_stamp(LIB_PATH)
+        if why:
+            raise VaebError(f"stale {LIB_PATH}: {why}; rebuild with `python -c 'import __graft_entry__ as g; g.build()'`")
     lib = ctypes.CDLL(LIB_PATH)
     sig = {
         "vaeb_last_error": ([], ctypes.c_char_p),
@@ -113,6 +120,8 @@ def load():
         "vaeb_validate": ([_P, _F, _I64, ctypes.POINTER(ctypes.c_double)], ctypes.c_int),
         "vaeb_reconstruct": ([_P, _F, _I64, _F], ctypes.c_int),
         "vaeb_reconstruct_sampled": ([_P, _F, _I64, ctypes.c_int32, _F], ctypes.c_int),
+        "vaeb_reconstruct_full": ([_P, _F, _I64, ctypes.c_int32, _F, _F], ctypes.c_int),
+        "vaeb_decode": ([_P, _F, _I64, _F, _F], ctypes.c_int),
         "vaeb_comm_unique_id": ([ctypes.POINTER(ctypes.c_uint8)], ctypes.c_int),
         "vaeb_comm_init": ([_P, ctypes.POINTER(ctypes.c_uint8), ctypes.c_int32, ctypes.c_int32], ctypes.c_int),
         "vaeb_get_grads": ([_P, _F, _I64], ctypes.c_int),
@@ -120,6 +129,10 @@ def load():
         "vaeb_profile_steps": ([_P, ctypes.c_int32, _F, ctypes.POINTER(ctypes.c_int32), ctypes.c_int32,
                                 ctypes.POINTER(ctypes.c_int32)], ctypes.c_int),
         "vaeb_kernel_name": ([ctypes.c_int32, ctypes.c_char_p, ctypes.c_int32], ctypes.c_int),
+        "vaeb_graph_status": ([_P, ctypes.POINTER(ctypes.c_int32), ctypes.c_char_p, ctypes.c_int32], ctypes.c_int),
+        "vaeb_comm_info": ([_P] + [ctypes.POINTER(ctypes.c_int32)] * 3, ctypes.c_int),
+        "vaeb_time_update_many": ([_P, ctypes.POINTER(ctypes.c_int32), ctypes.c_int32, _F,
+                                   ctypes.POINTER(ctypes.c_double)], ctypes.c_int),
         "vaeb_debug_timeline": ([_P, ctypes.c_int32, ctypes.POINTER(ctypes.c_uint64), _I64,
                                  ctypes.POINTER(ctypes.c_int32)], ctypes.c_int),
         "vaeb_test_gemm_bf16": ([_P] + [ctypes.c_int32] * 5 + [_F, _F, _F, ctypes.c_int32], ctypes.c_int),
@@ -311,6 +324,49 @@ class Context:
         y = np.empty((x.shape[0], self.cfg.D), np.float32)
         check(self.lib.vaeb_reconstruct_sampled(self.h, fptr(x), x.shape[0], int(n_samples), fptr(y)))
         return y
+
+    def reconstruct_full(self, x, n_samples=0, log_sigma=True):
+        """(y, y_log_sigma): decoder mean and (Gaussian decoder) log-sigma head, at z = mu or
+        averaged over n_samples posterior draws (VAEB.py:267-291); y_log_sigma is None for
+        the Bernoulli decoder or when log_sigma is False."""
+        x = np.ascontiguousarray(x, np.float32)
+        y = np.empty((x.shape[0], self.cfg.D), np.float32)
+        lv = np.empty_like(y) if (log_sigma and self.cfg.decoder == DEC_GAUSSIAN) else None
+        check(self.lib.vaeb_reconstruct_full(self.h, fptr(x), x.shape[0], int(n_samples), fptr(y),
+                                             fptr(lv) if lv is not None else None))
+        return y, lv
+
+    def decode(self, z, log_sigma=True):
+        """(mu, log_sigma) of the decoder at given latents z [n x Z] (freyFace.py:173-187,
+        237-245); log_sigma is None for the Bernoulli decoder or when not requested."""
+        z = np.ascontiguousarray(np.atleast_2d(z), np.float32)
+        if z.shape[1] != self.cfg.Z:
+            raise VaebError(f"decode: z has {z.shape[1]} columns, the model's latent size is {self.cfg.Z}")
+        mu = np.empty((z.shape[0], self.cfg.D), np.float32)
+        lv = np.empty_like(mu) if (log_sigma and self.cfg.decoder == DEC_GAUSSIAN) else None
+        check(self.lib.vaeb_decode(self.h, fptr(z), z.shape[0], fptr(mu), fptr(lv) if lv is not None else None))
+        return mu, lv
+
+    def time_update_many(self, indices):
+        """(GPU ms, host enqueue ms) of one update_many call (diagnostics)."""
+        idx = np.ascontiguousarray(indices, np.int32)
+        g, h = ctypes.c_float(), ctypes.c_double()
+        check(self.lib.vaeb_time_update_many(self.h, idx.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), idx.size,
+                                             ctypes.byref(g), ctypes.byref(h)))
+        return g.value, h.value
+
+    def graph_status(self):
+        """(mode, message): 'off' | 'not_captured' | 'replay' | 'eager_fallback' (message: why)."""
+        m = ctypes.c_int32()
+        buf = ctypes.create_string_buffer(512)
+        check(self.lib.vaeb_graph_status(self.h, ctypes.byref(m), buf, 512))
+        return GRAPH_MODES[m.value], buf.value.decode(errors="replace")
+
+    def comm_info(self):
+        """{'rccl_version', 'dp_overlap' (None without a communicator), 'world'}."""
+        v, o, w = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32()
+        check(self.lib.vaeb_comm_info(self.h, ctypes.byref(v), ctypes.byref(o), ctypes.byref(w)))
+        return {"rccl_version": v.value, "dp_overlap": None if o.value < 0 else bool(o.value), "world": w.value}
 
     # ---- data parallel
     @staticmethod

@@ -57,35 +57,36 @@ def get_arg(arg, args, default, type_):
     return default
 
 
-def get_flag(flag, args):
-    """VAEB.py:483-489."""
-    flag = '--' + flag
+def get_flag(flag, args, prefix='--'):
+    """VAEB.py:483-489 (freyFace.py:282-288 spells flags with one dash: prefix '-')."""
+    flag = prefix + flag
     have_flag = flag in args
     if have_flag:
         args.remove(flag)
     return have_flag
 
 
-def parse_args(argv=None):
-    """VAEB.py:491-504."""
+def parse_args(argv=None, spec=None, flags=None, flag_prefix='--'):
+    """VAEB.py:491-504 (spec / flags: another driver's tables, e.g. freyFace.py:20-30, whose
+    parse_args (:290-300) does not report unused arguments)."""
     args = copy.deepcopy(sys.argv[1:] if argv is None else list(argv))
     arg_dict = {}
-    for arg_name, (default, type_) in command_line_args.items():
+    for arg_name, (default, type_) in (spec or command_line_args).items():
         arg_dict[arg_name] = get_arg(arg_name, args, default, type_)
-    for flag_name in command_line_flags:
-        arg_dict[flag_name] = get_flag(flag_name, args)
-    if len(args) > 0:
+    for flag_name in (flags or command_line_flags):
+        arg_dict[flag_name] = get_flag(flag_name, args, flag_prefix)
+    if len(args) > 0 and spec is None:
         print('Have unused args: {0}'.format(args))
     return arg_dict
 
 
-def print_args(args):
+def print_args(args, out=print):
     """VAEB.py:507-512."""
-    print('Parameters used:')
-    print('--------------------------------------')
+    out('Parameters used:')
+    out('--------------------------------------')
     for k, v in args.items():
-        print('\t{0}: {1}'.format(k, v))
-    print('--------------------------------------')
+        out('\t{0}: {1}'.format(k, v))
+    out('--------------------------------------')
 
 
 def load_model(file_name):
@@ -100,7 +101,7 @@ def save_model(model, file_name):
     model.save(file_name)
 
 
-def load_dataset(continuous, synthetic=False):
+def load_dataset(continuous, synthetic=False, splits=2):
     """Data as train_model reads it (VAEB.py:541-556): freyfaces.pkl split 1500 / rest,
     or mnist.pkl.gz's (train, valid) images; both from the working directory.  With
     `synthetic` (or when the file is absent and synthetic is set) the SURVEY 8(d)
@@ -114,10 +115,16 @@ def load_dataset(continuous, synthetic=False):
             data = frey_like()
         return data[:1500], data[1500:]
     if os.path.exists('mnist.pkl.gz') or not synthetic:
-        (x_train, _), (x_valid, _), _ = read_array_pickle('mnist.pkl.gz')
+        sets = read_array_pickle('mnist.pkl.gz')
+        if splits == 3:   # VAEB.load's form (VAEB.py:237-239)
+            return tuple((np.asarray(x, np.float32), np.asarray(y)) for x, y in sets)
+        (x_train, _), (x_valid, _), _ = sets
         return np.asarray(x_train, np.float32), np.asarray(x_valid, np.float32)
-    x = mnist_like(60000)
-    return x[:50000], x[50000:]
+    x = mnist_like(70000)
+    if splits == 3:
+        lab = np.zeros(10000, np.int64)
+        return (x[:50000], np.zeros(50000, np.int64)), (x[50000:60000], lab), (x[60000:], lab)
+    return x[:50000], x[50000:60000]
 
 
 def train_model(args):

@@ -6,6 +6,11 @@
 namespace vaeb {
 
 // ----------------------------------------------------------------- ELBO reduction
+// The context's 64-bit control block (vaeb_hip.hip vaeb_create): slots 0, 1 the epoch ELBO
+// accumulators (double), 2 the sticky step status, 3 the last step's SGVB / B (float), 4
+// the fixed-point hand-off range-guard word, then the hand-off accumulators (latent.hpp).
+constexpr int kBlkStatus = 2, kBlkElbo = 3, kBlkFxErr = 4, kBlkAcc = 5;
+
 struct ElboArgs {
     const float* lp_part; int64_t n_lp;   // [Me][nctD] per-row log p(x|z) partials
     const float* kl_part; int64_t n_kl;   // [Mbp][nctZ] KL partials (LB / FV) or
@@ -106,6 +111,16 @@ DEV void elbo_emit(const ElboArgs& e, double lp, double kl, double fv) {
     // (VAEB.py:327-328); FV: B * (sum logp + sum KL) + thetaPrior (VAEB.py:364).
     const double data = (e.est == EST_LA) ? (lp + kl) / e.L : lp / e.L + kl;
     const double sg = (e.est == EST_FV) ? e.data_mul * data + fv : data;
+    if (e.epoch) {
+        // training step: fold the fixed-point hand-offs' range-guard word (latent.hpp fx_inc,
+        // slot 4 of the control block) into the sticky status slot 2 the host reads at its
+        // next sync (vaeb_update / vaeb_epoch_elbo -> VAEB_ERR_NUMERIC); cleared for the next step
+        unsigned long long* w = reinterpret_cast<unsigned long long*>(e.epoch);
+        const unsigned long long err =
+            __hip_atomic_exchange((__attribute__((address_space(1))) unsigned long long*)(w + kBlkFxErr), 0ull,
+                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (err) w[kBlkStatus] |= err;
+    }
     if (e.eval_acc) { e.eval_acc[0] += data; e.eval_acc[1] = fv; }
     if (e.dp_slot) {
         *e.dp_slot = (float)sg;

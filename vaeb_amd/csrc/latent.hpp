@@ -91,19 +91,33 @@ DEV bool arrive_last(int* cnt, int target, int* sflag) {
 // ---------------------------------------------------------------- atomic hand-off
 // The alternative to slab + ticket + reducer: every contributing workgroup adds its
 // partial of element e into ONE 64-bit accumulator with a returning agent-scope atomic,
-// as a counted fixed-point number  inc = 2^56 + round(v * 2^32)  (two's complement).  The
-// add that brings the count field to n (the number of contributors) returns the complete
+// as a counted fixed-point number (two's complement)
+//     inc = 2^59 + round(v * 2^32)      (count field: bits 59..63, fan-in <= 16)
+// The add that brings the count field to n (the number of contributors) returns the complete
 // sum, so that workgroup -- whichever it is -- finishes element e itself: no slab stores,
 // no drain, no ticket, no reducer.  Every access to an accumulator is an atomic RMW on
 // that one location (a single modification order), so no cross-location ordering, fence or
 // cache rule is involved; the completer resets it (atomic store) for the next launch.
 // Integer adds are associative: the sum, and so the result, is bitwise the same for any
-// arrival order.  Range |sum| < 2^23, resolution 2^-32 (the latent sums here are O(1..100)).
+// arrival order.
+// Range guard: any subset of <= 16 partials with |v| < 2^17 sums below 2^53 in magnitude,
+// so the fields above bit 53 always decode exactly.  A partial outside that range -- or NaN
+// or inf (a diverging run) -- adds the count plus a POISON unit 2^54 (bits 54..58) instead
+// of a value: the completer sees the poison and writes NaN, which then propagates through
+// the step as it would on the slab path, and the accumulator is still reset cleanly.  The
+// contributor also sets the sticky word err[0] = acc[-1] (read and cleared by the step's
+// ELBO reduction, which reports it as VAEB_ERR_NUMERIC to the host).
 typedef __attribute__((address_space(1))) unsigned long long gu64;
 constexpr double kFxScale = 4294967296.0;   // 2^32
-DEV uint64_t fx_inc(float v) {
+constexpr float kFxMax = 131072.f;          // 2^17
+constexpr int kFxCntShift = 59, kFxPoisonShift = 54;
+DEV uint64_t fx_inc(float v, uint64_t* acc) {
+    if (__builtin_expect(!(__builtin_fabsf(v) < kFxMax), 0)) {
+        __hip_atomic_fetch_or((gu64*)(acc - 1), 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return (1ull << kFxCntShift) + (1ull << kFxPoisonShift);
+    }
     const int64_t q = (int64_t)__builtin_rint((double)v * kFxScale);
-    return (1ull << 56) + (uint64_t)q;
+    return (1ull << kFxCntShift) + (uint64_t)q;
 }
 // adds inc to *p and returns the accumulator's new value (issue every add of a lane
 // before decoding any: each decode waits for its add's return)
@@ -111,17 +125,20 @@ DEV uint64_t fx_add(uint64_t* p, uint64_t inc) {
     return __hip_atomic_fetch_add((gu64*)p, (unsigned long long)inc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) +
            inc;
 }
-// true (and the element's sum in `out`) when tot is the value after the n-th add
+// true (and the element's sum in `out`: NaN when a contributor was poisoned) when tot is
+// the value after the n-th add
 DEV bool fx_done(uint64_t tot, int n, float& out) {
-    const uint64_t cnt = (tot + (1ull << 55)) >> 56;
-    out = (float)((double)(int64_t)(tot - (cnt << 56)) * (1.0 / kFxScale));
-    return cnt == (uint64_t)n;
+    const uint64_t hi = (tot + (1ull << (kFxPoisonShift - 1))) >> kFxPoisonShift;   // count * 32 + poison
+    const float v = (float)((double)(int64_t)(tot - (hi << kFxPoisonShift)) * (1.0 / kFxScale));
+    out = (hi & 31) ? __builtin_nanf("") : v;
+    return (hi >> (kFxCntShift - kFxPoisonShift)) == (uint64_t)n;
 }
 DEV void fx_reset(uint64_t* p) { __hip_atomic_store((gu64*)p, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
 // Accumulator e lives at word e * kFxStride: the atomics execute at the memory side, and
 // consecutive 8-B words would put a whole hand-off (a few thousand accumulators, 32 adds
 // each) on a handful of memory channels.
 constexpr int kFxStride = 33;
+constexpr int kFxMaxFanIn = 16;
 DEV uint64_t* fx_at(uint64_t* base, int64_t e) { return base + e * kFxStride; }
 
 // A tile's 16 rows x 2Z partials (Z <= 32) are handed off by all 512 threads of its
@@ -129,42 +146,6 @@ DEV uint64_t* fx_at(uint64_t* base, int64_t e) { return base + e * kFxStride; }
 // elements t and t + 512 (NS = 2 slots when Z > 16, then the first is always present), element
 // e = (column e >> 4, row e & 15).  Only the second slot's add sits in a branch, so at most
 // one wait separates the two adds (a branch around every add made hipcc wait for each).
-// HO == 2 (ticketed form): the same repacked adds without return, then the slab protocol's
-// ticket; the last arriver reads every sum once with an agent-scope exchange (read + reset).
-// The guide's producer form {8-B agent atomics both sides} with its table row 1 ticket.
-template <int NS>
-DEV void fx_add_nr(uint64_t* acc, int64_t row0, int ncol, const float (*pm)[17], int ne) {
-#pragma unroll
-    for (int u = 0; u < NS; ++u) {
-        const int e = (int)threadIdx.x + 512 * u;
-        if (e < ne) {
-            const int c = e >> 4, r = e & 15;
-            __hip_atomic_fetch_add((gu64*)fx_at(acc, (row0 + r) * ncol + c), (unsigned long long)fx_inc(pm[c][r]),
-                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-    }
-}
-DEV float fx_take(uint64_t* p, int n) {
-    float v;
-    fx_done(__hip_atomic_exchange((gu64*)p, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), n, v);
-    return v;
-}
-// every wave's adds performed (vmcnt 0) before the workgroup's one ticket; true in the
-// workgroup whose ticket completed `target`
-DEV bool arrive_last_all(int* cnt, int target, int* sflag) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        const int old = __hip_atomic_fetch_add((gint*)cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        *sflag = (old == target - 1);
-    }
-    __syncthreads();
-    const bool last = *sflag != 0;
-    if (last && threadIdx.x == 0) __hip_atomic_store((gint*)cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // keep the reads below the ticket
-    return last;
-}
-
 template <int NS>
 struct FxSlots {
     uint64_t t[NS];
@@ -180,7 +161,7 @@ struct FxSlots {
         }
 #pragma unroll
         for (int u = 0; u < NS; ++u) {
-            const uint64_t inc = fx_inc(pm[col[u]][row[u]]);
+            const uint64_t inc = fx_inc(pm[col[u]][row[u]], acc);
             uint64_t* p = fx_at(acc, (row0 + row[u]) * ncol + col[u]);
             t[u] = 0;
             if (NS == 2 && u == 0) t[u] = fx_add(p, inc);   // always present when NS == 2
@@ -263,7 +244,7 @@ DEV void enc_latent_body(const StepArgs& a, const FvFold& fvf) {
     __shared__ f32x4 red[512 * CT];
     __shared__ float hs[16][16 * CT + 4];
     __shared__ int sflag;
-    __shared__ float pm[(HO == 1 || HO == 2) ? 64 : 1][17];   // the tile's [mu | lv] partials, [column][row]
+    __shared__ float pm[HO == 1 ? 64 : 1][17];   // the tile's [mu | lv] partials, [column][row]
     // contributors per row block: the grid's column workgroups (FV: rows beyond run the stream)
     // (grid extents from the arguments, not gridDim: reading the implicit arguments put one
     // more dependent scalar round trip ahead of every workgroup's first operand load)
@@ -347,7 +328,7 @@ DEV void enc_latent_body(const StepArgs& a, const FvFold& fvf) {
             for (int c = 1; c < CT; ++c) v = mfma4(av[c], bw[c][w], v);
             return v;
         };
-        if constexpr (HO == 1 || HO == 2) {
+        if constexpr (HO == 1) {
 #pragma unroll
             for (int w = 0; w < 2 * NCT; ++w) {
                 const f32x4 sv = part(w);
@@ -414,15 +395,8 @@ DEV void enc_latent_body(const StepArgs& a, const FvFold& fvf) {
         VAEB_STAMP(a, 2);
         return;
     }
-    if constexpr (HO == 2) {
-        __syncthreads();
-        fx_add_nr<NCT>(a.acc_ml, m0, 2 * Z, pm, 32 * Z);
-        VAEB_STAMP(a, 2);
-        if (!arrive_last_all(a.cnt_ml + bx, nctH, &sflag)) return;
-    } else {
-        VAEB_STAMP(a, 2);
-        if (!arrive_last(a.cnt_ml + bx, nctH, &sflag)) return;
-    }
+    VAEB_STAMP(a, 2);
+    if (!arrive_last(a.cnt_ml + bx, nctH, &sflag)) return;
     VAEB_STAMP(a, 3);
 
     // ---- reducer (the last tile of row block bx): the element-wise operands ride the
@@ -444,13 +418,6 @@ DEV void enc_latent_body(const StepArgs& a, const FvFold& fvf) {
     const int64_t grow0 = (a.order ? (int64_t)ld_launch_const(a.cursor + kCtlNext) * a.row_base_mul : 0) + a.row_base_add;
     const int64_t stp = a.step ? *a.step : 0;
     float mu = 0.f, lv = 0.f;
-    if constexpr (HO == 2) {
-        if (n < Z) {
-            mu = fx_take(fx_at(a.acc_ml, (int64_t)m * 2 * Z + n), nctH);
-            lv = fx_take(fx_at(a.acc_ml, (int64_t)m * 2 * Z + Z + n), nctH);
-        }
-        VAEB_STAMP(a, 4);
-    }
     const int NF4 = 8 * Z;                  // float4 per slab (2Z columns x 16 rows)
     const int NP = 512 / NF4;               // slab partitions (threads >= NP * NF4 idle)
     if constexpr (HO == 0) {
@@ -542,35 +509,13 @@ __global__ __launch_bounds__(512) void enc_latent_fv_kernel(StepArgs a, FvFold f
 // wrote); 2 = the encoder's CT = 2 partial [mu | lv] slabs (enc_latent_body<.., HO = 3, 2>,
 // ceil(H / 32) per row block) summed here in fixed order, + bias, eps drawn here, and column
 // tile 0 stores mu, lv, eps, z and the KL / LA terms for the backward and the ELBO.
-// C2 (Bernoulli only, NB = 2): each workgroup owns TWO 16-column output tiles (the B
-// operand's second slot is W2's next 16 columns): half the workgroups, each recomputing hd
-// and (ZM 2) summing the encoder slabs once for 32 columns.
-struct PDecOutC2 : PDecOut {
-    DEV float b1(int n, int k, int w) const { return PDecOut::b1(n + 16 * w, k, 0); }
-    struct Pre { PDecOut::Pre t[2]; };
-    DEV Pre prefetch(int m0, int n0) const { return Pre{{PDecOut::prefetch(m0, n0), PDecOut::prefetch(m0, n0 + 16)}}; }
-    template <int NB>
-    DEV void epilogue(int m0, int n0, const f32x4 (&acc)[NB], const Pre& pre) const {
-#pragma unroll
-        for (int w = 0; w < 2; ++w) {
-            if (n0 + 16 * w >= a.D) break;   // the last pair's second tile past D: no partial slot
-            const f32x4 one[1] = {acc[w]};
-            PDecOut::epilogue<1>(m0, n0 + 16 * w, one, pre.t[w]);
-        }
-    }
-};
-
-// (C2 holds twice the W2 operands: up to 256 VGPRs, so no spills; MNIST's 175 two-tile
-// workgroups need one per CU anyway)
-template <int NB, int ZS, bool V1, int ZM, bool C2 = false>
-__global__ __launch_bounds__(512, C2 ? 2 : 4) void decout_z_kernel(StepArgs a) {
+template <int NB, int ZS, bool V1, int ZM>
+__global__ __launch_bounds__(512, 4) void decout_z_kernel(StepArgs a) {
     constexpr bool AT = ZM != 0;
-    constexpr int CW = C2 ? 32 : 16;   // output columns per workgroup
-    static_assert(!C2 || NB == 2, "two Bernoulli column tiles ride the NB = 2 slots");
-    using PD = std::conditional_t<C2, PDecOutC2, PDecOut>;
+    constexpr int CW = 16;   // output columns per workgroup
+    using PD = PDecOut;
     VAEB_STAMP(a, 0);
-    PD p{};
-    static_cast<PDecOut&>(p) = PDecOut{a, nullptr, a.Me, a.D, a.H};
+    PD p{a, nullptr, a.Me, a.D, a.H};
     p.prepare_at(nullptr);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int li = lane & 15, q = lane >> 4;

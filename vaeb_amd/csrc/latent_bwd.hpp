@@ -184,15 +184,8 @@ DEV void dhd_dz_body(const PDhdT<V>& p0, int bx, int by, f32x4* red, int sid) {
         VAEB_STAMP_AT(a, sid, 2);
         return;
     }
-    if constexpr (HO == 2) {
-        __syncthreads();
-        fx_add_nr<NCT>(a.acc_dz, rbl * 16, 2 * Z, pm, 32 * Z);
-        VAEB_STAMP_AT(a, sid, 2);
-        if (!arrive_last_all(a.cnt_dz + rbl, nctH * a.L, &sflag)) return;
-    } else {
-        VAEB_STAMP_AT(a, sid, 2);
-        if (!arrive_last(a.cnt_dz + rbl, nctH * a.L, &sflag)) return;
-    }
+    VAEB_STAMP_AT(a, sid, 2);
+    if (!arrive_last(a.cnt_dz + rbl, nctH * a.L, &sflag)) return;
     VAEB_STAMP_AT(a, sid, 3);
 
     // ---- reducer: latent row block rbl, all L planes.  Thread (ml, j) owns one element;
@@ -219,15 +212,7 @@ DEV void dhd_dz_body(const PDhdT<V>& p0, int bx, int by, f32x4* red, int sid) {
     const int NP = 512 / NF4;         // slab partitions (threads >= NP * NF4 idle)
     const int f = threadIdx.x % NF4, part = threadIdx.x / NF4;
     float dzsum = 0.f, dzes = 0.f;
-    if constexpr (HO == 2) {   // the summed S = sum_l dZ_l and E = sum_l dZ_l eps_l (dZ not stored)
-        if (j < Z) {
-            dzsum = fx_take(fx_at(a.acc_dz, (int64_t)m * 2 * Z + j), nctH * a.L);
-            dzes = fx_take(fx_at(a.acc_dz, (int64_t)m * 2 * Z + Z + j), nctH * a.L);
-        }
-        dzsum = valid ? dzsum : 0.f;
-        dzes = valid ? dzes : 0.f;
-    }
-    for (int s = 0; s < (HO == 2 ? 0 : a.L); ++s) {
+    for (int s = 0; s < a.L; ++s) {
         const int64_t first = ((int64_t)s * nrb + rbl) * nctH * NF4;
         constexpr int SV = 12;
         f32x4 sum = zero4();

@@ -266,13 +266,13 @@ struct PDecOut {
             const int m = m0 + 4 * (lane >> 4) + r;
             const int i = m % a.Mbp;
             const bool valid = ncol && i < a.Mb;
-            float lp = 0.f, d2 = 0.f, d6 = 0.f, yv = 0.f;
+            float lp = 0.f, d2 = 0.f, d6 = 0.f, yv = 0.f, a6 = 0.f;
             if (valid) {
                 const float xv = pre.xv[r];
                 const float a2 = acc[0][r] + b2;
                 yv = sigmoidf(a2);
                 if (a.dec == DEC_GAUSSIAN) {
-                    const float a6 = acc[NB - 1][r] + b6;
+                    a6 = acc[NB - 1][r] + b6;
                     const float rr = xv - yv;
                     const float e = fexp(-a6);
                     lp = -kHalfLog2Pi - 0.5f * a6 - 0.5f * rr * rr * e;
@@ -290,6 +290,9 @@ struct PDecOut {
                     if (a.dec == DEC_GAUSSIAN) a.dA6[o] = d6;
                 } else if (a.mode == MODE_RECON) {
                     a.y[o] = yv;
+                    // the decoder's log-sigma head (VAEB.py:258, freyFace.py:178): the dA6
+                    // plane is free outside training
+                    if (a.dec == DEC_GAUSSIAN) a.dA6[o] = a6;
                 }
             }
             lp = sum16(lp);

@@ -10,6 +10,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdarg>
 #include <cstdlib>
 #include <cstdio>
@@ -114,7 +115,8 @@ struct vaeb_ctx {
     int* ictl = nullptr;          // cursor, cur_batch, order[kOrderCap], next (tile_engine.hpp)
     int64_t* step = nullptr;
     float* elbo_out = nullptr;
-    double* epoch = nullptr;      // [2]
+    double* epoch = nullptr;      // [2] of the control block blk (kernels_aux.hpp kBlk*)
+    uint64_t* blk = nullptr;      // epoch [2], status, elbo_out, fixed-point guard word, acc_ml, acc_dz
     double* eval_acc = nullptr;   // [2]
     // noise
     int eps_mode = VAEB_EPS_PHILOX;
@@ -139,29 +141,19 @@ struct vaeb_ctx {
     hipGraphExec_t g1[2] = {nullptr, nullptr};
     hipGraphExec_t gN[kGraphSteps + 1] = {};  // gN[n]: n steps from arena 0 (run_steps)
     bool graph_failed = false;
+    std::string graph_err;        // why the capture failed (vaeb_graph_status)
     // comm
     ncclComm_t comm = nullptr;
     int rank = 0, world = 1;
     hipStream_t s3 = nullptr;     // bf16 engine: dW2 (| dW6) + Adagrad forked beside the backward chain
     hipEvent_t fk_ev[4] = {};     // fork after dhd, s3's work done, [dMu | dLv] ready, ELBO partials
     bool bf_fork = true;          // VAEB_BF_FORK=0: dW2 in the dhd grid (bf_fuse) or after it
-    bool w3_256 = true;           // forked step: dW3 on 256 x 256 tiles beside dW2 (VAEB_BF_W3_256=0: 256 x 128)
     hipStream_t s2 = nullptr;     // DP: the gradient buckets' all-reduces and their Adagrad
     hipEvent_t dp_ev[3] = {};     // fork after dW2, bucket A reduced, bucket A updated
     bool dp_overlap = false;      // bucket A on s2 (bf16 engine; VAEB_DP_OVERLAP=0/1 overrides)
-    int dz_split = 8;             // P67 column splits per row block (fused.hpp dz_dh_body; VAEB_DZ_SPLIT)
     bool fold_bwd = true;         // Z <= 32: latent backward folded into the dhd launch (VAEB_FOLD_BWD=0: P67)
-    int w3_ts = 1;                // folded path's last launch: tile width / 16 (VAEB_W3_TS)
-    bool w3_gvec = true;          // ... 16-byte panel loads decided per group (VAEB_W3_GVEC)
-    int atomic_ho = 1;            // folded latent hand-offs: 1 by fan-in (ho_mode), 0 slabs, 2 ticketed atomics
-    int decout_c2 = 0;            // Bernoulli decoder, 2 column tiles per workgroup: -1 auto, VAEB_DECOUT_C2=0|1
+    int atomic_ho = 1;            // folded latent hand-offs: 1 by fan-in (ho_mode), 0 slabs
     int enc_red = -1;             // encoder slabs summed by the decoder launch: -1 auto, VAEB_ENC_RED=0|1
-    bool bf_lat4 = true;          // bf16 engine: 16-byte latent kernels where shapes allow (VAEB_BF_LAT4)
-    int enc_ct = 0;               // encoder h column tiles per workgroup: 0 auto, VAEB_ENC_CT=1|2 forces
-    bool enc_2b = false;          // bf16 enc on 256 x 128 tiles, 2 blocks / CU (VAEB_BF_ENC2B)
-    bool dhd_2b = false;          // bf16 forked dhd on 256 x 128 tiles, 2 blocks / CU (VAEB_BF_DHD2B)
-    bool decout_2b = true;        // bf16 Bernoulli decout on 256 x 128 tiles, 2 blocks / CU (VAEB_DECOUT_2B=0: 256 x 256)
-    bool bf_fuse = true;          // bf16 engine: dhd + dW2 (| dW6) in one grid (VAEB_BF_FUSE=0: two launches)
     // profiling
     hipEvent_t pev[kMaxProfKernels + 1] = {};
     int prof_n = 0, prof_reps = 1;
@@ -247,15 +239,12 @@ bool fused_latent(const vaeb_ctx* c) { return c->c.Z <= 32; }
 // the atomic form wins only at a small fan-in (contributors per element): Frey 560-200-2
 // (13 column tiles) 38.5 -> 32.2 us per step; MNIST 784-500-20 (32 column tiles) 44.5 ->
 // 49.3 us.  Forward fan-in: the H column tiles; backward: H column tiles x L planes.
-// HO = 2 (VAEB_ATOMIC_HO=2 only): the same adds without return + the slab protocol's ticket,
-// the last arriver reading each sum with one 8-B exchange -- measured slower than both
-// (MNIST 53.6 us, Frey 35.0 us): at fan-in 32 the 64-bit adds to one word serialise either
-// way.  VAEB_ATOMIC_HO=0 forces the slabs.
-constexpr int kFxMaxFanIn = 16;
+// (A third form -- the same adds without return + the slab protocol's ticket, the last
+// arriver reading each sum with one exchange -- measured slower than both, MNIST 53.6 us,
+// Frey 35.0 us, and was removed in round 3.)  VAEB_ATOMIC_HO=0 forces the slabs.
 int ho_mode(const vaeb_ctx* c, int fan_in) {
-    if (c->atomic_ho == 0 || fan_in > 255) return 0;
-    if (c->atomic_ho == 2) return 2;
-    return fan_in <= kFxMaxFanIn ? 1 : 0;
+    if (c->atomic_ho == 0) return 0;
+    return fan_in <= kFxMaxFanIn ? 1 : 0;   // the count field holds <= 16 contributors (latent.hpp)
 }
 int ho_ml(const vaeb_ctx* c, int ct) { return ho_mode(c, cdiv(c->c.H, 16 * ct)); }
 int ho_dz(const vaeb_ctx* c) { return ho_mode(c, cdiv(c->c.H, 16) * c->c.L); }
@@ -289,22 +278,21 @@ ElboArgs base_elbo(vaeb_ctx* c, const StepArgs& a) {
     return e;
 }
 
-template <int NB, bool V1, int AT, bool C2>
+template <int NB, bool V1, int AT>
 void launch_decout_zv(hipStream_t s, dim3 grid, const StepArgs& a) {
     switch ((a.Z + 3) / 4) {
-        case 1: hipLaunchKernelGGL((decout_z_kernel<NB, 1, V1, AT, C2>), grid, dim3(512), 0, s, a); break;
-        case 2: hipLaunchKernelGGL((decout_z_kernel<NB, 2, V1, AT, C2>), grid, dim3(512), 0, s, a); break;
-        case 3: case 4: hipLaunchKernelGGL((decout_z_kernel<NB, 4, V1, AT, C2>), grid, dim3(512), 0, s, a); break;
-        case 5: hipLaunchKernelGGL((decout_z_kernel<NB, 5, V1, AT, C2>), grid, dim3(512), 0, s, a); break;
-        default: hipLaunchKernelGGL((decout_z_kernel<NB, 8, V1, AT, C2>), grid, dim3(512), 0, s, a); break;
+        case 1: hipLaunchKernelGGL((decout_z_kernel<NB, 1, V1, AT>), grid, dim3(512), 0, s, a); break;
+        case 2: hipLaunchKernelGGL((decout_z_kernel<NB, 2, V1, AT>), grid, dim3(512), 0, s, a); break;
+        case 3: case 4: hipLaunchKernelGGL((decout_z_kernel<NB, 4, V1, AT>), grid, dim3(512), 0, s, a); break;
+        case 5: hipLaunchKernelGGL((decout_z_kernel<NB, 5, V1, AT>), grid, dim3(512), 0, s, a); break;
+        default: hipLaunchKernelGGL((decout_z_kernel<NB, 8, V1, AT>), grid, dim3(512), 0, s, a); break;
     }
 }
-// C2: Bernoulli decoder with two 16-column tiles per workgroup (grid y = ceil(D / 32))
-template <int NB, int AT, bool C2 = false>
+template <int NB, int AT>
 void launch_decout_z(hipStream_t s, dim3 grid, const StepArgs& a) {
     auto al = [](const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
-    if ((a.H & 3) == 0 && al(a.W1) && al(a.b1)) launch_decout_zv<NB, true, AT, C2>(s, grid, a);
-    else launch_decout_zv<NB, false, AT, C2>(s, grid, a);
+    if ((a.H & 3) == 0 && al(a.W1) && al(a.b1)) launch_decout_zv<NB, true, AT>(s, grid, a);
+    else launch_decout_zv<NB, false, AT>(s, grid, a);
 }
 
 // dhd_dz_wgrad_kernel at compile-time NCT (latent col tiles), GCH, load width, AT
@@ -362,8 +350,7 @@ void launch_enc_latent(hipStream_t s, dim3 g1, const StepArgs& a, const FvFold& 
         }
         return;
     }
-    if (ct == 4) launch_enc_latent_ct<HO, 4>(s, g1, a, fvf, deep);
-    else if (ct == 2) launch_enc_latent_ct<HO, 2>(s, g1, a, fvf, deep);
+    if (ct == 2) launch_enc_latent_ct<HO, 2>(s, g1, a, fvf, deep);
     else launch_enc_latent_ct<HO, 1>(s, g1, a, fvf, deep);
 }
 
@@ -388,7 +375,7 @@ int enqueue_forward(vaeb_ctx* c, const StepArgs& a0, Prof& pr, const FvFold& fvf
         // auto: where the slab + ticket form would be chosen (fan-in > 16; MNIST 784-500-20
         // 43.8 -> 42.5 us); at a small fan-in the counted atomics stay (Frey 30.8 vs 32.7 us)
         const bool red = (c->enc_red < 0 ? ho_ml(c, 1) == 0 : c->enc_red == 1) && fvf.rows == 0 && cdiv(a.H, 32) <= 32;
-        const int ct = red ? 2 : (c->enc_ct ? c->enc_ct : (fvf.rows > 0 ? 2 : 1));
+        const int ct = (red || fvf.rows > 0) ? 2 : 1;
         const dim3 g1(a.Mbp / 16, cdiv(a.H, 16 * ct) + fvf.rows);
         const bool deep = cdiv(cdiv(a.D, 16), 8) > 4;
         const int ho = red ? 3 : ho_ml(c, ct);
@@ -397,21 +384,16 @@ int enqueue_forward(vaeb_ctx* c, const StepArgs& a0, Prof& pr, const FvFold& fvf
         REP(pr) {
             if (ho == 3) launch_enc_latent<3>(s, g1, a, fvf, deep, ct);
             else if (ho == 1) launch_enc_latent<1>(s, g1, a, fvf, deep, ct);
-            else if (ho == 2) launch_enc_latent<2>(s, g1, a, fvf, deep, ct);
             else launch_enc_latent<0>(s, g1, a, fvf, deep, ct);
         }
         CHECK_LAUNCH();
         a.dbg = next_dbg(c);
-        // Bernoulli decoder with two column tiles per workgroup (VAEB_DECOUT_C2)
-        const bool c2 = !gaussian(c) && (c->decout_c2 < 0 ? at == 2 : c->decout_c2 == 1);
-        const dim3 g4(a.Me / 16, cdiv(a.D, c2 ? 32 : 16));
+        // (two 16-column tiles per Bernoulli workgroup, 175 instead of 343: 43.3 vs 43.1 us,
+        // removed in round 3)
+        const dim3 g4(a.Me / 16, cdiv(a.D, 16));
         pr.mark(17);
         REP(pr) {
-            if (c2) {
-                if (at == 2) launch_decout_z<2, 2, true>(s, g4, a);
-                else if (at == 1) launch_decout_z<2, 1, true>(s, g4, a);
-                else launch_decout_z<2, 0, true>(s, g4, a);
-            } else if (gaussian(c)) {
+            if (gaussian(c)) {
                 if (at == 2) launch_decout_z<2, 2>(s, g4, a);
                 else if (at == 1) launch_decout_z<2, 1>(s, g4, a);
                 else launch_decout_z<2, 0>(s, g4, a);
@@ -482,6 +464,7 @@ bool dhd_vec(const StepArgs& a) {
 constexpr int kWTJ_P5 = 32;    // dW2 (| dW6), beside the dhd tiles
 constexpr int kWTJ_P67 = 16;   // dW1, beside the dz / dh phase
 constexpr int kWTJ_W = 16;     // standalone launches: dW3 | dW45 (+ ELBO), non-fused dW1
+constexpr int kDzSplit = 8;    // P67 column splits per row block (fused.hpp dz_dh_body)
 
 // Weight-gradient arguments over `n` groups whose tiles start at block `base` of the
 // launch (+ the ELBO workgroup when e != nullptr).  *vec: 16-byte panel loads are legal.
@@ -531,24 +514,18 @@ int launch_wgrad(vaeb_ctx* c, hipStream_t s, const WGroup* groups, int n, const 
     if (da3) {
         if (n != 3) return fail(VAEB_ERR_ARG, "internal: the dA3-forming launch takes three groups");
         WGradArgs3 w;
-        const int tw = c->w3_ts * 16;
+        // 16-column tiles (32-wide: MNIST 46.3 vs 44.7 us, Frey 41.5 vs 38.4, removed in round 3)
         int vm = 0;   // 16-byte panel loads per group (Frey: dW3 yes, dW4 | dW5 and dW1 not)
-        if (int rc = prep_wgrad(c, groups, n, opt, e, a, 0, w, vec, tw, &vm)) return rc;
+        if (int rc = prep_wgrad(c, groups, n, opt, e, a, 0, w, vec, 16, &vm)) return rc;
         w.da3 = *da3;
-        if (!c->w3_gvec) vm = vec ? 7 : 0;
         const dim3 grid(w.total_wgs + (e ? 1 : 0));
-        auto go = [&](auto ts) {
-            constexpr int TS = decltype(ts)::value;
-            switch (vm) {
-                case 7: hipLaunchKernelGGL((wgrad3_kernel<7, TS>), grid, dim3(256), 0, s, w); break;
-                case 1: hipLaunchKernelGGL((wgrad3_kernel<1, TS>), grid, dim3(256), 0, s, w); break;
-                case 3: hipLaunchKernelGGL((wgrad3_kernel<3, TS>), grid, dim3(256), 0, s, w); break;
-                case 5: hipLaunchKernelGGL((wgrad3_kernel<5, TS>), grid, dim3(256), 0, s, w); break;
-                default: hipLaunchKernelGGL((wgrad3_kernel<0, TS>), grid, dim3(256), 0, s, w); break;
-            }
-        };
-        if (tw == 32) go(std::integral_constant<int, 2>{});
-        else go(std::integral_constant<int, 1>{});
+        switch (vm) {
+            case 7: hipLaunchKernelGGL((wgrad3_kernel<7, 1>), grid, dim3(256), 0, s, w); break;
+            case 1: hipLaunchKernelGGL((wgrad3_kernel<1, 1>), grid, dim3(256), 0, s, w); break;
+            case 3: hipLaunchKernelGGL((wgrad3_kernel<3, 1>), grid, dim3(256), 0, s, w); break;
+            case 5: hipLaunchKernelGGL((wgrad3_kernel<5, 1>), grid, dim3(256), 0, s, w); break;
+            default: hipLaunchKernelGGL((wgrad3_kernel<0, 1>), grid, dim3(256), 0, s, w); break;
+        }
     } else {
         WGradArgs w;
         if (int rc = prep_wgrad(c, groups, n, opt, e, a, 0, w, vec, kWTJ_W)) return rc;
@@ -729,7 +706,6 @@ int enqueue_train_step(vaeb_ctx* c, int par, bool prof, bool fresh = true) {
         REP(pr) {
             switch (ho_dz(c)) {
                 case 1: launch_dhd_dz<kWTJ_P5 / 16, 1>(s, grid, p5, p5s, w, ntile, gx, vec, deep); break;
-                case 2: launch_dhd_dz<kWTJ_P5 / 16, 2>(s, grid, p5, p5s, w, ntile, gx, vec, deep); break;
                 default: launch_dhd_dz<kWTJ_P5 / 16, 0>(s, grid, p5, p5s, w, ntile, gx, vec, deep); break;
             }
         }
@@ -761,7 +737,7 @@ int enqueue_train_step(vaeb_ctx* c, int par, bool prof, bool fresh = true) {
         a.dbg = next_dbg(c);
         WGroup g3 = make_group(c, c->z, a.Z, a.Me, 0, a.Z, c->dA1, a.H, a.H, nullptr, 0, 0, a.Me, 3, bo + 3, -1, -1);
         if (fused_latent(c)) {
-            const int nrow = a.Mbp / 16 * std::max(1, std::min(c->dz_split, cdiv(a.H, 16)));
+            const int nrow = a.Mbp / 16 * std::max(1, std::min(kDzSplit, cdiv(a.H, 16)));
             WGradArgs w;
             bool vec;
             if (int rc = prep_wgrad(c, &g3, 1, opt, nullptr, a, nrow, w, vec, kWTJ_P67)) return rc;
@@ -872,7 +848,18 @@ int run_steps(vaeb_ctx* c, int n) {
             int rc = capture(c, 1, 0, &c->g1[0]);
             if (rc == 0) rc = capture(c, 1, 1, &c->g1[1]);
             for (int m = 1; m <= kGraphSteps && rc == 0; ++m) rc = capture(c, m, 0, &c->gN[m]);
-            if (rc) { c->graph_failed = true; free_graphs(c); (void)hipGetLastError(); }
+            if (rc) {
+                // never silent: the reason is kept for vaeb_graph_status, and with a
+                // communicator of more than one rank the call fails (an eager multi-rank
+                // step is not the configuration that was measured or tested)
+                c->graph_failed = true;
+                c->graph_err = g_err;
+                free_graphs(c);
+                (void)hipGetLastError();
+                if (c->comm && c->world > 1)
+                    return fail(VAEB_ERR_HIP, "graph capture of the data-parallel step failed at world %d: %s",
+                                c->world, c->graph_err.c_str());
+            }
         }
         if (!c->graph_failed) {
             int i = 0;
@@ -969,21 +956,10 @@ int vaeb_create(const vaeb_config* cfg, vaeb_ctx** out) {
     hipError_t e = hipSetDevice(g.device);
     if (e != hipSuccess) { delete c; return fail(VAEB_ERR_HIP, "hipSetDevice(%d): %s", g.device, hipGetErrorString(e)); }
     e = hipStreamCreateWithFlags(&c->s, hipStreamNonBlocking);
-    if (const char* ds = getenv("VAEB_DZ_SPLIT")) c->dz_split = atoi(ds);
     if (const char* fb = getenv("VAEB_FOLD_BWD")) c->fold_bwd = atoi(fb) != 0;
-    if (const char* ts = getenv("VAEB_W3_TS")) c->w3_ts = atoi(ts) == 2 ? 2 : 1;
-    if (const char* gv = getenv("VAEB_W3_GVEC")) c->w3_gvec = atoi(gv) != 0;
-    if (const char* bf = getenv("VAEB_BF_FUSE")) c->bf_fuse = atoi(bf) != 0;
     if (const char* bk = getenv("VAEB_BF_FORK")) c->bf_fork = atoi(bk) != 0;
-    if (const char* w3 = getenv("VAEB_BF_W3_256")) c->w3_256 = atoi(w3) != 0;
-    if (const char* d2 = getenv("VAEB_DECOUT_2B")) c->decout_2b = atoi(d2) != 0;
-    if (const char* e2 = getenv("VAEB_BF_ENC2B")) c->enc_2b = atoi(e2) != 0;
-    if (const char* h2 = getenv("VAEB_BF_DHD2B")) c->dhd_2b = atoi(h2) != 0;
-    if (const char* ec = getenv("VAEB_ENC_CT")) { const int v = atoi(ec); c->enc_ct = (v == 2 || v == 4) ? v : 1; }
-    if (const char* ah = getenv("VAEB_ATOMIC_HO")) c->atomic_ho = atoi(ah);
-    if (const char* l4 = getenv("VAEB_BF_LAT4")) c->bf_lat4 = atoi(l4) != 0;
+    if (const char* ah = getenv("VAEB_ATOMIC_HO")) c->atomic_ho = atoi(ah) != 0 ? 1 : 0;
     if (const char* er = getenv("VAEB_ENC_RED")) c->enc_red = atoi(er) != 0 ? 1 : 0;
-    if (const char* c2 = getenv("VAEB_DECOUT_C2")) c->decout_c2 = atoi(c2) != 0 ? 1 : 0;
     if (e != hipSuccess) { delete c; return fail(VAEB_ERR_HIP, "stream/event create: %s", hipGetErrorString(e)); }
     const int64_t D = g.D, H = g.H, Z = g.Z;
     std::vector<int64_t> sz = {D * H, H * Z, H * Z, Z * H, H * D};
@@ -1011,8 +987,6 @@ int vaeb_create(const vaeb_config* cfg, vaeb_ctx** out) {
     rc = rc ? rc : dalloc(&c->xeval, (size_t)R * D);
     rc = rc ? rc : dalloc(&c->ictl, kCtlOrder + kOrderCap);
     rc = rc ? rc : dalloc(&c->step, 1);
-    rc = rc ? rc : dalloc(&c->elbo_out, 1);
-    rc = rc ? rc : dalloc(&c->epoch, 2);
     rc = rc ? rc : dalloc(&c->eval_acc, 2);
     rc = rc ? rc : dalloc(&c->h, (size_t)R * H);
     rc = rc ? rc : dalloc(&c->mu, (size_t)R * Z);
@@ -1036,8 +1010,15 @@ int vaeb_create(const vaeb_config* cfg, vaeb_ctx** out) {
         rc = rc ? rc : dalloc(&c->slab_dz, (size_t)(g.L * Bp * nctH * 32));
         rc = rc ? rc : dalloc(&c->cnt_ml, (size_t)(Bp / 16));
         rc = rc ? rc : dalloc(&c->cnt_dz, (size_t)(Bp / 16));
-        rc = rc ? rc : dalloc(&c->acc_ml, (size_t)(Bp * 2 * Z * kFxStride));
-        rc = rc ? rc : dalloc(&c->acc_dz, (size_t)(Bp * 2 * Z * kFxStride));
+        // one allocation: the guard word the contributors set sits at acc_ml[-1] (latent.hpp fx_inc)
+        const size_t nacc = (size_t)(Bp * 2 * Z * kFxStride);
+        rc = rc ? rc : dalloc(&c->blk, kBlkAcc + 2 * nacc);
+        if (!rc) {
+            c->epoch = reinterpret_cast<double*>(c->blk);
+            c->elbo_out = reinterpret_cast<float*>(c->blk + kBlkElbo);
+            c->acc_ml = c->blk + kBlkAcc;
+            c->acc_dz = c->acc_ml + nacc;
+        }
     }
     if (!rc && is_bf16(c)) rc = bf_alloc(c);
     if (!rc && is_bf16(c)) {
@@ -1072,17 +1053,15 @@ int vaeb_destroy(vaeb_ctx* c) {
     bf_free(c);
     if (c->comm) ncclCommDestroy(c->comm);
     float* fp[] = {c->theta2[0], c->theta2[1], c->acc, c->grad, c->fvmu, c->fvsg, c->fvam, c->fvas, c->fv_part, c->data, c->xeval, c->xval,
-                   c->elbo_out, c->eps_in, c->h, c->mu, c->lv, c->eps, c->z, c->hd, c->y, c->dA2, c->dA1,   // dA6 lives in dA2's block
+                   c->eps_in, c->h, c->mu, c->lv, c->eps, c->z, c->hd, c->y, c->dA2, c->dA1,   // dA6 lives in dA2's block
                    c->dZ, c->dMuLv, c->dA3, c->kl_part, c->lp_part, c->slab_ml, c->slab_dz, c->yacc,
                    c->fvzeta};
     for (float* p : fp) if (p) hipFree(p);
     if (c->cnt_ml) hipFree(c->cnt_ml);
     if (c->cnt_dz) hipFree(c->cnt_dz);
-    if (c->acc_ml) hipFree(c->acc_ml);
-    if (c->acc_dz) hipFree(c->acc_dz);
+    if (c->blk) hipFree(c->blk);   // epoch, elbo_out, acc_ml, acc_dz live in it
     if (c->ictl) hipFree(c->ictl);
     if (c->step) hipFree(c->step);
-    if (c->epoch) hipFree(c->epoch);
     if (c->eval_acc) hipFree(c->eval_acc);
     if (c->h_ctl) hipHostFree(c->h_ctl);
     if (c->h_elbo) hipHostFree(c->h_elbo);
@@ -1170,7 +1149,8 @@ int vaeb_get_fv_state(vaeb_ctx* c, float* mu, float* sg, float* am, float* as, i
 int vaeb_set_eps_mode(vaeb_ctx* c, int32_t mode, uint64_t seed) {
     if (!c || (mode != VAEB_EPS_PHILOX && mode != VAEB_EPS_HOST)) return fail(VAEB_ERR_ARG, "bad eps mode");
     HIP_TRY(hipStreamSynchronize(c->s));
-    if (mode != c->eps_mode) { free_graphs(c); c->graph_failed = false; }
+    // captured steps hold the eps mode's kernels and the Philox seed by value (make_args)
+    if (mode != c->eps_mode || seed != c->seed) { free_graphs(c); c->graph_failed = false; }
     c->eps_mode = mode;
     c->seed = seed;
     return 0;
@@ -1223,16 +1203,27 @@ static int host_eps_ready(vaeb_ctx* c, int64_t rows) {
     return 0;
 }
 
+// The sticky step status read at a sync point (kernels_aux.hpp elbo_emit): cleared, and
+// reported as VAEB_ERR_NUMERIC.
+static int take_status(vaeb_ctx* c, uint64_t st) {
+    if (!st) return 0;
+    HIP_TRY(hipMemsetAsync(c->blk + kBlkStatus, 0, sizeof(uint64_t), c->s));
+    HIP_TRY(hipStreamSynchronize(c->s));
+    return fail(VAEB_ERR_NUMERIC, "the step overflowed the fixed-point latent hand-off (a partial outside +-2^17, "
+                                  "NaN or inf): its latent values are NaN");
+}
+
 int vaeb_update(vaeb_ctx* c, int32_t batch_index, float* out) {
     if (!c) return fail(VAEB_ERR_ARG, "null ctx");
     if (int rc = check_batches(c, &batch_index, 1)) return rc;
     if (int rc = host_eps_ready(c, c->c.B)) return rc;
     if (int rc = upload_order(c, &batch_index, 1)) return rc;
     if (int rc = run_steps(c, 1)) return rc;
-    HIP_TRY(hipMemcpyAsync(c->h_elbo, c->elbo_out, sizeof(float), hipMemcpyDeviceToHost, c->s));
+    // [status, SGVB / B] in one copy (kernels_aux.hpp kBlk*)
+    HIP_TRY(hipMemcpyAsync(c->h_elbo, c->blk + kBlkStatus, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, c->s));
     HIP_TRY(hipStreamSynchronize(c->s));
-    if (out) *out = c->h_elbo[0];
-    return 0;
+    if (out) *out = c->h_elbo[2];
+    return take_status(c, reinterpret_cast<const uint64_t*>(c->h_elbo)[0]);
 }
 
 int vaeb_update_many(vaeb_ctx* c, const int32_t* idx, int32_t n) {
@@ -1255,12 +1246,17 @@ int vaeb_update_async(vaeb_ctx* c, int32_t batch_index) { return vaeb_update_man
 
 int vaeb_epoch_elbo(vaeb_ctx* c, double* out_sum, int64_t* out_steps) {
     if (!c) return fail(VAEB_ERR_ARG, "null ctx");
-    HIP_TRY(hipMemcpyAsync(c->h_d2, c->epoch, 2 * sizeof(double), hipMemcpyDeviceToHost, c->s));
-    HIP_TRY(hipMemsetAsync(c->epoch, 0, 2 * sizeof(double), c->s));
+    // epoch sums and the sticky status in one copy, then all three cleared
+    HIP_TRY(hipMemcpyAsync(c->h_d2, c->epoch, 3 * sizeof(double), hipMemcpyDeviceToHost, c->s));
+    HIP_TRY(hipMemsetAsync(c->epoch, 0, 3 * sizeof(double), c->s));
     HIP_TRY(hipStreamSynchronize(c->s));
     if (out_sum) *out_sum = c->h_d2[0];
     if (out_steps) *out_steps = (int64_t)c->h_d2[1];
-    return 0;
+    uint64_t st;
+    memcpy(&st, &c->h_d2[2], sizeof(st));
+    return st ? fail(VAEB_ERR_NUMERIC, "a step since the last read overflowed the fixed-point latent hand-off "
+                                       "(a partial outside +-2^17, NaN or inf): its latent values are NaN")
+              : 0;
 }
 
 int vaeb_synchronize(vaeb_ctx* c) {
@@ -1283,7 +1279,8 @@ static int eval_arena(vaeb_ctx* c, int* epar) {
 
 // One fp32 chunk: `rows` device rows at x = global rows [r0, r0 + rows).  MODE_EVAL adds
 // the chunk's SGVB into eval_acc; MODE_RECON copies the decoder means to out_y (host).
-static int eval_chunk_f32(vaeb_ctx* c, int epar, const float* x, int rows, int64_t r0, int mode, float* out_y) {
+static int eval_chunk_f32(vaeb_ctx* c, int epar, const float* x, int rows, int64_t r0, int mode, float* out_y,
+                          float* out_lv = nullptr) {
     const vaeb_config& g = c->c;
     StepArgs a = make_args(c, epar, rows, mode, x, false);
     a.row_base_add = r0;
@@ -1293,6 +1290,8 @@ static int eval_chunk_f32(vaeb_ctx* c, int epar, const float* x, int rows, int64
     if (int rc = enqueue_forward(c, a, pr)) return rc;
     if (mode == MODE_RECON) {
         HIP_TRY(hipMemcpyAsync(out_y, c->y, sizeof(float) * (size_t)rows * g.D, hipMemcpyDeviceToHost, c->s));
+        if (out_lv)
+            HIP_TRY(hipMemcpyAsync(out_lv, c->dA6, sizeof(float) * (size_t)rows * g.D, hipMemcpyDeviceToHost, c->s));
     } else {
         ElboArgs e = base_elbo(c, a);
         e.eval_acc = c->eval_acc;
@@ -1330,7 +1329,8 @@ static int eval_finish(vaeb_ctx* c, int64_t n, bool allreduce, double* out_sum) 
 }
 
 // Host rows: each chunk is staged through xeval (stream-ordered, one sync at the end).
-static int eval_rows(vaeb_ctx* c, const float* x, int64_t n, int mode, float* out_y, double* out_sum) {
+static int eval_rows(vaeb_ctx* c, const float* x, int64_t n, int mode, float* out_y, double* out_sum,
+                     float* out_lv = nullptr) {
     if (!c || !x || n <= 0) return fail(VAEB_ERR_ARG, "bad arguments");
     if (mode == MODE_EVAL && c->eps_mode == VAEB_EPS_HOST && c->eps_rows != n)
         return fail(VAEB_ERR_STATE, "host eps mode: validate needs eps for %lld rows (pushed %lld)", (long long)n,
@@ -1348,7 +1348,8 @@ static int eval_rows(vaeb_ctx* c, const float* x, int64_t n, int mode, float* ou
             continue;
         }
         HIP_TRY(hipMemcpyAsync(c->xeval, x + r0 * g.D, sizeof(float) * (size_t)rows * g.D, hipMemcpyHostToDevice, c->s));
-        if (int rc = eval_chunk_f32(c, epar, c->xeval, rows, r0, mode, yo)) return rc;
+        if (int rc = eval_chunk_f32(c, epar, c->xeval, rows, r0, mode, yo, out_lv ? out_lv + r0 * g.D : nullptr))
+            return rc;
     }
     if (mode == MODE_EVAL) return eval_finish(c, n, false, out_sum);
     HIP_TRY(hipStreamSynchronize(c->s));
@@ -1482,6 +1483,9 @@ int vaeb_checkpoint_load(vaeb_ctx* c, const char* path) {
     CkptHeader h{};
     if (fread(&h, sizeof(h), 1, fc.f) != 1 || memcmp(h.magic, kCkptMagic, 8) != 0 || h.version != 1)
         return fail(VAEB_ERR_ARG, "checkpoint: %s is not a version-1 vaeb checkpoint", path);
+    if (h.objective != g.objective || h.dtype != g.dtype)
+        return fail(VAEB_ERR_ARG, "checkpoint: %s was written by an objective=%d dtype=%d context, this one is "
+                    "objective=%d dtype=%d", path, h.objective, h.dtype, g.objective, g.dtype);
     if (h.D != g.D || h.H != g.H || h.Z != g.Z || h.L != g.L || h.decoder != g.decoder ||
         h.estimator != g.estimator || h.P != c->P)
         return fail(VAEB_ERR_ARG, "checkpoint: %s holds a %d-%d-%d L=%d dec=%d est=%d model, the context is "
@@ -1502,26 +1506,32 @@ int vaeb_checkpoint_load(vaeb_ctx* c, const char* path) {
         HIP_TRY(hipStreamSynchronize(c->s));
     }
     HIP_TRY(hipMemcpy(c->step, &h.step, sizeof(int64_t), hipMemcpyHostToDevice));
-    if (h.eps_mode != c->eps_mode) { free_graphs(c); c->graph_failed = false; }
+    // captured steps hold the eps mode's kernels and the Philox seed by value (make_args)
+    if (h.eps_mode != c->eps_mode || h.seed != c->seed) { free_graphs(c); c->graph_failed = false; }
     c->eps_mode = h.eps_mode;
     c->seed = h.seed;
     return 0;
 }
 
 int vaeb_reconstruct(vaeb_ctx* c, const float* x, int64_t n, float* out_y) {
-    if (!out_y) return fail(VAEB_ERR_ARG, "null out_y");
-    return eval_rows(c, x, n, MODE_RECON, out_y, nullptr);
+    return vaeb_reconstruct_full(c, x, n, 0, out_y, nullptr);
 }
 
-// VAEB.reconstruct with n_samples > 0 (VAEB.py:271-291): the decoder output averaged over
-// n_samples posterior draws z_s = mu + exp(lv / 2) eps_s, summed on device in sample order.
-// eps_s: Philox stream s + 1 of the validation domain, or (host eps mode) rows
-// [s * n, (s + 1) * n) of the pushed eps.  Continuous decoder: the mean of the decoder
-// means (the reference's final multivariate_normal draw is not reproduced).
 int vaeb_reconstruct_sampled(vaeb_ctx* c, const float* x, int64_t n, int32_t n_samples, float* out_y) {
-    if (!out_y) return fail(VAEB_ERR_ARG, "null out_y");
-    if (n_samples <= 0) return eval_rows(c, x, n, MODE_RECON, out_y, nullptr);
-    if (!c || !x || n <= 0) return fail(VAEB_ERR_ARG, "bad arguments");
+    return vaeb_reconstruct_full(c, x, n, n_samples, out_y, nullptr);
+}
+
+// VAEB.reconstruct (VAEB.py:267-291) before its closing multivariate_normal draw: the
+// decoder outputs at z = mu (n_samples <= 0) or averaged over n_samples posterior draws
+// z_s = mu + exp(lv / 2) eps_s, summed on device in sample order (:279-291).  eps_s:
+// Philox stream s + 1 of the validation domain, or (host eps mode) rows [s * n, (s + 1) * n)
+// of the pushed eps.  out_lv (Gaussian decoder, fp32 engine): the log-sigma head, averaged
+// the same way (:284, 289) -- the caller's draw is y_mu + exp(y_log_sigma) * N(0, 1) (:295-297).
+int vaeb_reconstruct_full(vaeb_ctx* c, const float* x, int64_t n, int32_t n_samples, float* out_y, float* out_lv) {
+    if (!c || !x || n <= 0 || !out_y) return fail(VAEB_ERR_ARG, "bad arguments");
+    if (out_lv && !gaussian(c)) return fail(VAEB_ERR_ARG, "the log-sigma head exists for the Gaussian decoder only");
+    if (out_lv && is_bf16(c)) return fail(VAEB_ERR_ARG, "the log-sigma output is served by fp32 contexts");
+    if (n_samples <= 0) return eval_rows(c, x, n, MODE_RECON, out_y, nullptr, out_lv);
     const bool host = c->eps_mode == VAEB_EPS_HOST;
     if (host && c->eps_rows != n * n_samples)
         return fail(VAEB_ERR_STATE, "host eps mode: sampled reconstruct needs eps for %lld rows (n * n_samples), pushed %lld",
@@ -1529,8 +1539,11 @@ int vaeb_reconstruct_sampled(vaeb_ctx* c, const float* x, int64_t n, int32_t n_s
     const vaeb_config& g = c->c;
     const int chunk = g.max_eval_rows;
     if (!c->yacc) {
-        if (int rc = dalloc(&c->yacc, (size_t)chunk * g.D)) return rc;
+        if (int rc = dalloc(&c->yacc, (size_t)chunk * g.D * (gaussian(c) ? 2 : 1))) return rc;
     }
+    float* lacc = gaussian(c) ? c->yacc + (size_t)chunk * g.D : nullptr;
+    int epar = c->par;
+    if (!is_bf16(c)) if (int rc = eval_arena(c, &epar)) return rc;
     for (int64_t r0 = 0; r0 < n; r0 += chunk) {
         const int rows = (int)std::min<int64_t>(chunk, n - r0);
         const int64_t ny = (int64_t)rows * g.D;
@@ -1551,7 +1564,7 @@ int vaeb_reconstruct_sampled(vaeb_ctx* c, const float* x, int64_t n, int32_t n_s
                 f.yout = c->y;
                 if (int rc = bf_forward(c, c->par, f, pr)) return rc;
             } else {
-                StepArgs a = make_args(c, c->par, rows, MODE_RECON, c->xeval, false);
+                StepArgs a = make_args(c, epar, rows, MODE_RECON, c->xeval, false);
                 a.L = 1; a.Me = a.Mbp;
                 a.eps_mode = host ? 1 : 0;
                 a.domain = domain;
@@ -1560,13 +1573,50 @@ int vaeb_reconstruct_sampled(vaeb_ctx* c, const float* x, int64_t n, int32_t n_s
                 if (int rc = enqueue_forward(c, a, pr)) return rc;
             }
             const float scale = (sidx == n_samples - 1) ? (float)n_samples : 0.f;
-            hipLaunchKernelGGL(recon_accum_kernel, dim3((unsigned)std::min<int64_t>(1024, cdiv(ny, 256))), dim3(256), 0,
-                               c->s, c->yacc, c->y, ny, sidx == 0 ? 1 : 0, scale);
+            const dim3 grid((unsigned)std::min<int64_t>(1024, cdiv(ny, 256)));
+            hipLaunchKernelGGL(recon_accum_kernel, grid, dim3(256), 0, c->s, c->yacc, c->y, ny, sidx == 0 ? 1 : 0, scale);
             CHECK_LAUNCH();
+            if (out_lv) {
+                hipLaunchKernelGGL(recon_accum_kernel, grid, dim3(256), 0, c->s, lacc, c->dA6, ny, sidx == 0 ? 1 : 0, scale);
+                CHECK_LAUNCH();
+            }
         }
         HIP_TRY(hipMemcpyAsync(out_y + r0 * g.D, c->yacc, sizeof(float) * (size_t)ny, hipMemcpyDeviceToHost, c->s));
+        if (out_lv)
+            HIP_TRY(hipMemcpyAsync(out_lv + r0 * g.D, lacc, sizeof(float) * (size_t)ny, hipMemcpyDeviceToHost, c->s));
         HIP_TRY(hipStreamSynchronize(c->s));
     }
+    return 0;
+}
+
+// The decoder from a given z (freyFace.py:173-187 `image(z)`, compiled at :237-245; VAEB.py
+// :253-265): hd = tanh(z W1 + b1), mu = sigmoid(hd W2 + b2), and for the Gaussian decoder the
+// log-sigma head hd W6 + b6 (out_lv).  fp32 contexts; z is [n x Z] row-major.
+int vaeb_decode(vaeb_ctx* c, const float* z, int64_t n, float* out_mu, float* out_lv) {
+    if (!c || !z || n <= 0 || !out_mu) return fail(VAEB_ERR_ARG, "bad arguments");
+    if (out_lv && !gaussian(c)) return fail(VAEB_ERR_ARG, "the log-sigma head exists for the Gaussian decoder only");
+    if (is_bf16(c)) return fail(VAEB_ERR_ARG, "vaeb_decode is served by fp32 contexts");
+    const vaeb_config& g = c->c;
+    const int chunk = g.max_eval_rows;
+    int epar = c->par;
+    if (int rc = eval_arena(c, &epar)) return rc;
+    for (int64_t r0 = 0; r0 < n; r0 += chunk) {
+        const int rows = (int)std::min<int64_t>(chunk, n - r0);
+        StepArgs a = make_args(c, epar, rows, MODE_RECON, c->xeval, false);
+        a.L = 1; a.Me = a.Mbp;
+        // z rows, pad rows zero (PDecHid writes hd = 0 there)
+        HIP_TRY(hipMemsetAsync(c->z, 0, sizeof(float) * (size_t)a.Mbp * g.Z, c->s));
+        HIP_TRY(hipMemcpyAsync(c->z, z + r0 * g.Z, sizeof(float) * (size_t)rows * g.Z, hipMemcpyHostToDevice, c->s));
+        launch_tile<1, 4, 1, 1, 8>(c->s, PDecHid{a, a.Me, a.H, a.Z});
+        CHECK_LAUNCH();
+        if (gaussian(c)) launch_bigk<2>(c->s, PDecOut{a, nullptr, a.Me, a.D, a.H});
+        else launch_bigk<1>(c->s, PDecOut{a, nullptr, a.Me, a.D, a.H});
+        CHECK_LAUNCH();
+        HIP_TRY(hipMemcpyAsync(out_mu + r0 * g.D, c->y, sizeof(float) * (size_t)rows * g.D, hipMemcpyDeviceToHost, c->s));
+        if (out_lv)
+            HIP_TRY(hipMemcpyAsync(out_lv + r0 * g.D, c->dA6, sizeof(float) * (size_t)rows * g.D, hipMemcpyDeviceToHost, c->s));
+    }
+    HIP_TRY(hipStreamSynchronize(c->s));
     return 0;
 }
 
@@ -1585,7 +1635,10 @@ int vaeb_comm_init(vaeb_ctx* c, const uint8_t id_bytes[128], int32_t rank, int32
         return fail(VAEB_ERR_ARG, "the full-variational paths are single-rank");
     if (c->comm) return fail(VAEB_ERR_STATE, "communicator already initialised");
     HIP_TRY(hipSetDevice(c->c.device));
-    c->dp_overlap = is_bf16(c);
+    // bucket A's all-reduce + Adagrad on a second stream beside the backward: at world > 1,
+    // where the all-reduce has a cost to hide, and on the bf16 engine also at world 1 (its
+    // 34 MB bucket-A Adagrad pays for the fork alone: 933 vs ~940 us per step)
+    c->dp_overlap = is_bf16(c) || world > 1;
     if (const char* ov = getenv("VAEB_DP_OVERLAP")) c->dp_overlap = atoi(ov) != 0;
     if (!c->s2) {
         HIP_TRY(hipStreamCreateWithFlags(&c->s2, hipStreamNonBlocking));
@@ -1610,6 +1663,9 @@ int vaeb_get_activation(vaeb_ctx* c, const char* name, float* out, int64_t n) {
     if (!c || !name || !out) return fail(VAEB_ERR_ARG, "null argument");
     float* ptrs[] = {c->h, c->mu, c->lv, c->eps, c->z, c->hd, c->dA2, c->dA6, c->dA1, c->dZ, c->dMuLv, c->dA3, c->y,
                      c->kl_part, c->lp_part};
+    if (strcmp(name, "dZ") == 0 && fused_latent(c) && c->fold_bwd && !is_bf16(c) && ho_dz(c) == 1)
+        return fail(VAEB_ERR_STATE, "dZ is not stored by the atomic latent hand-off (fan-in <= 16, latent_bwd.hpp): "
+                                    "create the context with VAEB_ATOMIC_HO=0 to read it");
     for (auto& a : kActs)
         if (strcmp(a.name, name) == 0) {
             if (!ptrs[a.which]) return fail(VAEB_ERR_STATE, "activation %s not allocated", name);
@@ -1787,6 +1843,49 @@ int vaeb_bench_gemm_bf16(vaeb_ctx* c, int32_t ako, int32_t bko, int32_t M, int32
     if (e1) hipEventDestroy(e1);
     for (void* p : {(void*)a, (void*)b, (void*)o, (void*)bias}) if (p) hipFree(p);
     return rc;
+}
+
+int vaeb_time_update_many(vaeb_ctx* c, const int32_t* idx, int32_t n, float* out_gpu_ms, double* out_enqueue_ms) {
+    if (!c || !out_gpu_ms) return fail(VAEB_ERR_ARG, "null argument");
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    HIP_TRY(hipEventCreate(&e0));
+    HIP_TRY(hipEventCreate(&e1));
+    HIP_TRY(hipStreamSynchronize(c->s));
+    HIP_TRY(hipEventRecord(e0, c->s));
+    const auto t0 = std::chrono::steady_clock::now();
+    int rc = vaeb_update_many(c, idx, n);
+    const auto t1 = std::chrono::steady_clock::now();
+    if (rc == 0) {
+        hipEventRecord(e1, c->s);
+        hipEventSynchronize(e1);
+        hipEventElapsedTime(out_gpu_ms, e0, e1);
+        if (out_enqueue_ms) *out_enqueue_ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
+    }
+    hipEventDestroy(e0);
+    hipEventDestroy(e1);
+    return rc;
+}
+
+int vaeb_graph_status(vaeb_ctx* c, int32_t* mode, char* msg, int32_t cap) {
+    if (!c || !mode) return fail(VAEB_ERR_ARG, "null argument");
+    if (!c->c.use_graph) *mode = VAEB_GRAPH_OFF;
+    else if (c->graph_failed) *mode = VAEB_GRAPH_EAGER_FALLBACK;
+    else *mode = c->g1[0] ? VAEB_GRAPH_REPLAY : VAEB_GRAPH_NOT_CAPTURED;
+    if (msg && cap > 0) snprintf(msg, (size_t)cap, "%s", c->graph_failed ? c->graph_err.c_str() : "");
+    return 0;
+}
+
+int vaeb_comm_info(vaeb_ctx* c, int32_t* rccl_version, int32_t* dp_overlap, int32_t* world) {
+    if (!c) return fail(VAEB_ERR_ARG, "null ctx");
+    if (rccl_version) {
+        int v = 0;
+        ncclResult_t r = ncclGetVersion(&v);
+        if (r != ncclSuccess) return fail(VAEB_ERR_COMM, "ncclGetVersion: %s", ncclGetErrorString(r));
+        *rccl_version = v;
+    }
+    if (dp_overlap) *dp_overlap = c->comm ? (c->dp_overlap ? 1 : 0) : -1;
+    if (world) *world = c->comm ? c->world : 1;
+    return 0;
 }
 
 int vaeb_kernel_name(int32_t id, char* out, int32_t cap) {

@@ -249,19 +249,41 @@ class VAEB:
         v = self._ctx.validate_resident()
         return v / self._nvalid if self.objective == "mean_map" else v
 
-    def reconstruct(self, x, n_samples=0):
-        """VAEB.reconstruct (VAEB.py:267-300): the decoder mean at z = mu for n_samples <= 0,
-        else the decoder output averaged over n_samples posterior draws.  The continuous
-        decoder returns the (averaged) decoder mean: the reference's closing
-        multivariate_normal draw over a [rows x D] mean cannot run."""
+    def reconstruct(self, x, n_samples=0, mean=False):
+        """VAEB.reconstruct (VAEB.py:267-300): the decoder output at z = mu for n_samples <= 0,
+        else averaged over n_samples posterior draws z = mu + exp(lv / 2) eps (:271-291).
+        The Bernoulli decoder returns those means.  The continuous decoder, as the reference,
+        returns one draw N(y_mu, exp(y_log_sigma)^2 I) from numpy's global generator
+        (:293-297; drawn per pixel as y_mu + exp(y_log_sigma) * np.random.standard_normal,
+        the same distribution as the reference's multivariate_normal with a diagonal
+        covariance, not the same stream).  mean=True (extension) returns y_mu instead.
+        A 1-D x (one row, as reconstruction.py:32 passes) gives a 1-D result."""
         x = np.asarray(x, np.float32)
-        if n_samples <= 0:
-            return self._ctx.reconstruct(x)
-        if self._stream is not None:
+        one = x.ndim == 1
+        x = np.atleast_2d(x)
+        if n_samples > 0 and self._stream is not None:
             # one srng.normal draw per sample (VAEB.py:280), rows stacked sample-major
             self._ctx.push_eps(np.concatenate([self._stream.draw(x.shape[0], self.n_latent)
                                                for _ in range(n_samples)], axis=1))
-        return self._ctx.reconstruct_sampled(x, n_samples)
+        y, ls = self._ctx.reconstruct_full(x, max(int(n_samples), 0), log_sigma=self.continuous and not mean)
+        if ls is not None:
+            y = (y.astype(np.float64) + np.exp(ls.astype(np.float64)) * np.random.standard_normal(y.shape))
+        return y[0] if one else y
+
+    def decoder(self, z):
+        """VAEB.decoder (VAEB.py:253-265) evaluated at given latents z [n x Z]: (mu,
+        log_sigma) for the continuous decoder, y for the Bernoulli one."""
+        mu, ls = self._ctx.decode(np.asarray(z, np.float32))
+        return (mu, ls) if self.continuous else mu
+
+    def freyFace(self, z):
+        """The compiled `freyFace` function of freyFace.py (:173-187, 237-245): the decoder at
+        z -- [mu, log_sigma] (continuous) or y (Bernoulli), float64 like the reference's
+        dmatrix output."""
+        out = self.decoder(z)
+        if self.continuous:
+            return [out[0].astype(np.float64), out[1].astype(np.float64)]
+        return out.astype(np.float64)
 
     # ------------------------------------------------------------------ checkpoints
     def save(self, file_name):
@@ -295,14 +317,17 @@ class VAEB:
     @staticmethod
     def load(file_name, data=None, **kw):
         """VAEB.load (VAEB.py:206-242): rebuild the model from a checkpoint and load the
-        dataset (freyfaces.pkl / mnist.pkl.gz) unless `data` = (x_train, x_valid) is given."""
+        dataset as the reference does -- (x_train, x_valid) from freyfaces.pkl, or
+        mnist.pkl.gz's ((x, y) train, valid, test) -- unless `data` is given (either form)."""
         print('Loading model form : {0}'.format(file_name))
         hdr, params = pickle_static.read_mdl(file_name)
         continuous = bool(hdr["continuous"])
         if data is None:
             from .cli import load_dataset
-            data = load_dataset(continuous)
-        x_train = data[0]
+            data = load_dataset(continuous, splits=3 if not continuous else 2)
+        # the reference returns (x_train, x_valid) for Frey and mnist.pkl.gz's three
+        # (images, labels) pairs for MNIST (VAEB.py:229-239)
+        x_train = data[0] if np.ndim(data[0]) == 2 and not isinstance(data[0], tuple) else data[0][0]
         model = VAEB(x_train, continuous, int(hdr["n_hidden_units"]), int(hdr["n_latent"]), int(hdr["batch_size"]),
                      int(hdr["L"]), float(hdr["learning_rate"]), bool(hdr.get("genericEstimator", False)), False,
                      params, **kw)
