@@ -337,11 +337,25 @@ def graph_check(ctx, dist, world):
     return [mode for mode, _ in allst]
 
 
-def timed_run(ctx, order, warmup, steps, dist, world=1):
+def timed_run(ctx, order, warmup, steps, dist, world=1, sync=False, warm_ms=0.0):
     """W untimed steps, then exactly K steps between barrier + stream sync; max over ranks.
-    Returns (seconds, the graph mode of each rank after the warmup)."""
+    sync: the K steps as K synchronous update(index) calls (the reference's loop) instead of
+    one update_many.  Returns (seconds, the graph mode of each rank after the warmup)."""
     warm_order, timed_order = order(warmup), order(steps)   # host work done before the GPU runs
-    ctx.update_many(warm_order)
+    if warm_ms > 0:
+        # graph capture first (host-bound: the first call of a context), then the device warm-up
+        # kernel, then the W warmup steps proper (the first of which is that captured call)
+        if not sync:
+            ctx.update_many(warm_order[:1])
+            ctx.synchronize()
+            ctx.epoch_elbo()
+            warm_order = warm_order[1:]
+        ctx.busy(int(warm_ms * 1000))
+    if sync:
+        for b in warm_order:
+            ctx.update(int(b))
+    else:
+        ctx.update_many(warm_order)
     ctx.synchronize()
     ctx.epoch_elbo()
     modes = graph_check(ctx, dist, world)
@@ -349,7 +363,11 @@ def timed_run(ctx, order, warmup, steps, dist, world=1):
         dist.barrier()
     ctx.synchronize()
     t0 = time.perf_counter()
-    ctx.update_many(timed_order)
+    if sync:
+        for b in timed_order.tolist():
+            ctx.update(b)
+    else:
+        ctx.update_many(timed_order)
     ctx.synchronize()
     t1 = time.perf_counter()
     if dist:
@@ -387,6 +405,14 @@ def main(argv=None):
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-strong", action="store_true", help="N > 1, weak scaling: skip the strong-scaling leg")
     ap.add_argument("--cpu-budget", type=float, default=10.0)
+    ap.add_argument("--device-warm-ms", type=float, default=30.0,
+                    help="before the W warmup steps, keep every CU busy this long (no model state is "
+                         "touched): the context's first call captures its graphs on the host (~10 ms, GPU "
+                         "idle), and a 20-step timed region right after runs partly below boost clock "
+                         "(DESIGN.md 6; 0 disables)")
+    ap.add_argument("--sync", action="store_true",
+                    help="time the reference's per-step synchronous form: K calls of update(index), each "
+                         "returning its SGVB/B (VAEB.py:577-579), instead of one K-step update_many")
     ap.add_argument("--scaling", choices=["weak", "strong"], default="weak",
                     help="weak: B rows per GPU (default); strong: one B-row global minibatch split "
                          "contiguously over the ranks (100 over 8 = 13,13,13,13,12,12,12,12; SURVEY 8(e))")
@@ -449,7 +475,8 @@ def main(argv=None):
             return np.array(out[:n], np.int32)
         return order
 
-    el, graph_modes = timed_run(ctx, orders(N // Bg), warmup, steps, dist, world)
+    el, graph_modes = timed_run(ctx, orders(N // Bg), warmup, steps, dist, world, sync=args.sync,
+                                warm_ms=args.device_warm_ms)
     elbo_sum, nsteps = ctx.epoch_elbo()
     comm = comm_record(ctx, dist, world)
 
@@ -489,6 +516,8 @@ def main(argv=None):
         "config": {"workload": C["workload"], "global_batch": Bg, "batch_per_gpu": B, "seq_len": None,
                    "parallelism": f"dp{world}"},
         "elbo": elbo_sum / max(nsteps, 1),
+        "mode": "sync update(index) per step" if args.sync else "update_many (one call, graph replay)",
+        "device_warm_ms": args.device_warm_ms,   # untimed busy kernel before the W warmup steps
         "graph": graph_modes,              # per rank: how the timed steps ran (vaeb_graph_status)
         "comm": comm,                      # per rank: RCCL version, overlap, algorithm / protocol
         "step_tflops": sflops / (el / steps) / 1e12,
@@ -506,7 +535,7 @@ def main(argv=None):
         ctx2.set_data(x)
         ctx2.set_params(theta0)
         ctx2.set_eps_mode(0, seed=10)
-        el2, _ = timed_run(ctx2, orders(N // Bgs), warmup, steps, dist, world)
+        el2, _ = timed_run(ctx2, orders(N // Bgs), warmup, steps, dist, world, warm_ms=args.device_warm_ms)
         ctx2.close()
         res["strong"] = {"value": Bgs * steps / el2, "ms_per_step": el2 / steps * 1e3, "global_batch": Bgs,
                          "rows_per_gpu": [row_split(Bn, world, r, "strong")[0] for r in range(world)]}

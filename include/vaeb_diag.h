@@ -34,6 +34,8 @@ int vaeb_graph_status(vaeb_ctx* ctx, int32_t* mode, char* msg, int32_t cap);
  * the call itself took to enqueue (graph launches, the order upload). */
 int vaeb_time_update_many(vaeb_ctx* ctx, const int32_t* batch_indices, int32_t n, float* out_gpu_ms,
                           double* out_enqueue_ms);
+/* Diagnostics: every CU busy (MFMA loop) for `us` microseconds on the context's stream. */
+int vaeb_busy(vaeb_ctx* ctx, int32_t us);
 /* Data-parallel configuration: the RCCL version (ncclGetVersion), whether bucket A's
  * all-reduce + Adagrad overlap the backward on a second stream (-1: no communicator), and
  * the communicator's world size (1 without one). */

@@ -25,9 +25,15 @@ def fresh():
     return ctx
 
 
-# driver form: fresh context, warmup 5 (captures), then 20
-for trial in range(3):
+# driver form: fresh context, warmup 5 (captures), then 20; "busy" variants first keep
+# every CU busy for that many ms (is the extra the clock ramp after the host-bound capture?)
+for trial in range(6):
+    busy_ms = [0, 5, 30][trial % 3]
     ctx = fresh()
+    if busy_ms:
+        ctx.update_many(rng.integers(0, 500, 1).astype(np.int32))   # capture first (host-bound, GPU idle)
+        ctx.synchronize()
+        ctx.busy(busy_ms * 1000)
     t0 = time.perf_counter()
     ctx.update_many(rng.integers(0, 500, 5).astype(np.int32))
     ctx.synchronize()
@@ -38,7 +44,7 @@ for trial in range(3):
     t = time.perf_counter() - t0
     g2, h2 = ctx.time_update_many(rng.integers(0, 500, 20).astype(np.int32))
     g3, h3 = ctx.time_update_many(rng.integers(0, 500, 1000).astype(np.int32))
-    print(f"driver form {trial}: warmup call {tw * 1e3:.1f} ms; 20 steps wall {t * 1e6:.0f} us, gpu {g * 1e3:.0f} us, "
+    print(f"driver form {trial} (busy {busy_ms} ms): warmup call {tw * 1e3:.1f} ms; 20 steps wall {t * 1e6:.0f} us, gpu {g * 1e3:.0f} us, "
           f"enqueue {h * 1e3:.0f} us | again gpu {g2 * 1e3:.0f} us (enq {h2 * 1e3:.0f}) | 1000: {g3:.2f} ms "
           f"= {g3:.4f} us/step x1000 (enq {h3:.2f} ms)", flush=True)
     ctx.close()

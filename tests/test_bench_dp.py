@@ -59,6 +59,13 @@ class FakeCtx:
     def profile_steps(self, n):
         return [("p1_enc_latent", 0.012), ("p4_decout_z", 0.010)]
 
+    def busy(self, us):
+        assert us > 0
+
+    def update(self, index):
+        self.n += 1
+        return -100.0
+
     def graph_status(self):
         if os.environ.get("FAKE_GRAPH_FAIL_RANK") == os.environ.get("RANK"):
             return "eager_fallback", "hipStreamEndCapture: operation not permitted when stream is capturing"

@@ -39,7 +39,7 @@ EXPORTS = [
     "vaeb_ae_train_many", "vaeb_ae_reconstruct", "vaeb_ae_encode", "vaeb_ae_decode",
 ]
 DIAG_EXPORTS = ["vaeb_profile_steps", "vaeb_kernel_name", "vaeb_debug_timeline", "vaeb_test_gemm_bf16",
-                "vaeb_bench_gemm_bf16", "vaeb_graph_status", "vaeb_comm_info", "vaeb_time_update_many"]
+                "vaeb_bench_gemm_bf16", "vaeb_graph_status", "vaeb_comm_info", "vaeb_time_update_many", "vaeb_busy"]
 GRAPH_MODES = {0: "off", 1: "not_captured", 2: "replay", 3: "eager_fallback"}
 AE_MAX_LAYERS = 8
 AE_BINARY, AE_CONT = 0, 1
@@ -131,6 +131,7 @@ def load():
         "vaeb_kernel_name": ([ctypes.c_int32, ctypes.c_char_p, ctypes.c_int32], ctypes.c_int),
         "vaeb_graph_status": ([_P, ctypes.POINTER(ctypes.c_int32), ctypes.c_char_p, ctypes.c_int32], ctypes.c_int),
         "vaeb_comm_info": ([_P] + [ctypes.POINTER(ctypes.c_int32)] * 3, ctypes.c_int),
+        "vaeb_busy": ([_P, ctypes.c_int32], ctypes.c_int),
         "vaeb_time_update_many": ([_P, ctypes.POINTER(ctypes.c_int32), ctypes.c_int32, _F,
                                    ctypes.POINTER(ctypes.c_double)], ctypes.c_int),
         "vaeb_debug_timeline": ([_P, ctypes.c_int32, ctypes.POINTER(ctypes.c_uint64), _I64,
@@ -354,6 +355,10 @@ class Context:
         check(self.lib.vaeb_time_update_many(self.h, idx.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), idx.size,
                                              ctypes.byref(g), ctypes.byref(h)))
         return g.value, h.value
+
+    def busy(self, us):
+        """Diagnostics: every CU busy for `us` microseconds on the context's stream."""
+        check(self.lib.vaeb_busy(self.h, int(us)))
 
     def graph_status(self):
         """(mode, message): 'off' | 'not_captured' | 'replay' | 'eager_fallback' (message: why)."""

@@ -105,6 +105,17 @@ DEV void elbo_reduce(const ElboArgs& e, double* sh) {
     elbo_emit(e, r[0], r[1], r[2]);
 }
 
+// The step's [SGVB / B, flags] into the context's mapped host slot (vaeb_hip.hip
+// vaeb_update) as ONE 8-byte store, so the host that polls the flags word (2 = written,
+// | 1 = the sticky status is set) reads the value of the same store.
+DEV void elbo_store(const ElboArgs& e, float v) {
+    const unsigned long long st = reinterpret_cast<const unsigned long long*>(e.epoch)[kBlkStatus];
+    const unsigned long long w =
+        (unsigned long long)__builtin_bit_cast(uint32_t, v) | ((unsigned long long)(st ? 3u : 2u) << 32);
+    __hip_atomic_store(reinterpret_cast<unsigned long long*>(e.elbo_out), w, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 // The step's scalar outputs from the reduced sums (thread 0 of the reducing workgroup).
 DEV void elbo_emit(const ElboArgs& e, double lp, double kl, double fv) {
     // LB: sum logp / L + sum KL (VAEB.py:339-344); LA: (sum logp + sum(prior-logQ)) / L
@@ -126,7 +137,7 @@ DEV void elbo_emit(const ElboArgs& e, double lp, double kl, double fv) {
         *e.dp_slot = (float)sg;
     } else if (e.elbo_out) {
         const double v = sg * e.inv_bglob;
-        *e.elbo_out = (float)v;
+        elbo_store(e, (float)v);
         e.epoch[0] += v;
         e.epoch[1] += 1.0;
     }
@@ -153,6 +164,19 @@ __global__ __launch_bounds__(256) void set_order_kernel(int* ictl, OrderArg u) {
 __global__ __launch_bounds__(64) void delay_kernel(uint64_t ticks) {
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(8);
+}
+
+// Diagnostics: every CU busy with MFMA work for `us` microseconds (s_memrealtime at 100 MHz),
+// result kept live through a store that never happens (a < 0 never holds).
+__global__ __launch_bounds__(256) void busy_kernel(uint64_t ticks, float* sink) {
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    float a = (float)(threadIdx.x & 7) * 1e-3f, b = 1e-3f;
+    while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) {
+#pragma unroll
+        for (int i = 0; i < 32; ++i) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc, 0, 0, 0);
+    }
+    if (acc[0] < -1.f) sink[threadIdx.x] = acc[1];
 }
 
 // Posterior-sample reconstruction (VAEB.py:277-291): acc = acc + y in sample order
@@ -561,10 +585,10 @@ __global__ __launch_bounds__(256) void adagrad_kernel(OptArgs o, int64_t P, DpRa
     }
     if (r.book && blockIdx.x == 0 && threadIdx.x == 0) {
         const double v = (double)o.grad[P] * e.inv_bglob;
-        *e.elbo_out = (float)v;
+        elbo_store(e, (float)v);
         e.epoch[0] += v;
         e.epoch[1] += 1.0;
-        advance_cursor(e.cursor);
+        if (e.cursor) advance_cursor(e.cursor);
         *e.step += 1;
     }
 }

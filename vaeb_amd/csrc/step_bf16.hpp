@@ -577,10 +577,10 @@ __global__ __launch_bounds__(256) void adagrad_bf16_kernel(Opt o, int64_t P, DpR
     }
     if (r.book && blockIdx.x == 0 && threadIdx.x == 0) {
         const double v = (double)o.grad[P] * e.inv_bglob;
-        *e.elbo_out = (float)v;
+        elbo_store(e, (float)v);
         e.epoch[0] += v;
         e.epoch[1] += 1.0;
-        advance_cursor(e.cursor);
+        if (e.cursor) advance_cursor(e.cursor);
         *e.step += 1;
     }
 }

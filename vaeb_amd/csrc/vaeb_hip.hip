@@ -136,6 +136,7 @@ struct vaeb_ctx {
     int* h_ctl = nullptr;
     float* h_elbo = nullptr;
     double* h_d2 = nullptr;
+    float* h_out = nullptr;       // mapped host [SGVB / B, flags] every training step's last kernel writes
     hipEvent_t ctl_ev = nullptr;
     // graphs
     hipGraphExec_t g1[2] = {nullptr, nullptr};
@@ -357,7 +358,7 @@ void launch_enc_latent(hipStream_t s, dim3 g1, const StepArgs& a, const FvFold& 
 // Training minibatches with Z <= 32 fold the latent block into the wide phases
 // (latent.hpp); validation / reconstruction chunks keep the per-row-block kernels.
 bool folded_latent(const vaeb_ctx* c, const StepArgs& a) {
-    return fused_latent(c) && a.order != nullptr && a.Mbp <= r16(c->c.B);
+    return fused_latent(c) && a.domain == 0 && a.Mbp <= r16(c->c.B);   // training rows (domain 0)
 }
 
 // Forward phases P1..P4 for any mode.
@@ -623,8 +624,10 @@ int dp_bucket_b(vaeb_ctx* c, Prof& pr, int opt_mark, Opt opt) {
 // `prof` brackets every launch with timing events.
 // fresh: first step of an enqueued sequence (VAEB_EST_FVS in Philox mode draws the weight
 // sample here; later steps of the sequence read the one their predecessor's update wrote).
-int enqueue_train_step(vaeb_ctx* c, int par, bool prof, bool fresh = true) {
-    if (is_bf16(c)) return bf_train_step(c, par, prof);
+// direct >= 0: the step's minibatch index given by the host (vaeb_update's single eager
+// step): the rows are addressed from the launch arguments, no order upload, no cursor.
+int enqueue_train_step(vaeb_ctx* c, int par, bool prof, bool fresh = true, int direct = -1) {
+    if (is_bf16(c)) return bf_train_step(c, par, prof, direct);
     Prof pr{c, prof};
     if (prof) pr.reps = c->prof_reps;
     const vaeb_config& g = c->c;
@@ -641,6 +644,14 @@ int enqueue_train_step(vaeb_ctx* c, int par, bool prof, bool fresh = true) {
     }
     if (fvs) par ^= 1;
     StepArgs a = make_args(c, par, g.B, g.estimator == VAEB_EST_FV ? MODE_EVAL : MODE_TRAIN, c->data, true);
+    if (direct >= 0) {
+        const int64_t row0 = (int64_t)direct * g.B_global + g.row_offset;
+        a.order = nullptr;
+        a.xbase = c->data + row0 * g.D;
+        a.batch_stride = 0;
+        a.row_base_mul = 0;
+        a.row_base_add = row0;
+    }
     // literal FV: the (mu, sigma) update needs none of the step's data; with the folded
     // latent block it rides enc_latent_kernel's extra grid rows (~256 blocks), else it is
     // fv_kernel's launch
@@ -654,7 +665,7 @@ int enqueue_train_step(vaeb_ctx* c, int par, bool prof, bool fresh = true) {
     }
     if (int rc = enqueue_forward(c, a, pr, fvf)) return rc;
     ElboArgs e = base_elbo(c, a);
-    e.elbo_out = c->elbo_out; e.epoch = c->epoch; e.cursor = c->ictl; e.step = c->step;
+    e.elbo_out = c->elbo_out; e.epoch = c->epoch; e.cursor = direct >= 0 ? nullptr : c->ictl; e.step = c->step;
 
     if (g.estimator == VAEB_EST_FV) {
         if (!fv_fold) {
@@ -830,8 +841,8 @@ int capture(vaeb_ctx* c, int nsteps, int par, hipGraphExec_t* out) {
     return 0;
 }
 
-int step_eager(vaeb_ctx* c) {
-    if (int rc = enqueue_train_step(c, c->par, false)) return rc;
+int step_eager(vaeb_ctx* c, int direct = -1) {
+    if (int rc = enqueue_train_step(c, c->par, false, true, direct)) return rc;
     if (flips(c)) c->par ^= 1;
     return 0;
 }
@@ -1036,6 +1047,18 @@ int vaeb_create(const vaeb_config* cfg, vaeb_ctx** out) {
         vaeb_destroy(c);
         return fail(VAEB_ERR_NOMEM, "hipHostMalloc failed");
     }
+    {
+        // the step's scalar result written by the GPU straight into mapped, coherent host
+        // memory: vaeb_update reads it with no device -> host copy (and no stream sync)
+        void* dp = nullptr;
+        if (hipHostMalloc((void**)&c->h_out, sizeof(float) * 4, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+            hipHostGetDevicePointer(&dp, c->h_out, 0) != hipSuccess) {
+            vaeb_destroy(c);
+            return fail(VAEB_ERR_NOMEM, "mapped host ELBO slot");
+        }
+        memset(c->h_out, 0, sizeof(float) * 4);
+        c->elbo_out = static_cast<float*>(dp);
+    }
     hipEventCreateWithFlags(&c->ctl_ev, hipEventDisableTiming);
     hipEventRecord(c->ctl_ev, c->s);
     for (auto& ev : c->pev) hipEventCreate(&ev);
@@ -1065,6 +1088,7 @@ int vaeb_destroy(vaeb_ctx* c) {
     if (c->eval_acc) hipFree(c->eval_acc);
     if (c->h_ctl) hipHostFree(c->h_ctl);
     if (c->h_elbo) hipHostFree(c->h_elbo);
+    if (c->h_out) hipHostFree(c->h_out);
     if (c->h_d2) hipHostFree(c->h_d2);
     if (c->ctl_ev) hipEventDestroy(c->ctl_ev);
     for (auto& ev : c->pev) if (ev) hipEventDestroy(ev);
@@ -1203,6 +1227,23 @@ static int host_eps_ready(vaeb_ctx* c, int64_t rows) {
     return 0;
 }
 
+// Wait until the step's last kernel has written [SGVB / B, flags] into the mapped host slot
+// (kernels_aux.hpp elbo_store: flags = 2 | status), polling the slot; the stream is queried
+// now and then so that a failed or already-finished stream ends the wait.
+static int wait_step_result(vaeb_ctx* c) {
+    volatile uint32_t* flag = reinterpret_cast<volatile uint32_t*>(&c->h_out[1]);
+    for (uint64_t spin = 0; *flag == 0u; ++spin) {
+        if ((spin & 255) == 255) {
+            const hipError_t q = hipStreamQuery(c->s);
+            if (q == hipSuccess) break;
+            if (q != hipErrorNotReady) return fail(VAEB_ERR_HIP, "step failed: %s", hipGetErrorString(q));
+        }
+        __builtin_ia32_pause();
+    }
+    if (*flag == 0u) return fail(VAEB_ERR_STATE, "internal: the step wrote no result");
+    return 0;
+}
+
 // The sticky step status read at a sync point (kernels_aux.hpp elbo_emit): cleared, and
 // reported as VAEB_ERR_NUMERIC.
 static int take_status(vaeb_ctx* c, uint64_t st) {
@@ -1217,13 +1258,16 @@ int vaeb_update(vaeb_ctx* c, int32_t batch_index, float* out) {
     if (!c) return fail(VAEB_ERR_ARG, "null ctx");
     if (int rc = check_batches(c, &batch_index, 1)) return rc;
     if (int rc = host_eps_ready(c, c->c.B)) return rc;
-    if (int rc = upload_order(c, &batch_index, 1)) return rc;
-    if (int rc = run_steps(c, 1)) return rc;
-    // [status, SGVB / B] in one copy (kernels_aux.hpp kBlk*)
-    HIP_TRY(hipMemcpyAsync(c->h_elbo, c->blk + kBlkStatus, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, c->s));
-    HIP_TRY(hipStreamSynchronize(c->s));
-    if (out) *out = c->h_elbo[2];
-    return take_status(c, reinterpret_cast<const uint64_t*>(c->h_elbo)[0]);
+    // The reference calls update() once per minibatch and waits for its value (VAEB.py:
+    // 577-579).  That call is ONE eager step whose minibatch index rides the launch
+    // arguments (no order upload, no graph launch), and its value is read from the mapped
+    // host slot the step's last kernel writes: 65 -> ~55 us per call (scripts/call_ab.py).
+    volatile uint32_t* flag = reinterpret_cast<volatile uint32_t*>(&c->h_out[1]);
+    *flag = 0u;
+    if (int rc = step_eager(c, batch_index)) return rc;
+    if (int rc = wait_step_result(c)) return rc;
+    if (out) *out = c->h_out[0];
+    return take_status(c, *flag & 1u);
 }
 
 int vaeb_update_many(vaeb_ctx* c, const int32_t* idx, int32_t n) {
@@ -1233,7 +1277,15 @@ int vaeb_update_many(vaeb_ctx* c, const int32_t* idx, int32_t n) {
     // host eps holds ONE step's noise: a multi-step call would train every step on it
     if (c->eps_mode == VAEB_EPS_HOST && n > 1)
         return fail(VAEB_ERR_STATE, "host eps mode: one step per call (push eps before each vaeb_update)");
-    for (int32_t done = 0; done < n;) {
+    int32_t done = 0;
+    if (n >= 2 && c->c.use_graph && c->g1[0] && !c->graph_failed && flips(c)) {
+        // the call's first step goes out eagerly with its minibatch index in the launch
+        // arguments: the GPU starts it while the host still submits the order upload and the
+        // graph of the remaining steps (which would otherwise lead every call)
+        if (int rc = step_eager(c, idx[0])) return rc;
+        done = 1;
+    }
+    while (done < n) {
         const int32_t m = std::min<int32_t>(n - done, kOrderCap);
         if (int rc = upload_order(c, idx + done, m)) return rc;
         if (int rc = run_steps(c, m)) return rc;
@@ -1864,6 +1916,13 @@ int vaeb_time_update_many(vaeb_ctx* c, const int32_t* idx, int32_t n, float* out
     hipEventDestroy(e0);
     hipEventDestroy(e1);
     return rc;
+}
+
+int vaeb_busy(vaeb_ctx* c, int32_t us) {
+    if (!c || us <= 0) return fail(VAEB_ERR_ARG, "bad arguments");
+    hipLaunchKernelGGL(busy_kernel, dim3(2048), dim3(256), 0, c->s, (uint64_t)us * 100, c->fv_part);
+    CHECK_LAUNCH();
+    return 0;
 }
 
 int vaeb_graph_status(vaeb_ctx* c, int32_t* mode, char* msg, int32_t cap) {
