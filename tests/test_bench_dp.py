@@ -72,7 +72,7 @@ class FakeCtx:
         return "replay", ""
 
     def comm_info(self):
-        return {"rccl_version": 22700, "dp_overlap": self.world > 1, "world": self.world}
+        return {"rccl_version": 22700, "dp_overlap": False, "world": self.world}
 
     def close(self):
         pass
@@ -117,7 +117,7 @@ def test_bench_two_ranks_weak_and_strong():
     line = json.loads(res[0][1].strip().splitlines()[-1])
     assert line["n_gpus"] == 2 and line["scaling"] == "weak" and line["config"]["global_batch"] == 200
     assert line["graph"] == ["replay", "replay"]
-    assert [c["dp_overlap"] for c in line["comm"]] == [True, True] and line["comm"][1]["algo"] == "auto"
+    assert [c["dp_overlap"] for c in line["comm"]] == [False, False] and line["comm"][1]["algo"] == "auto"
     assert line["strong"]["rows_per_gpu"] == [50, 50] and line["strong"]["global_batch"] == 100
     assert line["value"] == pytest.approx(200 * 40 / (line["ms_per_step"] * 40 / 1e3), rel=1e-6)
     assert res[1][1].strip() == ""   # only rank 0 prints

@@ -51,11 +51,11 @@ def test_vaeb_class_theano_rng_mode_is_reproducible():
 @pytest.mark.parametrize("continuous,use_graph,overlap", [(False, True, "1"), (True, True, "1"), (False, False, "1"),
                                                          (False, True, "0"), (True, True, "0")])
 def test_dp_path_world1_matches_fused_path(continuous, use_graph, overlap, monkeypatch):
-    """The data-parallel path (gradients stored; with VAEB_DP_OVERLAP=1 -- the default at
-    world > 1 -- bucket A = W2 [| W6] all-reduced and updated on the second stream while the
-    backward continues, bucket B + SGVB after it; with 0 -- the fp32 default at world 1 --
-    one all-reduce and one optimizer launch) at world size 1 against the fused-optimizer
-    path: Bernoulli / Gaussian decoder, graph-replayed and eager."""
+    """The data-parallel path (gradients stored; with VAEB_DP_OVERLAP=1 -- the bf16 engine's
+    default -- bucket A = W2 [| W6] all-reduced and updated on the second stream while the
+    backward continues, bucket B + SGVB after it; with 0 -- the fp32 default -- one
+    all-reduce and one optimizer launch) at world size 1 against the fused-optimizer path:
+    Bernoulli / Gaussian decoder, graph-replayed and eager."""
     from vaeb_amd import _lib
     monkeypatch.setenv("VAEB_DP_OVERLAP", overlap)
     cfg = O.Config(D=560, H=200, Z=2, continuous=True) if continuous else O.Config(D=784, H=500, Z=20)

@@ -1687,10 +1687,15 @@ int vaeb_comm_init(vaeb_ctx* c, const uint8_t id_bytes[128], int32_t rank, int32
         return fail(VAEB_ERR_ARG, "the full-variational paths are single-rank");
     if (c->comm) return fail(VAEB_ERR_STATE, "communicator already initialised");
     HIP_TRY(hipSetDevice(c->c.device));
-    // bucket A's all-reduce + Adagrad on a second stream beside the backward: at world > 1,
-    // where the all-reduce has a cost to hide, and on the bf16 engine also at world 1 (its
-    // 34 MB bucket-A Adagrad pays for the fork alone: 933 vs ~940 us per step)
-    c->dp_overlap = is_bf16(c) || world > 1;
+    // Bucket A's all-reduce + Adagrad on a second stream beside the backward, where the
+    // window it can hide behind is longer than what the fork costs.  The graph's fork and
+    // join cost ~19 us per step whatever the world size (fp32 MNIST at world 1: 66.0 vs
+    // 47.1 us, profiles/r3/dp_world1_start.txt), and on the fp32 engine the backward left
+    // after dW2 (| dW6) is the one last launch, ~10 us: at most 10 us of all-reduce could
+    // hide there at ANY world size, so the fp32 step never forks.  On the bf16 engine
+    // (config 5) the window is ~500 us and bucket A (34 MB) alone is worth the fork at
+    // world 1 already (933 vs ~940 us per step), so it always forks.
+    c->dp_overlap = is_bf16(c);
     if (const char* ov = getenv("VAEB_DP_OVERLAP")) c->dp_overlap = atoi(ov) != 0;
     if (!c->s2) {
         HIP_TRY(hipStreamCreateWithFlags(&c->s2, hipStreamNonBlocking));
