@@ -534,12 +534,12 @@ __global__ __launch_bounds__(512, 4) void decout_z_kernel(StepArgs a) {
 #pragma unroll
     for (int w = 0; w < NB; ++w) acc[w] = zero4();
     // W1^T rows kb + 4 li + (0..3) at latent 4t + q; b1 at kb + 16 q + 4 r + (0..3); W2 rows
-    // kb + 16 q + 4 r + u.  ZM 0 / 1: the first block's loads are issued BEFORE the z
-    // prologue (whose own loads -- z, or mu / lv / eps -- they do not depend on), so both
-    // round trips overlap (MNIST ZM 0 decout 10.5 -> 10.2 us); a block past H reads zeros.
-    // ZM 2 keeps them in the loop: beside its 16 slab float4s in flight they pushed the
-    // kernel past 128 VGPRs (spills at 4 blocks / CU; at 2 blocks / CU 87 of MNIST's 343
-    // workgroups waited for a second round: 12.7 -> 15.7 us).
+    // kb + 16 q + 4 r + u.  The first block's loads are issued BEFORE the z prologue (whose
+    // own loads -- z, mu / lv / eps, or the encoder's slabs -- they do not depend on), so
+    // both round trips overlap (MNIST ZM 0 decout 10.5 -> 10.2 us); a block past H reads
+    // zeros.  ZM 2 spreads its slab sum over all 512 threads (at most kSlabPer loads each)
+    // so that the hoisted block still fits 128 VGPRs (round 2's 16 slab float4s per thread
+    // beside it spilled).
     f32x4 w1v[ZS], b1v[4];
     float w2b[4][4][NB];
     auto load_block = [&](int kb) {
@@ -560,7 +560,7 @@ __global__ __launch_bounds__(512, 4) void decout_z_kernel(StepArgs a) {
                     w2b[u][r][w] = p.b1(n0 + li, k, w);
                 }
     };
-    if constexpr (ZM != 2) load_block(64 * wave);
+    load_block(64 * wave);
     float zb[ZS];
     if constexpr (!AT) {
         const rsrc_t bz = mkbuf(a.z, (int64_t)a.Me * Z * 4);
@@ -572,6 +572,7 @@ __global__ __launch_bounds__(512, 4) void decout_z_kernel(StepArgs a) {
         __shared__ float zs[16][33];
         __shared__ float gs[16][33];
         __shared__ float msum[ZM == 2 ? 64 : 1][17];   // ZM 2: summed [mu | lv] slab, [column][row]
+        __shared__ f32x4 spart[ZM == 2 ? 512 : 1];      // ZM 2: per-partition slab sums
         const int per = 16 * Z;
         const int l = m0 / a.Mbp;                 // a 16-row block never straddles two planes
         const int i0 = m0 - l * a.Mbp;
@@ -591,24 +592,35 @@ __global__ __launch_bounds__(512, 4) void decout_z_kernel(StepArgs a) {
             grow0p = (a.order ? (int64_t)ld_launch_const(a.cursor + kCtlNext) * a.row_base_mul : 0) + a.row_base_add;
         }
         if constexpr (ZM == 2) {
-            // thread (c, mq) sums float4 (column c, rows 4 mq .. 4 mq + 3) of the row block's
-            // nct slabs, contributor order, 16 loads per round trip
+            // float4 f (column f >> 2, rows 4 (f & 3) .. + 3) of the row block's nct slabs:
+            // partition part = t / nf4 of the 512 threads sums slabs part, part + np, ... in
+            // order (at most kSlabPer loads in flight per thread), then thread f adds the np
+            // partition sums in order -- a fixed order, so the result is deterministic
+            constexpr int kSlabPer = 6;
             const int nct = (H + 31) >> 5, nf4 = 8 * Z;
+            const int np = 512 / nf4;   // nf4 <= 256 (Z <= 32): np >= 2
             const rsrc_t bsl = mkbuf(a.slab_ml, (int64_t)(a.Mbp >> 4) * nct * nf4 * 16);
-            if ((int)threadIdx.x < nf4) {
-                const int64_t first = (int64_t)(i0 >> 4) * nct * nf4 + threadIdx.x;
-                f32x4 sum = zero4();
-                for (int c0 = 0; c0 < nct; c0 += 16) {
-                    f32x4 v[16];
+            const int f = (int)threadIdx.x % nf4, part = (int)threadIdx.x / nf4;
+            const int64_t first = (int64_t)(i0 >> 4) * nct * nf4 + f;
+            f32x4 sum = zero4();
+            for (int c0 = part; c0 < nct; c0 += kSlabPer * np) {
+                f32x4 v[kSlabPer];
 #pragma unroll
-                    for (int u = 0; u < 16; ++u)
-                        v[u] = bld4(bsl, c0 + u < nct ? (uint32_t)((first + (int64_t)(c0 + u) * nf4) * 16) : kOOB);
-#pragma unroll
-                    for (int u = 0; u < 16; ++u) sum += v[u];
+                for (int u = 0; u < kSlabPer; ++u) {
+                    const int ct = c0 + u * np;
+                    v[u] = bld4(bsl, (part < np && ct < nct) ? (uint32_t)((first + (int64_t)ct * nf4) * 16) : kOOB);
                 }
+#pragma unroll
+                for (int u = 0; u < kSlabPer; ++u) sum += v[u];
+            }
+            spart[threadIdx.x] = sum;
+            __syncthreads();
+            if ((int)threadIdx.x < nf4) {
+                f32x4 t = spart[threadIdx.x];
+                for (int pp = 1; pp < np; ++pp) t += spart[pp * nf4 + threadIdx.x];
                 const int c = threadIdx.x >> 2, mq = threadIdx.x & 3;
 #pragma unroll
-                for (int k = 0; k < 4; ++k) msum[c][4 * mq + k] = sum[k];
+                for (int k = 0; k < 4; ++k) msum[c][4 * mq + k] = t[k];
             }
             __syncthreads();
         }
@@ -665,7 +677,7 @@ __global__ __launch_bounds__(512, 4) void decout_z_kernel(StepArgs a) {
         }
     }
     for (int kb = 64 * wave; kb < H; kb += 64 * 8) {
-        if (ZM == 2 || kb != 64 * wave) load_block(kb);
+        if (kb != 64 * wave) load_block(kb);
         if (kb == 0) {   // wave 0, first block: its loads are in flight
             p.x = x_rows(a);
             pre = p.prefetch(m0, n0);
