@@ -56,6 +56,29 @@ def test_gemm_layouts(gctx, ako, bko, M, N, K, ks):
     assert np.all(np.abs(C - ref) <= bound), float(np.max(np.abs(C - ref) / bound))
 
 
+GEMM8_SHAPES = [(256, 256, 512, 1), (296, 520, 328, 1), (512, 512, 4096, 2), (200, 136, 64, 1), (8, 520, 4096, 4),
+                (768, 256, 1000, 3)]
+
+
+@pytest.mark.parametrize("ako,bko", [(0, 0), (0, 1), (1, 0), (1, 1)])
+@pytest.mark.parametrize("M,N,K,ks", GEMM8_SHAPES)
+def test_gemm8_layouts(gctx, ako, bko, M, N, K, ks):
+    """The 256 x 256 8-phase main loop (gemm8_kernel: BK = 64, two K-tile buffers, one
+    half-tile staged per phase, staggered wave groups) on every operand layout, partial
+    tiles, K tails (K % 64 != 0), one-K-tile slices and split-K, same bound as above."""
+    rng = np.random.default_rng(3 * M + 5 * N + K + ks + 10 * ako + 20 * bko)
+    A = rng.standard_normal((M, K)).astype(np.float32)
+    B = rng.standard_normal((K, N)).astype(np.float32)
+    As = A.T.copy() if ako else A
+    Bs = B if bko else B.T.copy()
+    C = gctx.test_gemm_bf16(As, Bs, ako, bko, M, N, K, -ks)
+    Aq = O.bf16_round(A).astype(np.float64)
+    Bq = O.bf16_round(B).astype(np.float64)
+    ref = Aq @ Bq
+    bound = 1e-5 * (np.abs(Aq) @ np.abs(Bq)) + 1e-30
+    assert np.all(np.abs(C - ref) <= bound), float(np.max(np.abs(C - ref) / bound))
+
+
 CASES = [
     ("bern_LB", dict(D=256, H=128, Z=32), 256),
     ("bern_LB_tails", dict(D=200, H=136, Z=24), 200),
@@ -280,3 +303,29 @@ def test_bf16_forked_and_single_stream_steps_agree(monkeypatch):
     f, u = out["1", True], out["0", True]
     assert abs(f[0] - u[0]) <= 1e-6 * abs(u[0])
     assert np.abs(f[1] - u[1]).max() <= 1e-6 and np.abs(f[2] - u[2]).max() <= 1e-6 * max(1.0, np.abs(u[2]).max())
+
+
+def test_bf16_gemm8_step_matches_ring_step(monkeypatch):
+    """The step with its 256 x 256 launches on the 8-phase loop (VAEB_BF_GEMM8=1; the forked
+    dW2 | dW6 and dW3 use them at any size) against the BK = 32 ring: both accumulate every
+    output over K in the same 32-wide order, so 6 Philox steps agree to 1e-6."""
+    from vaeb_amd import _lib
+    cfg = O.Config(D=512, H=256, Z=32)
+    B = 512
+    x = (np.random.default_rng(5).random((6 * B, cfg.D)) < 0.4).astype(np.float32)
+    order = np.array([3, 1, 4, 1, 5, 0], np.int32)
+    out = {}
+    for g8 in ("0", "1"):
+        monkeypatch.setenv("VAEB_BF_GEMM8", g8)
+        ctx = _lib.Context(cfg.D, cfg.H, cfg.Z, B, max_eval_rows=B, dtype=_lib.DTYPE_BF16)
+        ctx.set_data(x)
+        ctx.set_params(O.flatten(O.init_params(cfg)))
+        ctx.set_eps_mode(_lib.EPS_PHILOX, 10)
+        ctx.set_step(0)
+        ctx.update_many(order)
+        s_, n_ = ctx.epoch_elbo()
+        out[g8] = (s_ / n_, ctx.get_params())
+        ctx.close()
+    monkeypatch.setenv("VAEB_BF_GEMM8", "0")
+    assert abs(out["0"][0] - out["1"][0]) <= 1e-6 * abs(out["0"][0])
+    assert np.abs(out["0"][1] - out["1"][1]).max() <= 1e-6

@@ -361,9 +361,20 @@ __global__ __launch_bounds__(NTHR, 2 * Shape<BNT>::kBlocksPerCU) void gemm2_kern
 
 // ------------------------------------------------------------------ helpers
 // Lane l's element (i, j, r) of a wave block at (mw, nw): row mw + 16i + 4(l>>4) + r,
-// column nw + 16j + (l&15).
+// column nw + CM::off(j) + (l&15).  The column map CM says where the wave's four 16-column
+// fragment tiles sit: ColStd -- 64 contiguous columns (gemm_body); Col8 -- two 32-column
+// pieces 128 apart (gemm8_body: a wave's column quadrants of the 256-wide tile).  slot(nw):
+// the per-row partial slot of the wave block (EpiDecOut), one per 64 columns of a tile.
+struct ColStd {
+    static constexpr int off(int j) { return 16 * j; }
+    DEV static int slot(int nw) { return nw >> 6; }
+};
+struct Col8 {
+    static constexpr int off(int j) { return 16 * (j & 1) + 128 * (j >> 1); }
+    DEV static int slot(int nw) { return ((nw >> 8) << 2) + ((nw & 255) >> 5); }
+};
 DEV int erow(int mw, int i, int r, int lane) { return mw + 16 * i + 4 * (lane >> 4) + r; }
-DEV int ecol(int nw, int j, int lane) { return nw + 16 * j + (lane & 15); }
+template <class CM = ColStd> DEV int ecol(int nw, int j, int lane) { return nw + CM::off(j) + (lane & 15); }
 
 // Column sums of the wave's 64 x 64 block (each lane: its column of tile j), reduced
 // over the 4 lane groups that share a column.  Lanes 0..15 hold the result for tile j.
@@ -435,7 +446,7 @@ DEV void tile_store(const char* t, bf16_t* dst, int ld, int r0, int c0, int rlim
 struct EpiF32 {
     static constexpr bool kIn = false, kOut = false;
     float* out; int ldo; int M, N; int64_t slab;
-    template <int W>
+    template <int W, class CM = ColStd>
     DEV void apply(int mw, int nw, f32x4 (&acc)[4][4], int kz, char*) const {
         const int lane = threadIdx.x & 63;
         float* o = out + (int64_t)kz * slab;
@@ -445,7 +456,7 @@ struct EpiF32 {
             for (int j = 0; j < 4; ++j)
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
-                    const int row = erow(mw, i, r, lane), col = ecol(nw, j, lane);
+                    const int row = erow(mw, i, r, lane), col = ecol<CM>(nw, j, lane);
                     if (row < M && col < N) o[(int64_t)row * ldo + col] = acc[i][j][r];
                 }
     }
@@ -456,13 +467,13 @@ struct EpiBiasAct {
     static constexpr bool kIn = false, kOut = true;
     const float* bias; int tanh_act; int M, N;
     bf16_t* out; int ldo;
-    template <int W>
+    template <int W, class CM = ColStd>
     DEV void apply(int mw, int nw, f32x4 (&acc)[4][4], int, char* smem) const {
         const int lane = threadIdx.x & 63;
         const int lr0 = mw & (BM - 1), lc0 = nw & (W - 1);
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            const int col = ecol(nw, j, lane);
+            const int col = ecol<CM>(nw, j, lane);
             const float b = col < N ? bias[col] : 0.f;
 #pragma unroll
             for (int i = 0; i < 4; ++i)
@@ -470,7 +481,7 @@ struct EpiBiasAct {
                 for (int r = 0; r < 4; ++r) {
                     float v = acc[i][j][r] + b;
                     if (tanh_act) v = ftanh(v);
-                    lds_st_bf<W>(smem, erow(lr0, i, r, lane), ecol(lc0, j, lane), v);
+                    lds_st_bf<W>(smem, erow(lr0, i, r, lane), ecol<CM>(lc0, j, lane), v);
                 }
         }
     }
@@ -491,19 +502,19 @@ struct EpiDTanh {
     DEV void load_in(int m0, int n0, char* smem) const {
         tile_load<W, W>(smem, mkbuf(t, (int64_t)M * ldt * 2), ldt, m0, n0, M, N, 0);
     }
-    template <int W>
+    template <int W, class CM = ColStd>
     DEV void apply(int mw, int nw, f32x4 (&acc)[4][4], int, char* smem) const {
         const int lane = threadIdx.x & 63;
         const int lr0 = mw & (BM - 1), lc0 = nw & (W - 1);
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            const int col = ecol(nw, j, lane);
+            const int col = ecol<CM>(nw, j, lane);
             float cs = 0.f;
 #pragma unroll
             for (int i = 0; i < 4; ++i)
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
-                    const int lr = erow(lr0, i, r, lane), lc = ecol(lc0, j, lane);
+                    const int lr = erow(lr0, i, r, lane), lc = ecol<CM>(lc0, j, lane);
                     const float tv = lds_bf<W>(smem, lr, lc);
                     const float v = acc[i][j][r] * (1.f - tv * tv);
                     lds_st_bf<W>(smem, lr, lc, v);
@@ -546,8 +557,9 @@ struct EpiDecOut {
         if constexpr (GAUSS) tile_load<W / 2, W, true>(smem, src, ldx, m0, n0 / 2, M, D, Mx);
         else tile_load<W, W>(smem, src, ldx, m0, n0, M, D, Mx);
     }
-    template <int W>
+    template <int W, class CM = ColStd>
     DEV void apply(int mw, int nw, f32x4 (&acc)[4][4], int, char* smem) const {
+        static_assert(!GAUSS || CM::off(2) == 32, "the Gaussian interleave pairs tiles j and j + 2, 32 columns apart");
         const int lane = threadIdx.x & 63;
         const int lr0 = mw & (BM - 1), lc0 = nw & (W - 1);
         // fragment row i outermost: only its 4 row partials and the JN column partials stay
@@ -558,7 +570,7 @@ struct EpiDecOut {
         float bb2[JN], bb6[JN], cs2[JN], cs6[JN];
 #pragma unroll
         for (int j = 0; j < JN; ++j) {
-            col[j] = ecol(nw, j, lane);                                   // dA column
+            col[j] = ecol<CM>(nw, j, lane);                               // dA column
             d[j] = GAUSS ? (nw >> 1) + 16 * j + (lane & 15) : col[j];     // data column
             cok[j] = d[j] < D;
             bb2[j] = cok[j] ? b2[d[j]] : 0.f;
@@ -576,7 +588,7 @@ struct EpiDecOut {
                 for (int r = 0; r < 4; ++r) {
                     const int row = erow(mw, i, r, lane), lr = erow(lr0, i, r, lane);
                     const bool ok = cok[j] && row < M;
-                    const float xv = lds_bf<W>(smem, lr, ecol(lc0, j, lane));
+                    const float xv = lds_bf<W>(smem, lr, ecol<CM>(lc0, j, lane));
                     const float a2 = acc[i][j][r] + bb2[j];
                     float y, lpv, g2, g6 = 0.f;
                     if constexpr (!GAUSS) {
@@ -599,10 +611,10 @@ struct EpiDecOut {
                     rs[r] += ok ? lpv : 0.f;
                     if (yout && ok) yout[(int64_t)row * D + d[j]] = y;
                     if (train) {
-                        lds_st_bf<W>(smem, lr, ecol(lc0, j, lane), g2);
+                        lds_st_bf<W>(smem, lr, ecol<CM>(lc0, j, lane), g2);
                         cs2[j] += ok ? g2 : 0.f;
                         if constexpr (GAUSS) {
-                            lds_st_bf<W>(smem, lr, ecol(lc0, j, lane) + 32, g6);
+                            lds_st_bf<W>(smem, lr, ecol<CM>(lc0, j, lane) + 32, g6);
                             cs6[j] += ok ? g6 : 0.f;
                         }
                     }
@@ -613,7 +625,7 @@ struct EpiDecOut {
                     if constexpr (!GAUSS) rs[r] -= flog(pd[r]);
                     const float sr = sum16(rs[r]);
                     const int row = erow(mw, i, r, lane);
-                    if ((lane & 15) == 0 && row < M) lp[(int64_t)row * nlp + (nw >> 6)] = sr;
+                    if ((lane & 15) == 0 && row < M) lp[(int64_t)row * nlp + CM::slot(nw)] = sr;
                 }
             }
         }
@@ -680,7 +692,7 @@ struct EpiAdagrad {
     // the fragment row are issued before its stores (buffer loads, masked elements read
     // out of range), instead of a load -> store chain per element that hipcc cannot
     // reorder (theta_in / accum may alias the stores, as far as it can tell).
-    template <int W>
+    template <int W, class CM = ColStd>
     DEV void apply(int mw, int nw, f32x4 (&acc)[4][4], int, char*) const {
         const int lane = threadIdx.x & 63;
         const rsrc_t bth = mkbuf(opt.th_in, opt.n * 4), bac = mkbuf(opt.accum, opt.n * 4);
@@ -693,7 +705,7 @@ struct EpiAdagrad {
             for (int j = 0; j < 4; ++j)
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
-                    const int row = erow(mw, i, r, lane), col = ecol(nw, j, lane);
+                    const int row = erow(mw, i, r, lane), col = ecol<CM>(nw, j, lane);
                     off[j][r] = (row < M && col < N) ? (uint32_t)map.at(row, col) * 4u : kOOB;
                     th[j][r] = bld(bth, opt.update ? off[j][r] : kOOB);
                     ac[j][r] = bld(bac, opt.update ? off[j][r] : kOOB);
@@ -702,7 +714,7 @@ struct EpiAdagrad {
             for (int j = 0; j < 4; ++j)
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
-                    const int row = erow(mw, i, r, lane), col = ecol(nw, j, lane);
+                    const int row = erow(mw, i, r, lane), col = ecol<CM>(nw, j, lane);
                     const float dsg = acc[i][j][r];
                     if (opt.store_grad) bst(bgr, off[j][r], dsg);
                     if (opt.update) {
@@ -718,6 +730,178 @@ struct EpiAdagrad {
         }
     }
 };
+
+// ------------------------------------------------------------------ 256^2 8-phase main loop
+// The guide's 256 x 256, BK = 64 schedule (cdna_hip_programming.md §5 "The 256² 8-phase
+// template"), written for this engine's operand layouts and epilogues.
+//  * LDS: two K-tile buffers of 64 KiB; a buffer holds A then B, each as four 8-KiB blocks
+//    (k-sub s = 0, 1: k 0..31 / 32..63) x (half h = 0, 1: rows / columns 0..127 / 128..255)
+//    at (2 s + h) 8 KiB, every block the 128-row BK = 32 image of TileDma / frag (KC rows
+//    of 64 B, KO k-rows of 256 B, swizzled as gemm_body's), so the LDS-DMA and fragment code
+//    is shared.  A half-tile = one operand's half = 2 blocks = 2 LDS-DMA per thread.
+//  * waves: (wr, wc) = (wave >> 2, wave & 3).  Phase p of a K-tile computes the C quadrant
+//    (ah, bh) = (0,0), (0,1), (1,1), (1,0) of the 256 x 256 tile: wave (wr, wc) owns rows
+//    ah 128 + wr 64 .. + 64 and columns bh 128 + wc 32 .. + 32 of it, 4 x 2 fragment tiles x
+//    2 k-steps = 16 MFMAs.  Fragment reads per phase: 8 A + 4 B (phase 0), 4 B (phase 1),
+//    8 A (phase 2), none (phase 3 reuses phase 0's B).
+//  * staging: one half-tile per phase, K-tile t's phases stage B_hi(t+1), A_hi(t+1),
+//    A_lo(t+2), B_lo(t+2).  Each half is restaged >= 2 phases after its last fragment read
+//    (WAR rule under the staggered groups) and read >= 5 phases after its DMA was issued;
+//    every phase waits vmcnt(8) (4 half-tiles in flight) before its first barrier, which
+//    retires the half the NEXT phase reads (RAW: wait in phase p, read in p + 1 or later).
+//    K-tiles past the slice stage out-of-range (zero) DMAs, so the count never changes.
+//  * waves 4..7 run one barrier behind waves 0..3 (ping-pong: one group reads fragments
+//    while the other's MFMAs run on the same SIMD); s_setprio(1) around the MFMA cluster.
+//  * epilogue: the functors of gemm_body with the column map Col8 (a wave's fragment
+//    tiles j = 0, 1 at columns wc 32 + 16 j, j = 2, 3 at 128 + wc 32 + 16 (j - 2)).
+DEV void vm_wait8() { asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); }
+
+template <int LA, int LB, class Epi>
+DEV void gemm8_body(const GemmArgs& g, const Epi& e, int bid, int kz, char* smem) {
+    constexpr int BK8 = 64, kBlock = 8192, kOperand = 4 * kBlock, kBuf = 2 * kOperand;
+    int tm, tn;
+    tile_of(g, bid, tm, tn);
+    const int m0 = tm * BM, n0 = tn * 256;
+    const int kbeg = kz * g.kslice;
+    const int kend = min(g.K, kbeg + g.kslice);
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int wr = wave >> 2, wc = wave & 3;
+    const v4i da = mkdesc(g.A + g.ab.offset(), g.a_bytes), db = mkdesc(g.B, g.b_bytes);
+    const TileDma<LA, 128> la[2] = {{da, g.lda, g.M, kend, m0}, {da, g.lda, g.M, kend, m0 + 128}};
+    const TileDma<LB, 128> lb[2] = {{db, g.ldb, g.N, kend, n0}, {db, g.ldb, g.N, kend, n0 + 128}};
+    // half-tile h of operand op (0 = A, 1 = B) of K-tile t
+    auto stage = [&](int op, int h, int t) {
+        char* img = smem + (t & 1) * kBuf + op * kOperand + h * kBlock;
+        const int k0 = kbeg + t * BK8;
+        if (op == 0) {
+            la[h].issue(img, k0, wave, lane);
+            la[h].issue(img + 2 * kBlock, k0 + 32, wave, lane);
+        } else {
+            lb[h].issue(img, k0, wave, lane);
+            lb[h].issue(img + 2 * kBlock, k0 + 32, wave, lane);
+        }
+    };
+    f32x4 acc[2][2][4][2];
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j) acc[a][b][i][j] = zero4();
+    bf16x8 af[4][2], bf0[2][2], bf1[2][2];
+    auto read_a = [&](const char* buf, int h) {
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) af[i][kk] = frag<LA, 128>(buf + (2 * kk + h) * kBlock, wr * 64 + 16 * i, 0, lane);
+    };
+    auto read_b = [&](const char* buf, int h, bf16x8 (&bf)[2][2]) {
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+                bf[j][kk] = frag<LB, 128>(buf + kOperand + (2 * kk + h) * kBlock, wc * 32 + 16 * j, 0, lane);
+    };
+    auto mma = [&](f32x4 (&c)[4][2], const bf16x8 (&bf)[2][2]) {
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j)
+                    c[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][kk], bf[j][kk], c[i][j], 0, 0, 0);
+        __builtin_amdgcn_s_setprio(0);
+    };
+    // first barrier of a phase (after its reads, its stage and the counted wait), the
+    // fragment reads retired, the MFMA cluster, the second barrier
+    auto bar = [&]() {
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    const int nkt = (kend - kbeg + BK8 - 1) / BK8;
+    // prologue: K-tile 0 whole, then A_lo(1), B_lo(1); A_lo(0), B_lo(0) certified
+    stage(0, 0, 0);
+    stage(1, 0, 0);
+    stage(1, 1, 0);
+    stage(0, 1, 0);
+    stage(0, 0, 1);
+    stage(1, 0, 1);
+    vm_wait8();
+    bar();
+    if (wr == 1) bar();
+    for (int t = 0; t < nkt; ++t) {
+        const char* buf = smem + (t & 1) * kBuf;
+        // phase 0: quadrant (0, 0); stage B_hi(t + 1)
+        read_a(buf, 0);
+        read_b(buf, 0, bf0);
+        stage(1, 1, t + 1);
+        vm_wait8();
+        bar();
+        mma(acc[0][0], bf0);
+        bar();
+        // phase 1: quadrant (0, 1); stage A_hi(t + 1)
+        read_b(buf, 1, bf1);
+        stage(0, 1, t + 1);
+        vm_wait8();
+        bar();
+        mma(acc[0][1], bf1);
+        bar();
+        // phase 2: quadrant (1, 1); stage A_lo(t + 2)
+        read_a(buf, 1);
+        stage(0, 0, t + 2);
+        vm_wait8();
+        bar();
+        mma(acc[1][1], bf1);
+        bar();
+        // phase 3: quadrant (1, 0) (A_hi and B_lo from registers); stage B_lo(t + 2)
+        stage(1, 0, t + 2);
+        vm_wait8();
+        bar();
+        mma(acc[1][0], bf0);
+        bar();
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the out-of-range tail DMAs
+    if (wr == 0) __builtin_amdgcn_s_barrier();          // re-align the groups' barrier counts
+    __syncthreads();
+    if constexpr (Epi::kIn) {
+        e.template load_in<256>(m0, n0, smem);
+        __syncthreads();
+    }
+#pragma unroll
+    for (int ah = 0; ah < 2; ++ah) {
+        f32x4 blk[4][4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) blk[i][j] = acc[ah][j >> 1][i][j & 1];
+        e.template apply<256, Col8>(m0 + ah * 128 + wr * 64, n0 + wc * 32, blk, kz, smem);
+    }
+    if constexpr (Epi::kOut) {
+        __syncthreads();
+        e.template store_out<256>(m0, n0, smem);
+    }
+}
+
+template <int LA, int LB, class Epi>
+__global__ __launch_bounds__(NTHR, 2) void gemm8_kernel(GemmArgs g, Epi e) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    gemm8_body<LA, LB, Epi>(g, e, blockIdx.x, blockIdx.y, smem);
+}
+// Two products in one grid on the 8-phase loop (gemm2_kernel's dhd ∥ dW2 grid)
+template <int LA1, int LB1, class E1, int LA2, int LB2, class E2>
+__global__ __launch_bounds__(NTHR, 2) void gemm8x2_kernel(GemmArgs g1, E1 e1, GemmArgs g2, E2 e2, int nb1) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int b = blockIdx.x;
+    if (b < nb1) gemm8_body<LA1, LB1, E1>(g1, e1, b, 0, smem);
+    else gemm8_body<LA2, LB2, E2>(g2, e2, b - nb1, 0, smem);
+}
+// dynamic LDS of gemm8_kernel: the two K-tile buffers, or the 256-wide epilogue tile
+constexpr int lds8_bytes() { return (2 * 65536 > BM * epitch<256>()) ? 2 * 65536 : BM * epitch<256>(); }
 
 }  // namespace bf
 }  // namespace vaeb

@@ -971,6 +971,10 @@ int vaeb_create(const vaeb_config* cfg, vaeb_ctx** out) {
     if (const char* bk = getenv("VAEB_BF_FORK")) c->bf_fork = atoi(bk) != 0;
     if (const char* ah = getenv("VAEB_ATOMIC_HO")) c->atomic_ho = atoi(ah) != 0 ? 1 : 0;
     if (const char* er = getenv("VAEB_ENC_RED")) c->enc_red = atoi(er) != 0 ? 1 : 0;
+    {
+        const char* g8 = getenv("VAEB_BF_GEMM8");
+        g_gemm8 = g8 ? atoi(g8) != 0 : false;
+    }
     if (e != hipSuccess) { delete c; return fail(VAEB_ERR_HIP, "stream/event create: %s", hipGetErrorString(e)); }
     const int64_t D = g.D, H = g.H, Z = g.Z;
     std::vector<int64_t> sz = {D * H, H * Z, H * Z, Z * H, H * D};
@@ -1794,6 +1798,9 @@ int vaeb_debug_timeline(vaeb_ctx* c, int32_t batch_index, uint64_t* out, int64_t
 
 int vaeb_test_gemm_bf16(vaeb_ctx* c, int32_t ako, int32_t bko, int32_t M, int32_t N, int32_t K, const float* A,
                         const float* B, float* C, int32_t ksplit) {
+    // ksplit < 0: the 256 x 256 8-phase main loop (gemm8_kernel) with -ksplit slices
+    const bool force8 = ksplit < 0;
+    if (force8) ksplit = -ksplit;
     if (!c || !A || !B || !C || M <= 0 || N <= 0 || K <= 0 || ksplit <= 0) return fail(VAEB_ERR_ARG, "bad arguments");
     if (K % 8 || (ako && M % 8) || (bko && N % 8))
         return fail(VAEB_ERR_ARG, "bf16 GEMM: K (and a K-outer operand's rows) must be multiples of 8");
@@ -1815,7 +1822,13 @@ int vaeb_test_gemm_bf16(vaeb_ctx* c, int32_t ako, int32_t bko, int32_t M, int32_
         const bf::EpiF32 e{fc, N, M, N, (int64_t)M * N};
         const int lda = ako ? M : K, ldb = bko ? N : K;
         const int64_t ab = (int64_t)na * 2, bbytes = (int64_t)nb * 2;
-        if (!ako && !bko) rc = bf_gemm<bf::KC, bf::KC>(c->s, ba, lda, ab, bb, ldb, bbytes, M, N, K, ksplit, e);
+        if (force8) {
+            bf::GemmArgs g = bf_args256(ba, lda, ab, bb, ldb, bbytes, M, N, K, ksplit);
+            if (!ako && !bko) rc = bf_launch8<bf::KC, bf::KC>(c->s, g, nz, e);
+            else if (!ako && bko) rc = bf_launch8<bf::KC, bf::KO>(c->s, g, nz, e);
+            else if (ako && !bko) rc = bf_launch8<bf::KO, bf::KC>(c->s, g, nz, e);
+            else rc = bf_launch8<bf::KO, bf::KO>(c->s, g, nz, e);
+        } else if (!ako && !bko) rc = bf_gemm<bf::KC, bf::KC>(c->s, ba, lda, ab, bb, ldb, bbytes, M, N, K, ksplit, e);
         else if (!ako && bko) rc = bf_gemm<bf::KC, bf::KO>(c->s, ba, lda, ab, bb, ldb, bbytes, M, N, K, ksplit, e);
         else if (ako && !bko) rc = bf_gemm<bf::KO, bf::KC>(c->s, ba, lda, ab, bb, ldb, bbytes, M, N, K, ksplit, e);
         else rc = bf_gemm<bf::KO, bf::KO>(c->s, ba, lda, ab, bb, ldb, bbytes, M, N, K, ksplit, e);
@@ -1855,6 +1868,10 @@ static int bench_gemm_launch(hipStream_t s, const bf16_t* A, const bf16_t* B, in
     g.M = M; g.N = N; g.K = K;
     g.tiles_m = cdiv(M, bf::BM); g.tiles_n = cdiv(N, bn);
     g.kslice = ((K + bf::BK - 1) / bf::BK) * bf::BK;
+    if (bn == 8) {
+        g.tiles_n = cdiv(N, 256);
+        return bf_launch8<LA, LB>(s, g, 1, e);
+    }
     if (bn == 256) return bf_launch<LA, LB, 256>(s, g, 1, e);
     return bf_launch<LA, LB, 128>(s, g, 1, e);
 }
@@ -1865,7 +1882,8 @@ int vaeb_bench_gemm_bf16(vaeb_ctx* c, int32_t ako, int32_t bko, int32_t M, int32
     if (!c || !out_ms || M <= 0 || N <= 0 || K <= 0 || reps <= 0) return fail(VAEB_ERR_ARG, "bad arguments");
     if (K % 8 || M % 8 || N % 8) return fail(VAEB_ERR_ARG, "bench gemm: M, N, K must be multiples of 8");
     if (bn == 0) bn = bf_bn(M, N);
-    if (bn != 128 && bn != 256) return fail(VAEB_ERR_ARG, "bench gemm: tile width 128 or 256");
+    if (bn != 128 && bn != 256 && bn != 8)
+        return fail(VAEB_ERR_ARG, "bench gemm: tile width 128 or 256 (8: 256 x 256 on the 8-phase loop)");
     bf16_t *a = nullptr, *b = nullptr, *o = nullptr;
     float* bias = nullptr;
     int rc = 0;
