@@ -316,7 +316,7 @@ def test_bf16_gemm8_step_matches_ring_step(monkeypatch):
     order = np.array([3, 1, 4, 1, 5, 0], np.int32)
     out = {}
     for g8 in ("0", "1"):
-        monkeypatch.setenv("VAEB_BF_GEMM8", g8)
+        monkeypatch.setenv("VAEB_BF_GEMM8", "15" if g8 == "1" else "0")
         ctx = _lib.Context(cfg.D, cfg.H, cfg.Z, B, max_eval_rows=B, dtype=_lib.DTYPE_BF16)
         ctx.set_data(x)
         ctx.set_params(O.flatten(O.init_params(cfg)))

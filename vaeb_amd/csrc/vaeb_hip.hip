@@ -973,7 +973,10 @@ int vaeb_create(const vaeb_config* cfg, vaeb_ctx** out) {
     if (const char* er = getenv("VAEB_ENC_RED")) c->enc_red = atoi(er) != 0 ? 1 : 0;
     {
         const char* g8 = getenv("VAEB_BF_GEMM8");
-        g_gemm8 = g8 ? atoi(g8) != 0 : false;
+        // default: the 8-phase loop for KC x KC (dhd) and KC x KO (enc, dechid); KO x KO (the
+        // forked dW2 | dW6 and dW3) keeps the ring: config 5 step 833 -> 816 us with this mask,
+        // 845 with all three, 858 with KO x KO added to enc (profiles/r3/gemm8_step_ab.txt)
+        g_gemm8 = g8 ? (int)strtol(g8, nullptr, 0) : 3;
     }
     if (e != hipSuccess) { delete c; return fail(VAEB_ERR_HIP, "stream/event create: %s", hipGetErrorString(e)); }
     const int64_t D = g.D, H = g.H, Z = g.Z;
