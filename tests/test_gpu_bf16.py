@@ -245,11 +245,16 @@ def test_bf16_full_size_row_linearity_and_determinism():
     assert s_again == s_full and np.array_equal(g_again, g_full) and np.array_equal(p_again, p_full)
 
 
-def test_bf16_dp_path_world1_matches_fused_optimizer():
+@pytest.mark.parametrize("overlap,fork", [("1", "1"), ("0", "1"), ("1", "0")])
+def test_bf16_dp_path_world1_matches_fused_optimizer(overlap, fork, monkeypatch):
     """The data-parallel path of the bf16 engine (gradients stored, RCCL all-reduce of
     [grads | SGVB], replicated Adagrad + shadow rewrite in adagrad_bf16_kernel) at world
-    size 1 against the fused-optimizer path, over 6 graph-replayed steps."""
+    size 1 against the fused-optimizer path, over 6 graph-replayed steps: forked (the
+    default: dW1, dW2 | dW6, dW45 on the second stream, bucket A reduced and updated there
+    right after dW2 -- or, without overlap, everything reduced after the join) and unforked."""
     from vaeb_amd import _lib
+    monkeypatch.setenv("VAEB_DP_OVERLAP", overlap)
+    monkeypatch.setenv("VAEB_BF_FORK", fork)
     cfg = O.Config(D=256, H=128, Z=32)
     B = 256
     x = data_for(cfg, 8 * B)
