@@ -26,10 +26,7 @@ constexpr int kLP = 4;    // samples whose per-element operands are prefetched /
 
 // Sum over the 32 lanes that share t >> 5 (one latent row).
 DEV float sum32(float v) {
-    v += __shfl_xor(v, 1, 64);
-    v += __shfl_xor(v, 2, 64);
-    v += __shfl_xor(v, 4, 64);
-    v += __shfl_xor(v, 8, 64);
+    v = sum16(v);
     v += __shfl_xor(v, 16, 64);
     return v;
 }

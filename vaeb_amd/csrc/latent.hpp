@@ -265,19 +265,26 @@ DEV void enc_latent_body(const StepArgs& a, const FvFold& fvf) {
     const int Z = a.Z, H = a.H;
     const rsrc_t bs = mkbuf(a.slab_ml, (int64_t)gxE * nctH * 2 * Z * 16 * 4);
 
-    PEnc::Pre pre[CT] = {};
-    f32x4 bw[CT][2 * NCT];
-    if (wave == 0) {
+    // Row-parallel epilogue: phase A -- wave w < 4 CT finishes row group r = w & 3 of h column
+    // tile c = w >> 2 (sum of the 8 K-slice partials, bias, tanh, h); phase B -- wave w < 2 NCT
+    // forms part w of the tile's [mu | lv] partial (mu / lv of latent tile w >> 1) from all of
+    // h through LDS.  (One wave running both phases serially was ~2.5 us of the launch.)  The
+    // ticketed slab form (HO 0) keeps its single storing wave for phase B (arrive_last).
+    constexpr bool kOneB = HO == 0;
+    const int ca = wave >> 2, ra = wave & 3;
+    const bool wa = wave < 4 * CT, wb = kOneB ? wave == 0 : wave < 2 * NCT;
+    PEnc::Pre pre{};
+    f32x4 bw[CT][kOneB ? 2 * NCT : 1];
+    if (wa) pre = p.prefetch(m0, n0 + 16 * ca);
+    if (wb) {
         const rsrc_t bw4 = mkbuf(a.W4, (int64_t)H * Z * 4), bw5 = mkbuf(a.W5, (int64_t)H * Z * 4);
 #pragma unroll
-        for (int c = 0; c < CT; ++c) {
-            pre[c] = p.prefetch(m0, n0 + 16 * c);
+        for (int c = 0; c < CT; ++c)
 #pragma unroll
-            for (int ct = 0; ct < NCT; ++ct) {
-                bw[c][2 * ct] = mc4(bw4, Z, ct * 16 + li, n0 + 16 * c + 4 * q, Z, H);
-                bw[c][2 * ct + 1] = mc4(bw5, Z, ct * 16 + li, n0 + 16 * c + 4 * q, Z, H);
+            for (int u = 0; u < (kOneB ? 2 * NCT : 1); ++u) {
+                const int w = kOneB ? u : wave;
+                bw[c][u] = mc4((w & 1) ? bw5 : bw4, Z, (w >> 1) * 16 + li, n0 + 16 * c + 4 * q, Z, H);
             }
-        }
     }
     // AT: the bias of each element this thread may complete (column c: b4[c] | b5[c - Z])
     float bias[NCT];
@@ -295,26 +302,24 @@ DEV void enc_latent_body(const StepArgs& a, const FvFold& fvf) {
     for (int c = 0; c < CT; ++c) acc[c] = zero4();
     wave_mainloop<CT, 8, GCH>(p, m0 + li, n0 + li, p.K, wave, acc);
     VAEB_STAMP(a, 1);
+    float* redh = reinterpret_cast<float*>(red);   // [c][r][slice][lane]: CT * 2048 floats
 #pragma unroll
-    for (int c = 0; c < CT; ++c) red[(c * 8 + wave) * 64 + lane] = acc[c];
+    for (int c = 0; c < CT; ++c)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) redh[((c * 4 + r) * 8 + wave) * 64 + lane] = acc[c][r];
     __syncthreads();
-    if (wave == 0) {
+    if (a.order && bx == 0 && by == 0 && threadIdx.x == 0) *a.cur_batch = a.cursor[kCtlNext];
+    if (wa) {
+        float t = redh[((ca * 4 + ra) * 8) * 64 + lane];
 #pragma unroll
-        for (int c = 0; c < CT; ++c)
-#pragma unroll
-            for (int s = 1; s < 8; ++s) acc[c] += red[(c * 8 + s) * 64 + lane];
-        if (a.order && bx == 0 && by == 0 && lane == 0) *a.cur_batch = a.cursor[kCtlNext];
-#pragma unroll
-        for (int c = 0; c < CT; ++c) {
-            const int n = n0 + 16 * c + li;
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int m = m0 + 4 * q + r;
-                const float hv = (m < a.Mb && n < H) ? ftanh(acc[c][r] + pre[c].b) : 0.f;
-                if (n < H) a.h[(int64_t)m * H + n] = hv;
-                hs[4 * q + r][16 * c + li] = hv;
-            }
-        }
+        for (int sl = 1; sl < 8; ++sl) t += redh[((ca * 4 + ra) * 8 + sl) * 64 + lane];
+        const int n = n0 + 16 * ca + li, m = m0 + 4 * q + ra;
+        const float hv = (m < a.Mb && n < H) ? ftanh(t + pre.b) : 0.f;
+        if (n < H) a.h[(int64_t)m * H + n] = hv;
+        hs[4 * q + ra][16 * ca + li] = hv;
+    }
+    __syncthreads();
+    if (wb) {
         // partial [mu|lv] of this tile: (16 x 16 CT h) . (16 CT rows of [W4|W5])
         f32x4 av[CT];
 #pragma unroll
@@ -322,36 +327,27 @@ DEV void enc_latent_body(const StepArgs& a, const FvFold& fvf) {
 #pragma unroll
             for (int s = 0; s < 4; ++s) av[c][s] = hs[li][16 * c + 4 * q + s];
         const int64_t base = ((int64_t)bx * nctH + by) * 2 * Z;
-        auto part = [&](int w) {
-            f32x4 v = mfma4(av[0], bw[0][w], zero4());
+        auto part = [&](int u) {
+            f32x4 v = mfma4(av[0], bw[0][u], zero4());
 #pragma unroll
-            for (int c = 1; c < CT; ++c) v = mfma4(av[c], bw[c][w], v);
+            for (int c = 1; c < CT; ++c) v = mfma4(av[c], bw[c][u], v);
             return v;
         };
-        if constexpr (HO == 1) {
 #pragma unroll
-            for (int w = 0; w < 2 * NCT; ++w) {
-                const f32x4 sv = part(w);
-                const int nz = (w >> 1) * 16 + li;
+        for (int u = 0; u < (kOneB ? 2 * NCT : 1); ++u) {
+            const int w = kOneB ? u : wave;
+            const f32x4 sv = part(u);
+            const int nz = (w >> 1) * 16 + li;   // latent column of this lane
+            if constexpr (HO == 1) {
                 if (nz < Z)
 #pragma unroll
                     for (int r = 0; r < 4; ++r) pm[(w & 1) * Z + nz][4 * q + r] = sv[r];
-            }
-        } else if constexpr (HO == 3) {
-            // the decoder launch sums the slabs (decout_z_kernel<.., ZM = 2>): plain stores,
-            // made visible by the kernel boundary
-#pragma unroll
-            for (int w = 0; w < 2 * NCT; ++w) {
-                const f32x4 sv = part(w);
-                const int nz = (w >> 1) * 16 + li;
+            } else if constexpr (HO == 3) {
+                // the decoder launch sums the slabs (decout_z_kernel<.., ZM = 2>): plain stores,
+                // made visible by the kernel boundary
                 __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, sv), bs,
                                                        nz < Z ? (uint32_t)(((base + (w & 1) * Z + nz) * 16 + 4 * q) * 4) : kOOB, 0, 0);
-            }
-        } else {
-#pragma unroll
-            for (int w = 0; w < 2 * NCT; ++w) {
-                const f32x4 sv = part(w);
-                const int nz = (w >> 1) * 16 + li;  // latent column of this lane
+            } else {
                 st4_sc1(bs, nz < Z ? (uint32_t)(((base + (w & 1) * Z + nz) * 16 + 4 * q) * 4) : kOOB, sv);
             }
         }
@@ -509,10 +505,14 @@ __global__ __launch_bounds__(512) void enc_latent_fv_kernel(StepArgs a, FvFold f
 // wrote); 2 = the encoder's CT = 2 partial [mu | lv] slabs (enc_latent_body<.., HO = 3, 2>,
 // ceil(H / 32) per row block) summed here in fixed order, + bias, eps drawn here, and column
 // tile 0 stores mu, lv, eps, z and the KL / LA terms for the backward and the ELBO.
-template <int NB, int ZS, bool V1, int ZM>
-__global__ __launch_bounds__(512, 4) void decout_z_kernel(StepArgs a) {
+// CT: 16-column output tiles per workgroup (1, or 2 for the Bernoulli decoder: one workgroup
+// per CU at MNIST instead of 343 workgroups on 256 CUs, and the W1 / slab reads and the hd
+// recompute shared by both tiles).  NT = NB * CT accumulators, tile-major.
+template <int NB, int ZS, bool V1, int ZM, int CT>
+DEV void decout_z_body(const StepArgs& a) {
     constexpr bool AT = ZM != 0;
-    constexpr int CW = 16;   // output columns per workgroup
+    constexpr int CW = 16 * CT;   // output columns per workgroup
+    constexpr int NT = NB * CT;
     using PD = PDecOut;
     VAEB_STAMP(a, 0);
     PD p{a, nullptr, a.Me, a.D, a.H};
@@ -529,10 +529,10 @@ __global__ __launch_bounds__(512, 4) void decout_z_kernel(StepArgs a) {
     const rsrc_t bw1 = mkbuf(a.W1, (int64_t)Z * H * 4);
     const rsrc_t bb1 = mkbuf(a.b1, (int64_t)H * 4);
     constexpr bool v1 = V1;
-    typename PD::Pre pre{};
-    f32x4 acc[NB];
+    typename PD::PreRow pre{};
+    f32x4 acc[NT];
 #pragma unroll
-    for (int w = 0; w < NB; ++w) acc[w] = zero4();
+    for (int w = 0; w < NT; ++w) acc[w] = zero4();
     // W1^T rows kb + 4 li + (0..3) at latent 4t + q; b1 at kb + 16 q + 4 r + (0..3); W2 rows
     // kb + 16 q + 4 r + u.  The first block's loads are issued BEFORE the z prologue (whose
     // own loads -- z, mu / lv / eps, or the encoder's slabs -- they do not depend on), so
@@ -541,7 +541,7 @@ __global__ __launch_bounds__(512, 4) void decout_z_kernel(StepArgs a) {
     // so that the hoisted block still fits 128 VGPRs (round 2's 16 slab float4s per thread
     // beside it spilled).
     f32x4 w1v[ZS], b1v[4];
-    float w2b[4][4][NB];
+    float w2b[4][4][NT];
     auto load_block = [&](int kb) {
 #pragma unroll
         for (int t = 0; t < ZS; ++t) {
@@ -555,11 +555,28 @@ __global__ __launch_bounds__(512, 4) void decout_z_kernel(StepArgs a) {
 #pragma unroll
             for (int r = 0; r < 4; ++r)
 #pragma unroll
-                for (int w = 0; w < NB; ++w) {
+                for (int w = 0; w < NT; ++w) {
                     const int k = kb + 16 * q + 4 * r + u;
-                    w2b[u][r][w] = p.b1(n0 + li, k, w);
+                    w2b[u][r][w] = p.b1(n0 + 16 * (w / NB) + li, k, w % NB);
                 }
     };
+    // ZM 2: the first kSlabPer slab loads of each thread are issued BEFORE the weight block:
+    // vmcnt counts in issue order, so the slab sum (the critical path to z) then waits only for
+    // its own loads, not for the 25 weight-block loads behind them.
+    constexpr int kSlabPer = 6;
+    f32x4 sv0[ZM == 2 ? kSlabPer : 1];
+    const int nctS = (H + 31) >> 5, nf4S = 8 * Z;
+    const int npS = 512 / nf4S;   // nf4 <= 256 (Z <= 32): np >= 2
+    const int fS = (int)threadIdx.x % nf4S, partS = (int)threadIdx.x / nf4S;
+    const rsrc_t bsl = mkbuf(a.slab_ml, ZM == 2 ? (int64_t)(a.Mbp >> 4) * nctS * nf4S * 16 : 0);
+    const int64_t firstS = (int64_t)((m0 % a.Mbp) >> 4) * nctS * nf4S + fS;
+    if constexpr (ZM == 2) {
+#pragma unroll
+        for (int u = 0; u < kSlabPer; ++u) {
+            const int ct = partS + u * npS;
+            sv0[u] = bld4(bsl, (partS < npS && ct < nctS) ? (uint32_t)((firstS + (int64_t)ct * nf4S) * 16) : kOOB);
+        }
+    }
     load_block(64 * wave);
     float zb[ZS];
     if constexpr (!AT) {
@@ -596,14 +613,12 @@ __global__ __launch_bounds__(512, 4) void decout_z_kernel(StepArgs a) {
             // partition part = t / nf4 of the 512 threads sums slabs part, part + np, ... in
             // order (at most kSlabPer loads in flight per thread), then thread f adds the np
             // partition sums in order -- a fixed order, so the result is deterministic
-            constexpr int kSlabPer = 6;
-            const int nct = (H + 31) >> 5, nf4 = 8 * Z;
-            const int np = 512 / nf4;   // nf4 <= 256 (Z <= 32): np >= 2
-            const rsrc_t bsl = mkbuf(a.slab_ml, (int64_t)(a.Mbp >> 4) * nct * nf4 * 16);
-            const int f = (int)threadIdx.x % nf4, part = (int)threadIdx.x / nf4;
-            const int64_t first = (int64_t)(i0 >> 4) * nct * nf4 + f;
+            const int nct = nctS, nf4 = nf4S, np = npS, f = fS, part = partS;
+            const int64_t first = firstS;
             f32x4 sum = zero4();
-            for (int c0 = part; c0 < nct; c0 += kSlabPer * np) {
+#pragma unroll
+            for (int u = 0; u < kSlabPer; ++u) sum += sv0[u];
+            for (int c0 = part + kSlabPer * np; c0 < nct; c0 += kSlabPer * np) {
                 f32x4 v[kSlabPer];
 #pragma unroll
                 for (int u = 0; u < kSlabPer; ++u) {
@@ -623,6 +638,7 @@ __global__ __launch_bounds__(512, 4) void decout_z_kernel(StepArgs a) {
                 for (int k = 0; k < 4; ++k) msum[c][4 * mq + k] = t[k];
             }
             __syncthreads();
+            VAEB_STAMP(a, 6);   // (timeline build) slab sum done
         }
         if ((int)threadIdx.x < per) {
             const int ml = threadIdx.x / Z, j = threadIdx.x - ml * Z;
@@ -666,6 +682,7 @@ __global__ __launch_bounds__(512, 4) void decout_z_kernel(StepArgs a) {
             }
         }
         __syncthreads();
+        VAEB_STAMP(a, 7);   // (timeline build) z formed
 #pragma unroll
         for (int t = 0; t < ZS; ++t) zb[t] = (4 * t + q < Z) ? zs[li][4 * t + q] : 0.f;
         if (col0 && threadIdx.x < 16 && (a.est == EST_LA || l == 0)) {
@@ -678,9 +695,9 @@ __global__ __launch_bounds__(512, 4) void decout_z_kernel(StepArgs a) {
     }
     for (int kb = 64 * wave; kb < H; kb += 64 * 8) {
         if (kb != 64 * wave) load_block(kb);
-        if (kb == 0) {   // wave 0, first block: its loads are in flight
+        if (kb == 64 * wave && wave < 4 * CT) {   // epilogue waves, first block: its loads are in flight
             p.x = x_rows(a);
-            pre = p.prefetch(m0, n0);
+            pre = p.prefetch_row(m0, n0 + 16 * (wave >> 2), wave & 3);
         }
         f32x4 hv[4];
 #pragma unroll
@@ -711,14 +728,49 @@ __global__ __launch_bounds__(512, 4) void decout_z_kernel(StepArgs a) {
 #pragma unroll
             for (int r = 0; r < 4; ++r)
 #pragma unroll
-                for (int w = 0; w < NB; ++w)
+                for (int w = 0; w < NT; ++w)
                     acc[w] = __builtin_amdgcn_mfma_f32_16x16x4f32(hv[u][r], w2b[u][r][w], acc[w], 0, 0, 0);
     }
+    if (wave < 4 * CT && 64 * wave >= H) {   // an epilogue wave without a K block (H <= 192)
+        p.x = x_rows(a);
+        pre = p.prefetch_row(m0, n0 + 16 * (wave >> 2), wave & 3);
+    }
     VAEB_STAMP(a, 1);
-    if (!ks_reduce<8, 8, NB>(acc, wave, wave)) return;
+    // Row-parallel epilogue: the 8 K-slice partials go through LDS as [slice][tile][r][lane],
+    // then wave r (< 4) sums row group r of the tile (slices in order 0..7) and finishes it.
+    // One wave running all four row groups serially was ~0.55 us per group (a single wave's
+    // dependent chain of likelihood, stores and the row sum): 2.2 us of the launch.
+    // (CT = 2: wave w < 8 finishes row group w & 3 of tile w >> 2)
+    __shared__ float redr[8][NT][4][64];
+#pragma unroll
+    for (int w = 0; w < NT; ++w)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) redr[wave][w][r][lane] = acc[w][r];
+    __syncthreads();
     VAEB_STAMP(a, 2);
-    p.epilogue(m0, n0, acc, pre);
+    const int et = wave >> 2, er = wave & 3;
+    if (wave >= 4 * CT || n0 + 16 * et >= a.D) return;
+    float c[NB];
+#pragma unroll
+    for (int w = 0; w < NB; ++w) {
+        float t = redr[0][et * NB + w][er][lane];
+#pragma unroll
+        for (int s = 1; s < 8; ++s) t += redr[s][et * NB + w][er][lane];
+        c[w] = t;
+    }
+    VAEB_STAMP_SYNC(a, 4);   // (timeline build) the epilogue's operands landed
+    p.epilogue_row(m0, n0 + 16 * et, er, c[0], c[NB - 1], pre);
     VAEB_STAMP(a, 3);
+    VAEB_STAMP_SYNC(a, 5);   // (timeline build) the epilogue's stores drained
+}
+template <int NB, int ZS, bool V1, int ZM>
+__global__ __launch_bounds__(512, 4) void decout_z_kernel(StepArgs a) {
+    decout_z_body<NB, ZS, V1, ZM, 1>(a);
+}
+// two 16-column tiles per workgroup (Bernoulli): one workgroup per CU, so the full register file
+template <int ZS, bool V1, int ZM>
+__global__ __launch_bounds__(512, 2) void decout_z2_kernel(StepArgs a) {
+    decout_z_body<1, ZS, V1, ZM, 2>(a);
 }
 
 }  // namespace vaeb

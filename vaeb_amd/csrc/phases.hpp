@@ -252,52 +252,67 @@ struct PDecOut {
         }
         return pr;
     }
-    template <int NB>
-    DEV void epilogue(int m0, int n0, const f32x4 (&acc)[NB], const Pre& pre) const {
+    // The operands of ONE row group r of the C/D map (rows m0 + 4 q + r): the row-parallel
+    // epilogue of decout_z_kernel, where wave r finishes row group r.
+    struct PreRow { float b2, b6, xv; };
+    DEV PreRow prefetch_row(int m0, int n0, int r) const {
+        const int lane = threadIdx.x & 63;
+        const int n = n0 + (lane & 15);
+        const bool ncol = n < a.D;
+        const int i = (m0 + 4 * (lane >> 4) + r) % a.Mbp;
+        PreRow pr;
+        pr.b2 = bld(mkbuf(a.b2, (int64_t)a.D * 4), ncol ? (uint32_t)n * 4u : kOOB);
+        pr.b6 = (a.dec == DEC_GAUSSIAN) ? bld(mkbuf(a.b6, (int64_t)a.D * 4), ncol ? (uint32_t)n * 4u : kOOB) : 0.f;
+        pr.xv = bld(mkbuf(x, (int64_t)a.Mb * a.D * 4), (ncol && i < a.Mb) ? (uint32_t)(i * a.D + n) * 4u : kOOB);
+        return pr;
+    }
+    // Row group r: c2 = (hd W2)[m][n], c6 = (hd W6)[m][n] (Gaussian).
+    DEV void epilogue_row(int m0, int n0, int r, float c2, float c6, const PreRow& pre) const {
         const int lane = threadIdx.x & 63;
         const int n = n0 + (lane & 15);
         const bool ncol = n < a.D;
         const int ct = n0 >> 4;
         const float sl = a.sc / (float)a.L;
-        const float b2 = pre.b2;
-        const float b6 = pre.b6;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const int m = m0 + 4 * (lane >> 4) + r;
-            const int i = m % a.Mbp;
-            const bool valid = ncol && i < a.Mb;
-            float lp = 0.f, d2 = 0.f, d6 = 0.f, yv = 0.f, a6 = 0.f;
-            if (valid) {
-                const float xv = pre.xv[r];
-                const float a2 = acc[0][r] + b2;
-                yv = sigmoidf(a2);
-                if (a.dec == DEC_GAUSSIAN) {
-                    a6 = acc[NB - 1][r] + b6;
-                    const float rr = xv - yv;
-                    const float e = fexp(-a6);
-                    lp = -kHalfLog2Pi - 0.5f * a6 - 0.5f * rr * rr * e;
-                    d2 = rr * e * yv * (1.f - yv) * sl;
-                    d6 = (-0.5f + 0.5f * rr * rr * e) * sl;
-                } else {
-                    lp = xv * a2 - softplusf(a2);
-                    d2 = (xv - yv) * sl;
-                }
+        const int m = m0 + 4 * (lane >> 4) + r;
+        const int i = m % a.Mbp;
+        const bool valid = ncol && i < a.Mb;
+        float lp = 0.f, d2 = 0.f, d6 = 0.f, yv = 0.f, a6 = 0.f;
+        if (valid) {
+            const float xv = pre.xv;
+            const float a2 = c2 + pre.b2;
+            yv = sigmoidf(a2);
+            if (a.dec == DEC_GAUSSIAN) {
+                a6 = c6 + pre.b6;
+                const float rr = xv - yv;
+                const float e = fexp(-a6);
+                lp = -kHalfLog2Pi - 0.5f * a6 - 0.5f * rr * rr * e;
+                d2 = rr * e * yv * (1.f - yv) * sl;
+                d6 = (-0.5f + 0.5f * rr * rr * e) * sl;
+            } else {
+                lp = xv * a2 - softplusf(a2);
+                d2 = (xv - yv) * sl;
             }
-            if (ncol) {
-                const int64_t o = (int64_t)m * a.D + n;
-                if (a.mode == MODE_TRAIN) {
-                    a.dA2[o] = d2;
-                    if (a.dec == DEC_GAUSSIAN) a.dA6[o] = d6;
-                } else if (a.mode == MODE_RECON) {
-                    a.y[o] = yv;
-                    // the decoder's log-sigma head (VAEB.py:258, freyFace.py:178): the dA6
-                    // plane is free outside training
-                    if (a.dec == DEC_GAUSSIAN) a.dA6[o] = a6;
-                }
-            }
-            lp = sum16(lp);
-            if ((lane & 15) == 0) a.lp_part[(int64_t)m * a.nctD + ct] = lp;
         }
+        if (ncol) {
+            const int64_t o = (int64_t)m * a.D + n;
+            if (a.mode == MODE_TRAIN) {
+                a.dA2[o] = d2;
+                if (a.dec == DEC_GAUSSIAN) a.dA6[o] = d6;
+            } else if (a.mode == MODE_RECON) {
+                a.y[o] = yv;
+                // the decoder's log-sigma head (VAEB.py:258, freyFace.py:178): the dA6
+                // plane is free outside training
+                if (a.dec == DEC_GAUSSIAN) a.dA6[o] = a6;
+            }
+        }
+        lp = sum16(lp);
+        if ((lane & 15) == 0) a.lp_part[(int64_t)m * a.nctD + ct] = lp;
+    }
+    template <int NB>
+    DEV void epilogue(int m0, int n0, const f32x4 (&acc)[NB], const Pre& pre) const {
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+            epilogue_row(m0, n0, r, acc[0][r], acc[NB - 1][r], PreRow{pre.b2, pre.b6, pre.xv[r]});
     }
 };
 

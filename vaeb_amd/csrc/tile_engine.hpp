@@ -168,12 +168,21 @@ DEV f32x4 mfma4(f32x4 a, f32x4 b, f32x4 c) {
     return c;
 }
 
-// Sum over the 16 lanes that share l >> 4 (one output row group of the C/D map).
+// One DPP lane move within a 16-lane row (all rows and banks enabled).
+template <int CTRL>
+DEV float dppf(float v) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
+}
+// Sum over the 16 lanes that share l >> 4 (one output row group of the C/D map), every lane
+// ending with the same value: quad_perm [1,0,3,2] and [2,3,0,1] (quad sums), row_half_mirror
+// (lane i <- 7 - i: the other quad of the half-row), row_mirror (lane i <- 15 - i: the other
+// half).  Four VALU-latency DPP adds instead of four ds_bpermute round trips through the LDS
+// unit (~100 cycles each with their waits: they dominated a single wave's epilogue rows).
 DEV float sum16(float v) {
-    v += __shfl_xor(v, 1, 64);
-    v += __shfl_xor(v, 2, 64);
-    v += __shfl_xor(v, 4, 64);
-    v += __shfl_xor(v, 8, 64);
+    v += dppf<0xB1>(v);
+    v += dppf<0x4E>(v);
+    v += dppf<0x141>(v);
+    v += dppf<0x140>(v);
     return v;
 }
 

@@ -154,6 +154,7 @@ struct vaeb_ctx {
     bool dp_overlap = false;      // bucket A on s2 (bf16 engine; VAEB_DP_OVERLAP=0/1 overrides)
     bool fold_bwd = true;         // Z <= 32: latent backward folded into the dhd launch (VAEB_FOLD_BWD=0: P67)
     int atomic_ho = 1;            // folded latent hand-offs: 1 by fan-in (ho_mode), 0 slabs
+    int decout_ct = -1;           // Bernoulli decoder column tiles per workgroup: -1 auto (2), VAEB_DECOUT_CT=1
     int enc_red = -1;             // encoder slabs summed by the decoder launch: -1 auto, VAEB_ENC_RED=0|1
     // profiling
     hipEvent_t pev[kMaxProfKernels + 1] = {};
@@ -280,7 +281,17 @@ ElboArgs base_elbo(vaeb_ctx* c, const StepArgs& a) {
 }
 
 template <int NB, bool V1, int AT>
-void launch_decout_zv(hipStream_t s, dim3 grid, const StepArgs& a) {
+void launch_decout_zv(hipStream_t s, dim3 grid, const StepArgs& a, int ct) {
+    if (NB == 1 && ct == 2) {   // two column tiles per workgroup
+        switch ((a.Z + 3) / 4) {
+            case 1: hipLaunchKernelGGL((decout_z2_kernel<1, V1, AT>), grid, dim3(512), 0, s, a); break;
+            case 2: hipLaunchKernelGGL((decout_z2_kernel<2, V1, AT>), grid, dim3(512), 0, s, a); break;
+            case 3: case 4: hipLaunchKernelGGL((decout_z2_kernel<4, V1, AT>), grid, dim3(512), 0, s, a); break;
+            case 5: hipLaunchKernelGGL((decout_z2_kernel<5, V1, AT>), grid, dim3(512), 0, s, a); break;
+            default: hipLaunchKernelGGL((decout_z2_kernel<8, V1, AT>), grid, dim3(512), 0, s, a); break;
+        }
+        return;
+    }
     switch ((a.Z + 3) / 4) {
         case 1: hipLaunchKernelGGL((decout_z_kernel<NB, 1, V1, AT>), grid, dim3(512), 0, s, a); break;
         case 2: hipLaunchKernelGGL((decout_z_kernel<NB, 2, V1, AT>), grid, dim3(512), 0, s, a); break;
@@ -290,10 +301,10 @@ void launch_decout_zv(hipStream_t s, dim3 grid, const StepArgs& a) {
     }
 }
 template <int NB, int AT>
-void launch_decout_z(hipStream_t s, dim3 grid, const StepArgs& a) {
+void launch_decout_z(hipStream_t s, dim3 grid, const StepArgs& a, int ct = 1) {
     auto al = [](const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
-    if ((a.H & 3) == 0 && al(a.W1) && al(a.b1)) launch_decout_zv<NB, true, AT>(s, grid, a);
-    else launch_decout_zv<NB, false, AT>(s, grid, a);
+    if ((a.H & 3) == 0 && al(a.W1) && al(a.b1)) launch_decout_zv<NB, true, AT>(s, grid, a, ct);
+    else launch_decout_zv<NB, false, AT>(s, grid, a, ct);
 }
 
 // dhd_dz_wgrad_kernel at compile-time NCT (latent col tiles), GCH, load width, AT
@@ -389,9 +400,9 @@ int enqueue_forward(vaeb_ctx* c, const StepArgs& a0, Prof& pr, const FvFold& fvf
         }
         CHECK_LAUNCH();
         a.dbg = next_dbg(c);
-        // (two 16-column tiles per Bernoulli workgroup, 175 instead of 343: 43.3 vs 43.1 us,
-        // removed in round 3)
-        const dim3 g4(a.Me / 16, cdiv(a.D, 16));
+        // Bernoulli: two 16-column tiles per workgroup (decout_z2_kernel)
+        const int dct = (!gaussian(c) && c->decout_ct != 1) ? 2 : 1;
+        const dim3 g4(a.Me / 16, cdiv(a.D, 16 * dct));
         pr.mark(17);
         REP(pr) {
             if (gaussian(c)) {
@@ -399,9 +410,9 @@ int enqueue_forward(vaeb_ctx* c, const StepArgs& a0, Prof& pr, const FvFold& fvf
                 else if (at == 1) launch_decout_z<2, 1>(s, g4, a);
                 else launch_decout_z<2, 0>(s, g4, a);
             } else {
-                if (at == 2) launch_decout_z<1, 2>(s, g4, a);
-                else if (at == 1) launch_decout_z<1, 1>(s, g4, a);
-                else launch_decout_z<1, 0>(s, g4, a);
+                if (at == 2) launch_decout_z<1, 2>(s, g4, a, dct);
+                else if (at == 1) launch_decout_z<1, 1>(s, g4, a, dct);
+                else launch_decout_z<1, 0>(s, g4, a, dct);
             }
         }
         CHECK_LAUNCH();
@@ -971,6 +982,7 @@ int vaeb_create(const vaeb_config* cfg, vaeb_ctx** out) {
     if (const char* bk = getenv("VAEB_BF_FORK")) c->bf_fork = atoi(bk) != 0;
     if (const char* ah = getenv("VAEB_ATOMIC_HO")) c->atomic_ho = atoi(ah) != 0 ? 1 : 0;
     if (const char* er = getenv("VAEB_ENC_RED")) c->enc_red = atoi(er) != 0 ? 1 : 0;
+    if (const char* dc = getenv("VAEB_DECOUT_CT")) c->decout_ct = atoi(dc) == 1 ? 1 : 2;
     {
         const char* g8 = getenv("VAEB_BF_GEMM8");
         // default: the 8-phase loop for KC x KC (dhd) and KC x KO (enc, dechid); KO x KO (the
