@@ -45,5 +45,5 @@ for rep in range(3):
             for j in range(8):
                 v = s[sel, j]
                 v = v[v > 0] - t0
-                if len(v) and (k == 1 or (j != 6 and j != 7)):
+                if len(v) and j != 7:
                     print(f"    slot {j}: n={len(v):4d} min={v.min():5d} med={int(np.median(v)):5d} max={v.max():5d}")

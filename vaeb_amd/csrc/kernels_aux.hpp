@@ -212,7 +212,9 @@ struct OptArgs {
 DEV float opt_rule(const OptArgs& o, float th, float& acc, float dsg) {
     const float g = dsg - o.prior * th;
     acc += g * g;
-    return th + o.lr * g / (sqrtf(acc) + o.eps) - o.decay * th * th;
+    // hardware sqrt / reciprocal (1 ulp each) instead of the IEEE-exact expansions: a
+    // weight-gradient epilogue wave ran ~50 instructions per parameter on them
+    return th + o.lr * g * __builtin_amdgcn_rcpf(__builtin_amdgcn_sqrtf(acc) + o.eps) - o.decay * th * th;
 }
 
 // ----------------------------------------------------------------- weight gradients
@@ -363,6 +365,12 @@ DEV void wgrad_body(const WA& p, const WGroup& g, int bid, float (*sa)[kWP], flo
     // resolve the batch pointer first: its load must not queue behind the prefetches below
     const float* at = g.at_is_x ? p.xbase + (int64_t)ld_launch_const(p.cur_batch) * p.batch_stride : g.at;
     const rsrc_t ba = mkbuf(at, (int64_t)g.klim_at * g.ld_at * 4);
+#ifdef VAEB_TIMELINE
+    if (VAEB_DBG_ON(p.dbg) && threadIdx.x == 0) {   // the batch pointer resolved
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        p.dbg[bid * 8 + 4] = __builtin_amdgcn_s_memrealtime();
+    }
+#endif
     const int lt = bid - g.wg_begin;
     const int i0 = (lt / g.tiles_j) * kWT, j0 = (lt % g.tiles_j) * kWTJ;
     const int lane = threadIdx.x & 63, wave = (threadIdx.x >> 6) & 3, kh = threadIdx.x >> 8;
@@ -440,7 +448,16 @@ DEV void wgrad_body(const WA& p, const WGroup& g, int bid, float (*sa)[kWP], flo
                 }
             }
         }
+#ifdef VAEB_TIMELINE
+        if (VAEB_DBG_ON(p.dbg) && kb == 0) {   // the stage's panel loads landed
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (threadIdx.x == 0) p.dbg[bid * 8 + 5] = __builtin_amdgcn_s_memrealtime();
+        }
+#endif
         if constexpr (DA3) da3_panel<NWV, TS>(p.da3, kb, j0, i0 == 0, sb);
+#ifdef VAEB_TIMELINE
+        if (VAEB_DBG_ON(p.dbg) && kb == 0 && threadIdx.x == 0) p.dbg[bid * 8 + 2] = __builtin_amdgcn_s_memrealtime();
+#endif
 #pragma unroll
         for (int u = 0; u < NU; ++u) {
             const int e = threadIdx.x + NTH * u;
@@ -454,6 +471,9 @@ DEV void wgrad_body(const WA& p, const WGroup& g, int bid, float (*sa)[kWP], flo
             if constexpr (!DA3) *reinterpret_cast<f32x4*>(&sb[kr][4 * c4]) = rb[u];
         }
         __syncthreads();
+#ifdef VAEB_TIMELINE
+        if (VAEB_DBG_ON(p.dbg) && kb == 0 && threadIdx.x == 0) p.dbg[bid * 8 + 6] = __builtin_amdgcn_s_memrealtime();
+#endif
         const int nch = min(kWKB, g.K - kb) >> 4;
         for (int c = kh; c < nch; c += NWV / 4) {
             const int kk = 16 * c + 4 * q;

@@ -62,9 +62,18 @@ DEV f32x4 ld4_sc1(rsrc_t b, uint32_t off) {
 // before the add, agent acquire after it) for the A/B in DESIGN.md 4.1: the release writes
 // back the XCD L2 (buffer_wbl2) and the acquire invalidates the CU's L1, ~1.7 us each by
 // the guide's price list.
+// NSW > 1: waves 0 .. NSW-1 stored slab bytes; each drains, the workgroup barrier follows,
+// then lane 0 makes the one ticket add (the guide's producer form "every storing wave's
+// s_waitcnt vmcnt(0), the workgroup's barrier, then ... flag/counter", the release replaced
+// by the sc1 stores as above).
+template <int NSW = 1>
 DEV bool arrive_last(int* cnt, int target, int* sflag) {
+    if constexpr (NSW > 1) {
+        if ((int)threadIdx.x < 64 * NSW) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+    }
     if (threadIdx.x < 64) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if constexpr (NSW == 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         if (threadIdx.x == 0) {
 #ifdef VAEB_SLAB_ACQREL
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");

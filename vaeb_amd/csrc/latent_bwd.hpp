@@ -74,25 +74,30 @@ DEV void dhd_dz_body(const PDhdT<V>& p0, int bx, int by, f32x4* red, int sid) {
     const int nrb = a.Mbp >> 4, nctH = (H + 15) >> 4;
     const int l = bx / nrb, rbl = bx % nrb;
 
-    typename PDhdT<V>::Pre pre{};
-    f32x4 w1v[NCT];
-    float ev[NCT][4];   // AT: eps_l at (row 4q + r, latent j)
-    if (wave == 0) {
-        pre = p.prefetch(m0, n0);
-        // W1^T rows n0 .. n0 + 15 at latent j = ct * 16 + li: 4 consecutive n per lane
+    // Row-parallel epilogue: phase A -- wave r < 4 finishes row group r of the dA1 tile (sum
+    // of the 8 K-slice partials, dtanh, dA1); phase B -- wave ct < NCT forms the tile's partial
+    // dZ for latent tile ct from all of dA1 through LDS (one wave running both phases serially
+    // took ~1.3 us of the launch's critical path).
+    const int er = wave & 3;
+    float hdv = 0.f;
+    f32x4 w1v{};
+    float ev[4];   // HO: eps_l at (row 4q + r, latent j = 16 wave + li)
+    if (wave < 4) {
+        const int n = n0 + li, m = m0 + 4 * q + er;
+        hdv = bld(mkbuf(a.hd, (int64_t)a.Me * H * 4), (n < H && m < a.Me) ? (uint32_t)(m * H + n) * 4u : kOOB);
+    }
+    if (wave < NCT) {
+        // W1^T rows n0 .. n0 + 15 at latent j = 16 wave + li: 4 consecutive n per lane
         const rsrc_t bw1 = mkbuf(a.W1, (int64_t)Z * H * 4);
         const bool vh = (H & 3) == 0 && aligned16(a.W1);
-#pragma unroll
-        for (int ct = 0; ct < NCT; ++ct) w1v[ct] = kc4(bw1, H, ct * 16 + li, n0 + 4 * q, Z, H, vh);
+        w1v = kc4(bw1, H, wave * 16 + li, n0 + 4 * q, Z, H, vh);
         if constexpr (HO != 0) {
             const rsrc_t be = mkbuf(a.eps, (int64_t)a.Me * Z * 4);
 #pragma unroll
-            for (int ct = 0; ct < NCT; ++ct)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const int j = ct * 16 + li, m = rbl * 16 + 4 * q + r;
-                    ev[ct][r] = bld(be, j < Z ? (uint32_t)((l * a.Mbp + m) * Z + j) * 4u : kOOB);
-                }
+            for (int r = 0; r < 4; ++r) {
+                const int j = wave * 16 + li, m = rbl * 16 + 4 * q + r;
+                ev[r] = bld(be, j < Z ? (uint32_t)((l * a.Mbp + m) * Z + j) * 4u : kOOB);
+            }
         }
     }
     // AT: mu, lv of each element this thread may complete (column c: dMu | dLv of latent c % Z)
@@ -110,45 +115,38 @@ DEV void dhd_dz_body(const PDhdT<V>& p0, int bx, int by, f32x4* red, int sid) {
     f32x4 acc[1] = {zero4()};
     wave_mainloop<1, 8, GCH>(p, m0 + li, n0 + li, p.K, wave, acc);
     VAEB_STAMP_AT(a, sid, 1);
-    red[wave * 64 + lane] = acc[0];
+    float* redf = reinterpret_cast<float*>(red);   // [r][slice][lane]
+#pragma unroll
+    for (int r = 0; r < 4; ++r) redf[(r * 8 + wave) * 64 + lane] = acc[0][r];
     __syncthreads();
-    if (wave == 0) {
+    if (wave < 4) {
+        float t = redf[(er * 8) * 64 + lane];
 #pragma unroll
-        for (int s = 1; s < 8; ++s) acc[0] += red[s * 64 + lane];
-        const int n = n0 + li;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const int m = m0 + 4 * q + r;
-            const float hd = pre.hd[r];
-            const float v = (n < H && (m % a.Mbp) < a.Mb) ? acc[0][r] * (1.f - hd * hd) : 0.f;
-            if (n < H) a.dA1[(int64_t)m * H + n] = v;
-            ts[4 * q + r][li] = v;
-        }
-        // partial dZ of this tile: (16 x 16 dA1) . (16 rows of W1^T)
+        for (int sl = 1; sl < 8; ++sl) t += redf[(er * 8 + sl) * 64 + lane];
+        const int n = n0 + li, m = m0 + 4 * q + er;
+        const float v = (n < H && (m % a.Mbp) < a.Mb) ? t * (1.f - hdv * hdv) : 0.f;
+        if (n < H) a.dA1[(int64_t)m * H + n] = v;
+        ts[4 * q + er][li] = v;
+    }
+    __syncthreads();
+    if (wave < NCT) {
+        // partial dZ of this tile, latent tile ct = wave: (16 x 16 dA1) . (16 rows of W1^T)
         f32x4 av;
 #pragma unroll
         for (int s = 0; s < 4; ++s) av[s] = ts[li][4 * q + s];
+        const f32x4 sv = mfma4(av, w1v, zero4());
+        const int j = wave * 16 + li;
         if constexpr (HO != 0) {
+            if (j < Z)
 #pragma unroll
-            for (int ct = 0; ct < NCT; ++ct) {
-                const f32x4 sv = mfma4(av, w1v[ct], zero4());
-                const int j = ct * 16 + li;
-                if (j < Z)
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) {
-                        pm[j][4 * q + r] = sv[r];
-                        pm[Z + j][4 * q + r] = sv[r] * ev[ct][r];
-                    }
-            }
+                for (int r = 0; r < 4; ++r) {
+                    pm[j][4 * q + r] = sv[r];
+                    pm[Z + j][4 * q + r] = sv[r] * ev[r];
+                }
         } else {
             const rsrc_t bs = mkbuf(a.slab_dz, (int64_t)a.L * a.Mbp * nctH * Z * 4);
             const int64_t blk = ((int64_t)l * nrb + rbl) * nctH + by;
-#pragma unroll
-            for (int ct = 0; ct < NCT; ++ct) {
-                const f32x4 sv = mfma4(av, w1v[ct], zero4());
-                const int j = ct * 16 + li;
-                st4_sc1(bs, j < Z ? (uint32_t)(((blk * Z + j) * 16 + 4 * q) * 4) : kOOB, sv);
-            }
+            st4_sc1(bs, j < Z ? (uint32_t)(((blk * Z + j) * 16 + 4 * q) * 4) : kOOB, sv);
         }
     }
     if constexpr (AT) {
@@ -185,7 +183,7 @@ DEV void dhd_dz_body(const PDhdT<V>& p0, int bx, int by, f32x4* red, int sid) {
         return;
     }
     VAEB_STAMP_AT(a, sid, 2);
-    if (!arrive_last(a.cnt_dz + rbl, nctH * a.L, &sflag)) return;
+    if (!arrive_last<NCT>(a.cnt_dz + rbl, nctH * a.L, &sflag)) return;
     VAEB_STAMP_AT(a, sid, 3);
 
     // ---- reducer: latent row block rbl, all L planes.  Thread (ml, j) owns one element;
