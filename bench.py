@@ -92,14 +92,14 @@ KERNEL_SYMBOLS = {"p1_enc": "PEnc", "p23_heads_dechid": "heads_dechid_kernel", "
                   "fvs_sample": "vaeb::fvs_sample_kernel",
                   "p8_wgrad_w3w45": "vaeb::wgrad_kernel",
                   "p1_enc_latent": ("vaeb::enc_latent",),   # enc_latent_kernel | enc_latent_fv_kernel
-                  "p4_decout_z": "vaeb::decout_z_kernel",
+                  "p4_decout_z": ("vaeb::decout_z",),   # decout_z_kernel | decout_z2_kernel
                   # bf16 GEMMs are one template: the epilogue / layout pair names the launch
                   # (all listed substrings must appear: the tile width is a template argument)
                   "bf_enc": ("gemm_kernel<0, 1,", "EpiBiasAct>"), "bf_decout": ("EpiDecOut<false>",),
                   "bf_dhd": ("gemm_kernel<0, 0,", "EpiDTanh>"), "bf_dW26": ("EpiAdagrad",),
                   "bf_dW3": ("EpiAdagrad",), "bf_dhd_dW26": ("gemm2_kernel",),
                   "p5_dhd_dz_w2": "vaeb::dhd_dz_wgrad_kernel", "p8_wgrad_w3w45w1": "vaeb::wgrad3_kernel"}
-PMC_FILES = {c: os.path.join(ROOT, "profiles", "r2", f"pmc_{c}_per_launch.json")
+PMC_FILES = {c: os.path.join(ROOT, "profiles", "r3", f"pmc_{c}_per_launch.json")
              for c in ("mnist", "frey", "fv", "fvs", "synth")}
 
 

@@ -1,12 +1,12 @@
 # Round evidence for every bench config, in one call: kernel-trace stats, FETCH_SIZE and
 # WRITE_SIZE PMC passes (separate runs, MI355X_MICROARCH.md §HBM), the MFMA-busy pass, then
-# the bench line with the CPU baseline (it reads the PMC traffic just copied into profiles/r1).
-# -> gpurun_out/round/<config>/ and profiles/r1/ (the box's copy; merged back via gpurun_out)
+# the bench line with the CPU baseline (it reads the PMC traffic just copied into profiles/${ROUND:-r3}).
+# -> gpurun_out/round/<config>/ and profiles/${ROUND:-r3}/ (the box's copy; merged back via gpurun_out)
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 OUT=gpurun_out/round
-mkdir -p $OUT/profiles
+mkdir -p $OUT/profiles profiles/${ROUND:-r3}
 for cfg in ${CONFIGS:-mnist frey fv fvs synth}; do
   O=$OUT/$cfg
   mkdir -p $O
@@ -25,8 +25,8 @@ for cfg in ${CONFIGS:-mnist frey fv fvs synth}; do
   fi
   cp $O/trace/run_kernel_stats.csv $OUT/profiles/${pre}kernel_stats.csv
   cp $O/pmc_summary.txt $OUT/profiles/${pre}pmc_summary.txt
-  cp $O/pmc_per_launch.json $OUT/profiles/pmc_${pre}per_launch.json
-  cp $O/pmc_per_launch.json profiles/r1/pmc_${pre}per_launch.json
+  cp $O/pmc_per_launch.json $OUT/profiles/pmc_${cfg}_per_launch.json
+  cp $O/pmc_per_launch.json profiles/${ROUND:-r3}/pmc_${cfg}_per_launch.json
   [ $cfg = mnist ] && cp $O/trace/run_domain_stats.csv $OUT/profiles/domain_stats.csv
   timeout -k 10 300 python3 bench.py --config $cfg > $O/bench_line.json 2> $O/bench_line.err || { tail $O/bench_line.err; exit 1; }
   cp $O/bench_line.json $OUT/profiles/${pre}bench_line.json
