@@ -11,7 +11,7 @@ for cfg in ${CONFIGS:-mnist frey fv fvs synth}; do
   O=$OUT/$cfg
   mkdir -p $O
   if [ $cfg = synth ]; then S="--steps 30 --warmup 3"; P="--steps 10 --warmup 2"; else S="--steps 1000 --warmup 100"; P="--steps 200 --warmup 20"; fi
-  if [ $cfg = mnist ]; then pre=""; else pre="${cfg}_"; fi
+  pre="${cfg}_"
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace -o run -- python3 bench.py --config $cfg $S --no-cpu-baseline > $O/bench_trace.json 2> $O/bench_trace.err || { tail $O/bench_trace.err; exit 1; }
   timeout -s KILL 200 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/fetch -o run -- python3 bench.py --config $cfg $P --no-cpu-baseline > /dev/null 2> $O/fetch.err || { tail $O/fetch.err; exit 1; }
   timeout -s KILL 200 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/write -o run -- python3 bench.py --config $cfg $P --no-cpu-baseline > /dev/null 2> $O/write.err || { tail $O/write.err; exit 1; }

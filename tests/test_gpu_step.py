@@ -378,7 +378,8 @@ def test_atomic_and_slab_handoffs_agree(kw, monkeypatch):
     """Every fp32 step form a switch can select, on the same 6 Philox steps: the default
     (VAEB_ATOMIC_HO=1: counted fixed-point atomics up to fan-in 16, slabs above), slabs +
     ticket + reducer everywhere (=0), the encoder slabs summed by the decoder launch
-    (VAEB_ENC_RED=1) and the unfolded latent backward (VAEB_FOLD_BWD=0: the P67 launches).
+    (VAEB_ENC_RED=1), the unfolded latent backward (VAEB_FOLD_BWD=0: the P67 launches) and
+    one 16-column tile per Bernoulli decoder workgroup (VAEB_DECOUT_CT=1).
     They sum the same partials in different arithmetic (exact integer vs ordered fp32), so
     they agree to rounding, and each is bitwise deterministic (graph == eager)."""
     from vaeb_amd import _lib
@@ -387,14 +388,16 @@ def test_atomic_and_slab_handoffs_agree(kw, monkeypatch):
     x = data_for(cfg, 8 * B)
     order = np.array([3, 1, 4, 1, 5, 7], np.int32)
     out = {}
-    # "decred": VAEB_ENC_RED=1, the encoder's slabs summed by every decoder workgroup
-    modes = {"atomic": ("1", "0", "1"), "slab": ("0", "0", "1"), "decred": ("1", "1", "1"),
-             "unfolded": ("1", "0", "0")}
+    # "decred": VAEB_ENC_RED=1, the encoder's slabs summed by every decoder workgroup;
+    # "dct1": one 16-column tile per Bernoulli decoder workgroup (default two)
+    modes = {"atomic": ("1", "0", "1", "2"), "slab": ("0", "0", "1", "2"), "decred": ("1", "1", "1", "2"),
+             "unfolded": ("1", "0", "0", "2"), "dct1": ("1", "0", "1", "1")}
     for mode in modes:
         for use_graph in (True, False):
             monkeypatch.setenv("VAEB_ATOMIC_HO", modes[mode][0])
             monkeypatch.setenv("VAEB_ENC_RED", modes[mode][1])
             monkeypatch.setenv("VAEB_FOLD_BWD", modes[mode][2])
+            monkeypatch.setenv("VAEB_DECOUT_CT", modes[mode][3])
             ctx = _lib.Context(cfg.D, cfg.H, cfg.Z, B, L=cfg.L,
                                decoder=_lib.DEC_GAUSSIAN if cfg.continuous else _lib.DEC_BERNOULLI,
                                max_eval_rows=B, use_graph=use_graph)
@@ -410,7 +413,7 @@ def test_atomic_and_slab_handoffs_agree(kw, monkeypatch):
         assert out[mode, True][0] == out[mode, False][0]
         assert np.array_equal(out[mode, True][1], out[mode, False][1])
     es = out["slab", True][0]
-    for mode in ("atomic", "decred", "unfolded"):
+    for mode in ("atomic", "decred", "unfolded", "dct1"):
         ea = out[mode, True][0]
         assert abs(ea - es) <= 1e-5 * abs(es), (mode, ea, es)
         d = np.abs(out[mode, True][1] - out["slab", True][1])
