@@ -86,6 +86,10 @@ CASES = [
     ("bern_LA_L2", dict(D=128, H=64, Z=16, estimator="LA", L=2), 136),
     ("gauss_mean_map", dict(D=128, H=64, Z=8, continuous=True, objective="mean_map"), 128),
     ("synth_shape_small_batch", dict(D=4096, H=2048, Z=128), 128),
+    # Z % 128 == 0, LB, L = 1: heads and dz run on the thin kernels with the latent block
+    # fused (thin_bf16.hpp); row tails of the 64- / 32-row blocks, a K tail (H % 32 != 0)
+    ("thin_tails", dict(D=264, H=200, Z=128), 200),
+    ("thin_gauss_mean_map", dict(D=128, H=64, Z=256, continuous=True, objective="mean_map"), 96),
     # long-K weight gradients (K = L * B >= 1024) with row / column / K tails
     ("bern_LB_longk", dict(D=512, H=256, Z=32), 1024),
     ("gauss_LA_L2_longk", dict(D=256, H=256, Z=16, continuous=True, estimator="LA", L=2), 1024),
@@ -308,6 +312,38 @@ def test_bf16_forked_and_single_stream_steps_agree(monkeypatch):
     f, u = out["1", True], out["0", True]
     assert abs(f[0] - u[0]) <= 1e-6 * abs(u[0])
     assert np.abs(f[1] - u[1]).max() <= 1e-6 and np.abs(f[2] - u[2]).max() <= 1e-6 * max(1.0, np.abs(u[2]).max())
+
+
+def test_bf16_thin_and_split_k_latent_agree(monkeypatch):
+    """The fused thin launches (VAEB_BF_THIN=1 default: heads + latent forward and dz +
+    latent backward each one full-K block per 64 / 32 rows) against the split-K slab
+    products + latent kernels (=0), 6 Philox steps at Z = 128: the same sums in a different
+    fp32 order, so the ELBO agrees to 1e-5 and the parameters to a few Adagrad steps where
+    a bf16 rounding of z or [dMu | dLv] flips; graph replay and eager launches agree bitwise."""
+    from vaeb_amd import _lib
+    cfg = O.Config(D=512, H=256, Z=128)
+    B = 512
+    x = (np.random.default_rng(6).random((6 * B, cfg.D)) < 0.4).astype(np.float32)
+    order = np.array([3, 1, 4, 1, 5, 0], np.int32)
+    out = {}
+    for thin in ("1", "0"):
+        for use_graph in (True, False):
+            monkeypatch.setenv("VAEB_BF_THIN", thin)
+            ctx = _lib.Context(cfg.D, cfg.H, cfg.Z, B, max_eval_rows=B, dtype=_lib.DTYPE_BF16, use_graph=use_graph)
+            ctx.set_data(x)
+            ctx.set_params(O.flatten(O.init_params(cfg)))
+            ctx.set_eps_mode(_lib.EPS_PHILOX, 10)
+            ctx.set_step(0)
+            ctx.update_many(order)
+            s_, n_ = ctx.epoch_elbo()
+            out[thin, use_graph] = (s_ / n_, ctx.get_params())
+            ctx.close()
+    for thin in ("1", "0"):
+        a, b = out[thin, True], out[thin, False]
+        assert a[0] == b[0] and np.array_equal(a[1], b[1])
+    t, u = out["1", True], out["0", True]
+    assert abs(t[0] - u[0]) <= 1e-5 * abs(u[0]), (t[0], u[0])
+    assert np.abs(t[1] - u[1]).max() <= 2 * len(order) * cfg.lr
 
 
 def test_bf16_gemm8_step_matches_ring_step(monkeypatch):

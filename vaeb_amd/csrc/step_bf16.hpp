@@ -608,6 +608,10 @@ struct BfState {
     float *mu = nullptr, *lv = nullptr, *eps = nullptr;
     double* elbo_parts = nullptr;      // [kElboBlocks][2] stage-1 ELBO sums
     int ks_heads = 1, ks_dz = 1, ks_w1 = 1, ks_w45 = 1;
+    // latent-width products with the latent block fused into their epilogues (thin_bf16.hpp;
+    // LB, L = 1, Z % 128 == 0): no split-K slabs; nkl KL partials per row (Z / 64)
+    bool thin = false;
+    int nkl = 1;
     ShadowMap smap{};
 };
 
