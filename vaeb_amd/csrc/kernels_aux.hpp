@@ -227,6 +227,12 @@ DEV float opt_rule(const OptArgs& o, float th, float& acc, float dsg) {
 // reads over the banks), then wave w computes rows 16w..16w+15 x 64 columns
 // (4 accumulators sharing one A fragment).  The epilogue applies prior + Adagrad
 // (theta / acc prefetched before the panels) or stores the gradient (DP / introspection).
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+#ifdef VAEB_NO_TV
+constexpr bool kNoTV = true;    // A/B build: the MFMA-layout epilogue (four 4-byte accesses per value group)
+#else
+constexpr bool kNoTV = false;
+#endif
 constexpr int kWT = 64;   // weight rows (i) per tile; the columns per tile are 16 * TS (wgrad_body)
 constexpr int kWKB = 128;
 constexpr int kWP = 68;
@@ -377,13 +383,40 @@ DEV void wgrad_body(const WA& p, const WGroup& g, int bid, float (*sa)[kWP], flo
     const int li = lane & 15, q = lane >> 4;
     const int NT = g.N0 + g.N1;
 
-    // ---- prefetch theta / acc of this lane's 16 outputs (rows i0+16w+4q+r, cols j0+16t+li)
+    // ---- prefetch theta / acc of this lane's outputs.  TV (VEC -- the host also checked that
+    // every group's arena offsets and widths are multiples of 4 -- and TS >= 2): the epilogue owns, per lane, four
+    // consecutive columns j0 + 16 t + 4 (lane & 3) .. + 3 of row i0 + 16 w + (lane >> 2) -- the
+    // accumulators are transposed through LDS -- so theta, the Adagrad state and the outputs
+    // move as 16-byte accesses (one vector-memory instruction instead of four).  Else rows
+    // i0 + 16 w + 4 q + r, column j0 + 16 t + li: the MFMA layout itself.
     const bool upd = p.opt.update != 0;
     const rsrc_t bth = mkbuf(p.opt.theta_in, p.P * 4), bac = mkbuf(p.opt.acc, p.P * 4);
     uint32_t off[kWTS][4];
     float th[kWTS][4], ac[kWTS][4];
+    uint32_t off4[kWTS];
+    f32x4 th4[kWTS], ac4[kWTS];
+    // (measured on the 32-wide dW2 tiles of the dhd launch 11.95 -> 11.37 us; on the 16-wide
+    // tiles of the last launch 9.77 -> 10.0 us, so those keep the MFMA layout)
+    constexpr bool TV = VEC && !kNoTV && kWTS >= 2;
+    if constexpr (TV) {
 #pragma unroll
-    for (int t = 0; t < kWTS; ++t) {
+        for (int t = 0; t < kWTS; ++t) {
+            const int j = j0 + 16 * t + 4 * (lane & 3);
+            const bool s1 = j >= g.N0;
+            const int jj = s1 ? j - g.N0 : j;
+            const int nrow = s1 ? g.N1 : g.N0;
+            const int i = i0 + 16 * wave + (lane >> 2);
+            const bool ok = j < NT && i <= g.rowsW;
+            const int64_t idx = (i < g.rowsW) ? (s1 ? g.offW1 : g.offW0) + (int64_t)i * nrow + jj
+                                              : (s1 ? g.offb1 : g.offb0) + jj;
+            off4[t] = ok ? (uint32_t)idx * 4u : kOOB;
+            const uint32_t lo = (upd && kh == 0) ? off4[t] : kOOB;
+            th4[t] = bld4(bth, lo);
+            ac4[t] = bld4(bac, lo);
+        }
+    }
+#pragma unroll
+    for (int t = 0; t < (TV ? 0 : kWTS); ++t) {
         const int j = j0 + 16 * t + li;
         const bool s1 = j >= g.N0;
         const int jj = s1 ? j - g.N0 : j;
@@ -505,6 +538,37 @@ DEV void wgrad_body(const WA& p, const WGroup& g, int bid, float (*sa)[kWP], flo
 
     // ---- epilogue: out-of-range byte offsets make masked buffer stores no-ops
     const rsrc_t bto = mkbuf(p.opt.theta_out, p.P * 4), bgr = mkbuf(p.opt.grad, p.P * 4);
+    if constexpr (TV) {
+        // transpose the wave's 16 x 16 TS accumulator block through its own LDS region (sb is
+        // free: the last stage's barrier retired every panel read; a wave reads only what it
+        // wrote, in order)
+        constexpr int TP = 16 * kWTS + 1;
+        float* tl = &sb[0][0] + wave * 16 * TP;
+#pragma unroll
+        for (int t = 0; t < kWTS; ++t)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) tl[(4 * q + r) * TP + 16 * t + li] = acc[t][r];
+#pragma unroll
+        for (int t = 0; t < kWTS; ++t) {
+            f32x4 gv, nt4, a4 = ac4[t];
+#pragma unroll
+            for (int c = 0; c < 4; ++c) gv[c] = tl[(lane >> 2) * TP + 16 * t + 4 * (lane & 3) + c];
+            if (p.opt.store_grad)
+                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, gv), bgr, off4[t], 0, 0);
+            if (upd) {
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    float a2 = a4[c];
+                    nt4[c] = opt_rule(p.opt, th4[t][c], a2, gv[c]);
+                    a4[c] = a2;
+                }
+                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, a4), bac, off4[t], 0, kStWT);
+                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, nt4), bto, off4[t], 0, kStWT);
+            }
+        }
+        if (VAEB_DBG_ON(p.dbg) && threadIdx.x == 0) p.dbg[bid * 8 + 3] = __builtin_amdgcn_s_memrealtime();
+        return;
+    }
 #pragma unroll
     for (int t = 0; t < kWTS; ++t)
 #pragma unroll
@@ -647,7 +711,6 @@ DEV float fvs_zeta(int64_t i, const float* zin, uint64_t seed, int64_t step) {
 // go to threads 0..2 of block 0.  kFvGrid x 256 threads x U x 4 elements cover MNIST's
 // 0.8 M parameters in one round trip.
 DEV void fv_group(int64_t g, int64_t n4, uint32_t& off) { off = g < n4 ? (uint32_t)(g * 16) : kOOB; }
-typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
 // 16-byte stores of the FV / FVS parameter streams: written through like bst_opt (FV step
 // 28.6 -> 28.2 us, fvs_update 9.4 -> 8.0 us)
 DEV void bst4(rsrc_t b, uint32_t off, f32x4 v) {

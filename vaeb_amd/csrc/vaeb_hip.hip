@@ -511,9 +511,12 @@ int prep_wgrad(vaeb_ctx* c, const WGroup* groups, int n, const OptArgs& opt, con
     auto al = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
     for (int gi = 0; gi < n; ++gi) {
         const WGroup& G = w.g[gi];
+        // (and 16-byte theta / Adagrad-state accesses in the epilogue: arena offsets % 4 == 0)
         const bool gv = (G.ld_at % 4 == 0) && (G.rowsW % 4 == 0) && (G.at_is_x ? al(a.xbase) : al(G.at)) &&
-                        (G.ld0 % 4 == 0) && (G.N0 % 4 == 0) && al(G.b0) &&
-                        (G.N1 == 0 || ((G.ld1 % 4 == 0) && (G.N1 % 4 == 0) && al(G.b1)));
+                        (G.ld0 % 4 == 0) && (G.N0 % 4 == 0) && al(G.b0) && G.offW0 % 4 == 0 && G.offb0 % 4 == 0 &&
+                        (G.N1 == 0 || ((G.ld1 % 4 == 0) && (G.N1 % 4 == 0) && al(G.b1) && G.offW1 % 4 == 0 &&
+                                       G.offb1 % 4 == 0)) &&
+                        al(c->theta2[0]) && al(c->theta2[1]) && al(c->acc) && al(c->grad);
         vec = vec && gv;
         if (vmask && gv) *vmask |= 1 << gi;
     }
