@@ -156,6 +156,7 @@ struct vaeb_ctx {
     bool dp_overlap = false;      // bucket A on s2 (bf16 engine; VAEB_DP_OVERLAP=0/1 overrides)
     bool fold_bwd = true;         // Z <= 32: latent backward folded into the dhd launch (VAEB_FOLD_BWD=0: P67)
     int atomic_ho = 1;            // folded latent hand-offs: 1 by fan-in (ho_mode), 0 slabs
+    bool graph_upload = true;     // hipGraphUpload at capture (VAEB_GRAPH_UPLOAD=0: at first launch)
     int decout_ct = -1;           // Bernoulli decoder column tiles per workgroup: -1 auto (2), VAEB_DECOUT_CT=1
     int enc_red = -1;             // encoder slabs summed by the decoder launch: -1 auto, VAEB_ENC_RED=0|1
     // profiling
@@ -854,6 +855,9 @@ int capture(vaeb_ctx* c, int nsteps, int par, hipGraphExec_t* out) {
     e = hipGraphInstantiate(out, gr, nullptr, nullptr, 0);
     hipGraphDestroy(gr);
     if (e != hipSuccess) return fail(VAEB_ERR_HIP, "hipGraphInstantiate: %s", hipGetErrorString(e));
+    // upload now, with the capture: a graph's first launch otherwise pays it inside the call
+    // that replays it (the driver's 20-step form replays a graph the warm-up never launched)
+    if (c->graph_upload && hipGraphUpload(*out, c->s) != hipSuccess) (void)hipGetLastError();
     return 0;
 }
 
@@ -989,6 +993,7 @@ int vaeb_create(const vaeb_config* cfg, vaeb_ctx** out) {
     if (const char* ah = getenv("VAEB_ATOMIC_HO")) c->atomic_ho = atoi(ah) != 0 ? 1 : 0;
     if (const char* er = getenv("VAEB_ENC_RED")) c->enc_red = atoi(er) != 0 ? 1 : 0;
     if (const char* dc = getenv("VAEB_DECOUT_CT")) c->decout_ct = atoi(dc) == 1 ? 1 : 2;
+    if (const char* gu = getenv("VAEB_GRAPH_UPLOAD")) c->graph_upload = atoi(gu) != 0;
     {
         const char* g8 = getenv("VAEB_BF_GEMM8");
         // default: the 8-phase loop for KC x KC (dhd) and KC x KO (enc, dechid); KO x KO (the
