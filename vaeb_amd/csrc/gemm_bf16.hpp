@@ -463,6 +463,16 @@ struct EpiF32 {
 };
 
 // v = act(acc + bias[col]) stored as bf16 (via the LDS tile, 16-B stores).
+// tanh for a bf16 result: 1 - 2 / (1 + e^{2x}) for |x| >= 2^-6 (absolute error ~1e-7, far
+// below the bf16 spacing), x itself below (|tanh x - x| < x^3 / 3: relative 8e-5 at 2^-6,
+// 1/100 of a bf16 ulp) -- two transcendentals and five simple ops, against ftanh's eleven
+// (ftanh keeps fp32 accuracy near 0 for the fp32 engine).  The encoder's and dechid's tanh
+// epilogues cost ~9 and ~7 us of config 5's step (timing-only build without them).
+DEV float ftanh_bf(float x) {
+    const float t = 1.f - 2.f * __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(x * (2.f * kLog2e)));
+    return __builtin_fabsf(x) < 0.015625f ? x : t;
+}
+
 struct EpiBiasAct {
     static constexpr bool kIn = false, kOut = true;
     const float* bias; int tanh_act; int M, N;
@@ -480,7 +490,9 @@ struct EpiBiasAct {
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     float v = acc[i][j][r] + b;
-                    if (tanh_act) v = ftanh(v);
+#ifndef VAEB_DBG_NO_TANH   // (timing-only build: the epilogue without its activation)
+                    if (tanh_act) v = ftanh_bf(v);
+#endif
                     lds_st_bf<W>(smem, erow(lr0, i, r, lane), ecol<CM>(lc0, j, lane), v);
                 }
         }
