@@ -315,9 +315,9 @@ def test_bf16_forked_and_single_stream_steps_agree(monkeypatch):
 
 
 def test_bf16_thin_and_split_k_latent_agree(monkeypatch):
-    """The fused thin launches (VAEB_BF_THIN=1 default: heads + latent forward and dz +
+    """The fused thin launches (VAEB_BF_THIN=3 default: heads + latent forward and dz +
     latent backward each one full-K block per 64 / 32 rows) against the split-K slab
-    products + latent kernels (=0), 6 Philox steps at Z = 128: the same sums in a different
+    products + latent kernels (=0; =2: dz only), 6 Philox steps at Z = 128: the same sums in a different
     fp32 order, so the ELBO agrees to 1e-5 and the parameters to a few Adagrad steps where
     a bf16 rounding of z or [dMu | dLv] flips; graph replay and eager launches agree bitwise."""
     from vaeb_amd import _lib
@@ -326,7 +326,7 @@ def test_bf16_thin_and_split_k_latent_agree(monkeypatch):
     x = (np.random.default_rng(6).random((6 * B, cfg.D)) < 0.4).astype(np.float32)
     order = np.array([3, 1, 4, 1, 5, 0], np.int32)
     out = {}
-    for thin in ("1", "0"):
+    for thin in ("3", "2", "0"):   # mask: 1 heads, 2 dz on the thin launches
         for use_graph in (True, False):
             monkeypatch.setenv("VAEB_BF_THIN", thin)
             ctx = _lib.Context(cfg.D, cfg.H, cfg.Z, B, max_eval_rows=B, dtype=_lib.DTYPE_BF16, use_graph=use_graph)
@@ -338,12 +338,14 @@ def test_bf16_thin_and_split_k_latent_agree(monkeypatch):
             s_, n_ = ctx.epoch_elbo()
             out[thin, use_graph] = (s_ / n_, ctx.get_params())
             ctx.close()
-    for thin in ("1", "0"):
+    for thin in ("3", "2", "0"):
         a, b = out[thin, True], out[thin, False]
         assert a[0] == b[0] and np.array_equal(a[1], b[1])
-    t, u = out["1", True], out["0", True]
-    assert abs(t[0] - u[0]) <= 1e-5 * abs(u[0]), (t[0], u[0])
-    assert np.abs(t[1] - u[1]).max() <= 2 * len(order) * cfg.lr
+    u = out["0", True]
+    for thin in ("3", "2"):
+        t = out[thin, True]
+        assert abs(t[0] - u[0]) <= 1e-5 * abs(u[0]), (thin, t[0], u[0])
+        assert np.abs(t[1] - u[1]).max() <= 2 * len(order) * cfg.lr
 
 
 def test_bf16_gemm8_step_matches_ring_step(monkeypatch):

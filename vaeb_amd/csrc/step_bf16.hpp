@@ -610,7 +610,7 @@ struct BfState {
     int ks_heads = 1, ks_dz = 1, ks_w1 = 1, ks_w45 = 1;
     // latent-width products with the latent block fused into their epilogues (thin_bf16.hpp;
     // LB, L = 1, Z % 128 == 0): no split-K slabs; nkl KL partials per row (Z / 64)
-    bool thin = false;
+    bool thin_h = false, thin_z = false;   // heads / dz on the thin launches
     int nkl = 1;
     ShadowMap smap{};
 };

@@ -149,7 +149,7 @@ struct vaeb_ctx {
     int rank = 0, world = 1;
     hipStream_t s3 = nullptr;     // bf16 engine: dW2 (| dW6) + Adagrad forked beside the backward chain
     hipEvent_t fk_ev[4] = {};     // fork after dhd, s3's work done, [dMu | dLv] ready, ELBO partials
-    bool bf_thin = true;          // VAEB_BF_THIN=0: split-K heads / dz + latent kernels instead of thin_bf16.hpp
+    int bf_thin = 3;              // VAEB_BF_THIN mask: 1 heads, 2 dz on thin_bf16.hpp (0: split-K + latent kernels)
     bool bf_fork = true;          // VAEB_BF_FORK=0: dW2 in the dhd grid (bf_fuse) or after it
     hipStream_t s2 = nullptr;     // DP: the gradient buckets' all-reduces and their Adagrad
     hipEvent_t dp_ev[3] = {};     // fork after dW2, bucket A reduced, bucket A updated
@@ -989,7 +989,7 @@ int vaeb_create(const vaeb_config* cfg, vaeb_ctx** out) {
     e = hipStreamCreateWithFlags(&c->s, hipStreamNonBlocking);
     if (const char* fb = getenv("VAEB_FOLD_BWD")) c->fold_bwd = atoi(fb) != 0;
     if (const char* bk = getenv("VAEB_BF_FORK")) c->bf_fork = atoi(bk) != 0;
-    if (const char* bt = getenv("VAEB_BF_THIN")) c->bf_thin = atoi(bt) != 0;
+    if (const char* bt = getenv("VAEB_BF_THIN")) c->bf_thin = atoi(bt) & 3;
     if (const char* ah = getenv("VAEB_ATOMIC_HO")) c->atomic_ho = atoi(ah) != 0 ? 1 : 0;
     if (const char* er = getenv("VAEB_ENC_RED")) c->enc_red = atoi(er) != 0 ? 1 : 0;
     if (const char* dc = getenv("VAEB_DECOUT_CT")) c->decout_ct = atoi(dc) == 1 ? 1 : 2;
