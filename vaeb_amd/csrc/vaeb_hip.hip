@@ -476,7 +476,10 @@ bool dhd_vec(const StepArgs& a) {
 // MNIST-20, 64 -> 32 wide took the dW2 launch 11.7 -> 9.5 us and the dW3 | dW45 launch
 // 10.9 -> 8.1 us; 16 wide takes the latter to 7.5 us but the dW2 launch (beside 224 dhd
 // tiles) back up to 11.1 us.
-constexpr int kWTJ_P5 = 32;    // dW2 (| dW6), beside the dhd tiles
+#ifndef VAEB_WTJ_P5
+#define VAEB_WTJ_P5 32
+#endif
+constexpr int kWTJ_P5 = VAEB_WTJ_P5;    // dW2 (| dW6), beside the dhd tiles
 constexpr int kWTJ_P67 = 16;   // dW1, beside the dz / dh phase
 constexpr int kWTJ_W = 16;     // standalone launches: dW3 | dW45 (+ ELBO), non-fused dW1
 constexpr int kDzSplit = 8;    // P67 column splits per row block (fused.hpp dz_dh_body)
