@@ -480,6 +480,10 @@ bool dhd_vec(const StepArgs& a) {
 #define VAEB_WTJ_P5 32
 #endif
 constexpr int kWTJ_P5 = VAEB_WTJ_P5;    // dW2 (| dW6), beside the dhd tiles
+#ifndef VAEB_W3_TS
+#define VAEB_W3_TS 1
+#endif
+constexpr int kW3TS = VAEB_W3_TS;       // 16-column groups per tile of the last launch (dW3 | dW45 | dW1)
 constexpr int kWTJ_P67 = 16;   // dW1, beside the dz / dh phase
 constexpr int kWTJ_W = 16;     // standalone launches: dW3 | dW45 (+ ELBO), non-fused dW1
 constexpr int kDzSplit = 8;    // P67 column splits per row block (fused.hpp dz_dh_body)
@@ -535,17 +539,18 @@ int launch_wgrad(vaeb_ctx* c, hipStream_t s, const WGroup* groups, int n, const 
     if (da3) {
         if (n != 3) return fail(VAEB_ERR_ARG, "internal: the dA3-forming launch takes three groups");
         WGradArgs3 w;
-        // 16-column tiles (32-wide: MNIST 46.3 vs 44.7 us, Frey 41.5 vs 38.4, removed in round 3)
+        // 16-column tiles (32-wide: MNIST 46.3 vs 44.7 us, Frey 41.5 vs 38.4 in round 2;
+        // -DVAEB_W3_TS=2 builds them for A/B)
         int vm = 0;   // 16-byte panel loads per group (Frey: dW3 yes, dW4 | dW5 and dW1 not)
-        if (int rc = prep_wgrad(c, groups, n, opt, e, a, 0, w, vec, 16, &vm)) return rc;
+        if (int rc = prep_wgrad(c, groups, n, opt, e, a, 0, w, vec, 16 * kW3TS, &vm)) return rc;
         w.da3 = *da3;
         const dim3 grid(w.total_wgs + (e ? 1 : 0));
         switch (vm) {
-            case 7: hipLaunchKernelGGL((wgrad3_kernel<7, 1>), grid, dim3(256), 0, s, w); break;
-            case 1: hipLaunchKernelGGL((wgrad3_kernel<1, 1>), grid, dim3(256), 0, s, w); break;
-            case 3: hipLaunchKernelGGL((wgrad3_kernel<3, 1>), grid, dim3(256), 0, s, w); break;
-            case 5: hipLaunchKernelGGL((wgrad3_kernel<5, 1>), grid, dim3(256), 0, s, w); break;
-            default: hipLaunchKernelGGL((wgrad3_kernel<0, 1>), grid, dim3(256), 0, s, w); break;
+            case 7: hipLaunchKernelGGL((wgrad3_kernel<7, kW3TS>), grid, dim3(256), 0, s, w); break;
+            case 1: hipLaunchKernelGGL((wgrad3_kernel<1, kW3TS>), grid, dim3(256), 0, s, w); break;
+            case 3: hipLaunchKernelGGL((wgrad3_kernel<3, kW3TS>), grid, dim3(256), 0, s, w); break;
+            case 5: hipLaunchKernelGGL((wgrad3_kernel<5, kW3TS>), grid, dim3(256), 0, s, w); break;
+            default: hipLaunchKernelGGL((wgrad3_kernel<0, kW3TS>), grid, dim3(256), 0, s, w); break;
         }
     } else {
         WGradArgs w;
