@@ -379,7 +379,8 @@ def test_atomic_and_slab_handoffs_agree(kw, monkeypatch):
     (VAEB_ATOMIC_HO=1: counted fixed-point atomics up to fan-in 16, slabs above), slabs +
     ticket + reducer everywhere (=0), the encoder slabs summed by the decoder launch
     (VAEB_ENC_RED=1), the unfolded latent backward (VAEB_FOLD_BWD=0: the P67 launches) and
-    one 16-column tile per Bernoulli decoder workgroup (VAEB_DECOUT_CT=1).
+    one 16-column tile per Bernoulli decoder workgroup (VAEB_DECOUT_CT=1) and the slab-only
+    encoder on 512-thread workgroups (VAEB_ENC16=0).
     They sum the same partials in different arithmetic (exact integer vs ordered fp32), so
     they agree to rounding, and each is bitwise deterministic (graph == eager)."""
     from vaeb_amd import _lib
@@ -390,14 +391,16 @@ def test_atomic_and_slab_handoffs_agree(kw, monkeypatch):
     out = {}
     # "decred": VAEB_ENC_RED=1, the encoder's slabs summed by every decoder workgroup;
     # "dct1": one 16-column tile per Bernoulli decoder workgroup (default two)
-    modes = {"atomic": ("1", "0", "1", "2"), "slab": ("0", "0", "1", "2"), "decred": ("1", "1", "1", "2"),
-             "unfolded": ("1", "0", "0", "2"), "dct1": ("1", "0", "1", "1")}
+    # "enc8": the slab-only encoder on 512-thread workgroups (default 1024, VAEB_ENC16)
+    modes = {"atomic": ("1", "0", "1", "2", "1"), "slab": ("0", "0", "1", "2", "1"), "decred": ("1", "1", "1", "2", "1"),
+             "unfolded": ("1", "0", "0", "2", "1"), "dct1": ("1", "0", "1", "1", "1"), "enc8": ("1", "1", "1", "2", "0")}
     for mode in modes:
         for use_graph in (True, False):
             monkeypatch.setenv("VAEB_ATOMIC_HO", modes[mode][0])
             monkeypatch.setenv("VAEB_ENC_RED", modes[mode][1])
             monkeypatch.setenv("VAEB_FOLD_BWD", modes[mode][2])
             monkeypatch.setenv("VAEB_DECOUT_CT", modes[mode][3])
+            monkeypatch.setenv("VAEB_ENC16", modes[mode][4])
             ctx = _lib.Context(cfg.D, cfg.H, cfg.Z, B, L=cfg.L,
                                decoder=_lib.DEC_GAUSSIAN if cfg.continuous else _lib.DEC_BERNOULLI,
                                max_eval_rows=B, use_graph=use_graph)
@@ -413,12 +416,17 @@ def test_atomic_and_slab_handoffs_agree(kw, monkeypatch):
         assert out[mode, True][0] == out[mode, False][0]
         assert np.array_equal(out[mode, True][1], out[mode, False][1])
     es = out["slab", True][0]
-    for mode in ("atomic", "decred", "unfolded", "dct1"):
+    frac = {}
+    for mode in ("atomic", "decred", "unfolded", "dct1", "enc8"):
         ea = out[mode, True][0]
         assert abs(ea - es) <= 1e-5 * abs(es), (mode, ea, es)
         d = np.abs(out[mode, True][1] - out["slab", True][1])
-        assert d.max() <= 2 * len(order) * cfg.lr          # a ~lr sign(g) step may flip where |g| ~ 1e-7
-        assert float((d > 1e-3 * cfg.lr).mean()) <= 1e-3
+        assert d.max() <= 2 * len(order) * cfg.lr, mode    # a ~lr sign(g) step may flip where |g| ~ 1e-7
+        frac[mode] = float((d > 1e-3 * cfg.lr).mean())
+    # Parameters whose gradient is a cancellation-dominated sum (|g| near rounding of its terms)
+    # take Adagrad steps that follow that rounding; a different K split of the encoder (enc8:
+    # 8 instead of 16 partials) moves ~0.13 % of MNIST's parameters by more than 1e-3 lr.
+    assert max(frac.values()) <= 2e-3, frac
 
 
 def test_fixed_point_handoff_overflow_is_reported_not_silent():

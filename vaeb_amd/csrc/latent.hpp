@@ -247,10 +247,13 @@ struct PEncCT : PEnc {
 };
 
 // CT: h column tiles per workgroup (1, or 2: half the contributors per latent element).
-template <int NCT, int GCH, bool FV, int HO, int CT = 1>
+// NWV: waves splitting K (8; or 16 -- 1024-thread workgroups -- on the slab-only path HO = 3,
+// whose epilogue needs no 512-thread layout).
+template <int NCT, int GCH, bool FV, int HO, int CT = 1, int NWV = 8>
 DEV void enc_latent_body(const StepArgs& a, const FvFold& fvf) {
+    static_assert(NWV == 8 || HO == 3, "16 waves: slab-only encoder");
     constexpr bool AT = HO == 1;
-    __shared__ f32x4 red[512 * CT];
+    __shared__ f32x4 red[64 * NWV * CT];
     __shared__ float hs[16][16 * CT + 4];
     __shared__ int sflag;
     __shared__ float pm[HO == 1 ? 64 : 1][17];   // the tile's [mu | lv] partials, [column][row]
@@ -309,19 +312,19 @@ DEV void enc_latent_body(const StepArgs& a, const FvFold& fvf) {
     f32x4 acc[CT];
 #pragma unroll
     for (int c = 0; c < CT; ++c) acc[c] = zero4();
-    wave_mainloop<CT, 8, GCH>(p, m0 + li, n0 + li, p.K, wave, acc);
+    wave_mainloop<CT, NWV, GCH>(p, m0 + li, n0 + li, p.K, wave, acc);
     VAEB_STAMP(a, 1);
     float* redh = reinterpret_cast<float*>(red);   // [c][r][slice][lane]: CT * 2048 floats
 #pragma unroll
     for (int c = 0; c < CT; ++c)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) redh[((c * 4 + r) * 8 + wave) * 64 + lane] = acc[c][r];
+        for (int r = 0; r < 4; ++r) redh[((c * 4 + r) * NWV + wave) * 64 + lane] = acc[c][r];
     __syncthreads();
     if (a.order && bx == 0 && by == 0 && threadIdx.x == 0) *a.cur_batch = a.cursor[kCtlNext];
     if (wa) {
-        float t = redh[((ca * 4 + ra) * 8) * 64 + lane];
+        float t = redh[((ca * 4 + ra) * NWV) * 64 + lane];
 #pragma unroll
-        for (int sl = 1; sl < 8; ++sl) t += redh[((ca * 4 + ra) * 8 + sl) * 64 + lane];
+        for (int sl = 1; sl < NWV; ++sl) t += redh[((ca * 4 + ra) * NWV + sl) * 64 + lane];
         const int n = n0 + 16 * ca + li, m = m0 + 4 * q + ra;
         const float hv = (m < a.Mb && n < H) ? ftanh(t + pre.b) : 0.f;
         if (n < H) a.h[(int64_t)m * H + n] = hv;
@@ -493,6 +496,11 @@ __global__ __launch_bounds__(512) void enc_latent_kernel(StepArgs a) {
 template <int NCT, int GCH, int HO, int CT>
 __global__ __launch_bounds__(512) void enc_latent_fv_kernel(StepArgs a, FvFold f) {
     enc_latent_body<NCT, GCH, true, HO, CT>(a, f);
+}
+// the slab-only encoder (HO = 3, CT = 2) on 16 waves
+template <int NCT, int GCH>
+__global__ __launch_bounds__(1024) void enc_latent16_kernel(StepArgs a) {
+    enc_latent_body<NCT, GCH, false, 3, 2, 16>(a, FvFold{});
 }
 
 // ----------------------------------------------------------------------------- P4'
