@@ -379,8 +379,8 @@ def test_atomic_and_slab_handoffs_agree(kw, monkeypatch):
     (VAEB_ATOMIC_HO=1: counted fixed-point atomics up to fan-in 16, slabs above), slabs +
     ticket + reducer everywhere (=0), the encoder slabs summed by the decoder launch
     (VAEB_ENC_RED=1), the unfolded latent backward (VAEB_FOLD_BWD=0: the P67 launches) and
-    one 16-column tile per Bernoulli decoder workgroup (VAEB_DECOUT_CT=1) and the slab-only
-    encoder on 512-thread workgroups (VAEB_ENC16=0).
+    one 16-column tile per Bernoulli decoder workgroup (VAEB_DECOUT_CT=1) and the encoders on
+    512-thread workgroups (VAEB_ENC16=0; =1: the atomic hand-off encoder only).
     They sum the same partials in different arithmetic (exact integer vs ordered fp32), so
     they agree to rounding, and each is bitwise deterministic (graph == eager)."""
     from vaeb_amd import _lib
@@ -391,9 +391,11 @@ def test_atomic_and_slab_handoffs_agree(kw, monkeypatch):
     out = {}
     # "decred": VAEB_ENC_RED=1, the encoder's slabs summed by every decoder workgroup;
     # "dct1": one 16-column tile per Bernoulli decoder workgroup (default two)
-    # "enc8": the slab-only encoder on 512-thread workgroups (default 1024, VAEB_ENC16)
-    modes = {"atomic": ("1", "0", "1", "2", "1"), "slab": ("0", "0", "1", "2", "1"), "decred": ("1", "1", "1", "2", "1"),
-             "unfolded": ("1", "0", "0", "2", "1"), "dct1": ("1", "0", "1", "1", "1"), "enc8": ("1", "1", "1", "2", "0")}
+    # "enc8": no encoder on 1024 threads (VAEB_ENC16=0); "enc16slab": only the slab-only one
+    # (=1; default 2: the atomic hand-off encoder on 1024-thread workgroups too)
+    modes = {"atomic": ("1", "0", "1", "2", "2"), "slab": ("0", "0", "1", "2", "2"), "decred": ("1", "1", "1", "2", "2"),
+             "unfolded": ("1", "0", "0", "2", "2"), "dct1": ("1", "0", "1", "1", "2"), "enc8": ("1", "1", "1", "2", "0"),
+             "enc16slab": ("1", "0", "1", "2", "1")}
     for mode in modes:
         for use_graph in (True, False):
             monkeypatch.setenv("VAEB_ATOMIC_HO", modes[mode][0])
@@ -417,7 +419,7 @@ def test_atomic_and_slab_handoffs_agree(kw, monkeypatch):
         assert np.array_equal(out[mode, True][1], out[mode, False][1])
     es = out["slab", True][0]
     frac = {}
-    for mode in ("atomic", "decred", "unfolded", "dct1", "enc8"):
+    for mode in ("atomic", "decred", "unfolded", "dct1", "enc8", "enc16slab"):
         ea = out[mode, True][0]
         assert abs(ea - es) <= 1e-5 * abs(es), (mode, ea, es)
         d = np.abs(out[mode, True][1] - out["slab", True][1])

@@ -155,7 +155,7 @@ DEV uint64_t* fx_at(uint64_t* base, int64_t e) { return base + e * kFxStride; }
 // elements t and t + 512 (NS = 2 slots when Z > 16, then the first is always present), element
 // e = (column e >> 4, row e & 15).  Only the second slot's add sits in a branch, so at most
 // one wait separates the two adds (a branch around every add made hipcc wait for each).
-template <int NS>
+template <int NS, int NTH = 512>
 struct FxSlots {
     uint64_t t[NS];
     bool ok[NS];
@@ -163,7 +163,7 @@ struct FxSlots {
     DEV void add(uint64_t* acc, int64_t row0, int ncol, const float (*pm)[17], int ne) {
 #pragma unroll
         for (int u = 0; u < NS; ++u) {
-            const int e = (int)threadIdx.x + 512 * u;
+            const int e = (int)threadIdx.x + NTH * u;
             ok[u] = e < ne;
             col[u] = ok[u] ? e >> 4 : 0;
             row[u] = e & 15;
@@ -247,12 +247,14 @@ struct PEncCT : PEnc {
 };
 
 // CT: h column tiles per workgroup (1, or 2: half the contributors per latent element).
-// NWV: waves splitting K (8; or 16 -- 1024-thread workgroups -- on the slab-only path HO = 3,
-// whose epilogue needs no 512-thread layout).
+// NWV: waves splitting K (8; or 16 -- 1024-thread workgroups -- on the slab-only path HO = 3
+// and the atomic hand-off HO = 1; the ticketed reducer HO = 0 keeps its 512-thread layout).
 template <int NCT, int GCH, bool FV, int HO, int CT = 1, int NWV = 8>
 DEV void enc_latent_body(const StepArgs& a, const FvFold& fvf) {
-    static_assert(NWV == 8 || HO == 3, "16 waves: slab-only encoder");
+    static_assert(NWV == 8 || (HO != 0 && !FV), "16 waves: no ticketed reducer, no FV stream");
     constexpr bool AT = HO == 1;
+    constexpr int NTH = 64 * NWV;
+    constexpr int NS = NWV == 16 ? 1 : NCT;   // atomic-add slots per thread: 32 Z <= 1024
     __shared__ f32x4 red[64 * NWV * CT];
     __shared__ float hs[16][16 * CT + 4];
     __shared__ int sflag;
@@ -299,12 +301,12 @@ DEV void enc_latent_body(const StepArgs& a, const FvFold& fvf) {
             }
     }
     // AT: the bias of each element this thread may complete (column c: b4[c] | b5[c - Z])
-    float bias[NCT];
+    float bias[NS];
     if constexpr (AT) {
         const rsrc_t b4 = mkbuf(a.b4, (int64_t)Z * 4), b5 = mkbuf(a.b5, (int64_t)Z * 4);
 #pragma unroll
-        for (int u = 0; u < NCT; ++u) {
-            const int e = (int)threadIdx.x + 512 * u, c = e >> 4;
+        for (int u = 0; u < NS; ++u) {
+            const int e = (int)threadIdx.x + NTH * u, c = e >> 4;
             const bool ok = e < 32 * Z;
             bias[u] = bld(b4, ok && c < Z ? (uint32_t)c * 4u : kOOB) + bld(b5, ok && c >= Z ? (uint32_t)(c - Z) * 4u : kOOB);
         }
@@ -370,7 +372,7 @@ DEV void enc_latent_body(const StepArgs& a, const FvFold& fvf) {
     }
     if constexpr (AT) {
         __syncthreads();
-        FxSlots<NCT> fx;
+        FxSlots<NS, NTH> fx;
         fx.add(a.acc_ml, m0, 2 * Z, pm, 32 * Z);
         if (by == 0) {   // the row block's eps, while the adds are in flight
             // the row base comes from `next` (kCtlNext): cur_batch is written by tile (0,0)
@@ -379,7 +381,7 @@ DEV void enc_latent_body(const StepArgs& a, const FvFold& fvf) {
                 (a.order ? (int64_t)ld_launch_const(a.cursor + kCtlNext) * a.row_base_mul : 0) + a.row_base_add;
             const uint64_t c23 = philox_c23(a.step ? *a.step : 0, a.domain);
             const int per = 16 * Z;
-            for (int id = threadIdx.x; id < a.L * per; id += 512) {
+            for (int id = threadIdx.x; id < a.L * per; id += NTH) {
                 const int l = id / per, ml = (id - l * per) / Z, j = id - l * per - ml * Z;
                 const int m = m0 + ml;
                 float e = 0.f;
@@ -391,7 +393,7 @@ DEV void enc_latent_body(const StepArgs& a, const FvFold& fvf) {
             }
         }
 #pragma unroll
-        for (int u = 0; u < NCT; ++u) {
+        for (int u = 0; u < NS; ++u) {
             float v;
             if (fx.ok[u] && fx_done(fx.t[u], nctH, v)) {
                 const int c = fx.col[u], m = m0 + fx.row[u];
@@ -497,10 +499,10 @@ template <int NCT, int GCH, int HO, int CT>
 __global__ __launch_bounds__(512) void enc_latent_fv_kernel(StepArgs a, FvFold f) {
     enc_latent_body<NCT, GCH, true, HO, CT>(a, f);
 }
-// the slab-only encoder (HO = 3, CT = 2) on 16 waves
-template <int NCT, int GCH>
+// the slab-only (HO = 3, CT = 2) and atomic hand-off (HO = 1) encoders on 16 waves
+template <int NCT, int GCH, int HO, int CT>
 __global__ __launch_bounds__(1024) void enc_latent16_kernel(StepArgs a) {
-    enc_latent_body<NCT, GCH, false, 3, 2, 16>(a, FvFold{});
+    enc_latent_body<NCT, GCH, false, HO, CT, 16>(a, FvFold{});
 }
 
 // ----------------------------------------------------------------------------- P4'

@@ -161,6 +161,9 @@ struct vaeb_ctx {
     // flight per CU): MNIST 38.82 -> 37.87 us/step in alternating runs (encoder 7.76 -> 7.22
     // us).  VAEB_ENC16=0: 512 threads.
     bool enc16 = true;
+    // the atomic hand-off encoder (HO 1, fan-in <= 16) on 16 waves too: Frey 29.19 -> 29.01
+    // us/step (encoder 6.98 -> 6.93 us).  VAEB_ENC16=1: the slab-only encoder only.
+    bool enc16_at = true;
     int decout_ct = -1;           // Bernoulli decoder column tiles per workgroup: -1 auto (2), VAEB_DECOUT_CT=1
     int enc_red = -1;             // encoder slabs summed by the decoder launch: -1 auto, VAEB_ENC_RED=0|1
     // profiling
@@ -358,11 +361,12 @@ void launch_enc_latent_ct(hipStream_t s, dim3 g1, const StepArgs& a, const FvFol
     }
 }
 template <int HO>
-void launch_enc_latent(hipStream_t s, dim3 g1, const StepArgs& a, const FvFold& fvf, bool deep, int ct, bool e16) {
+void launch_enc_latent(hipStream_t s, dim3 g1, const StepArgs& a, const FvFold& fvf, bool deep, int ct, bool e16,
+                       bool c16) {
     if constexpr (HO == 3) {   // slabs summed by the decoder launch: CT = 2 only, no FV stream
         if (e16) {   // 1024-thread workgroups, 16 waves splitting K (vaeb_ctx::enc16)
-            if (a.Z <= 16) hipLaunchKernelGGL((enc_latent16_kernel<1, 4>), g1, dim3(1024), 0, s, a);
-            else hipLaunchKernelGGL((enc_latent16_kernel<2, 4>), g1, dim3(1024), 0, s, a);
+            if (a.Z <= 16) hipLaunchKernelGGL((enc_latent16_kernel<1, 4, 3, 2>), g1, dim3(1024), 0, s, a);
+            else hipLaunchKernelGGL((enc_latent16_kernel<2, 4, 3, 2>), g1, dim3(1024), 0, s, a);
             return;
         }
         if (a.Z <= 16) {
@@ -372,6 +376,11 @@ void launch_enc_latent(hipStream_t s, dim3 g1, const StepArgs& a, const FvFold& 
             if (deep) hipLaunchKernelGGL((enc_latent_kernel<2, 8, 3, 2>), g1, dim3(512), 0, s, a);
             else hipLaunchKernelGGL((enc_latent_kernel<2, 4, 3, 2>), g1, dim3(512), 0, s, a);
         }
+        return;
+    }
+    if (HO == 1 && e16 && c16 && fvf.rows == 0 && ct == 1) {   // the atomic hand-off on 16 waves
+        if (a.Z <= 16) hipLaunchKernelGGL((enc_latent16_kernel<1, 4, 1, 1>), g1, dim3(1024), 0, s, a);
+        else hipLaunchKernelGGL((enc_latent16_kernel<2, 4, 1, 1>), g1, dim3(1024), 0, s, a);
         return;
     }
     if (ct == 2) launch_enc_latent_ct<HO, 2>(s, g1, a, fvf, deep);
@@ -406,9 +415,9 @@ int enqueue_forward(vaeb_ctx* c, const StepArgs& a0, Prof& pr, const FvFold& fvf
         const int at = red ? 2 : (ho == 1 ? 1 : 0);
         pr.mark(16);
         REP(pr) {
-            if (ho == 3) launch_enc_latent<3>(s, g1, a, fvf, deep, ct, c->enc16);
-            else if (ho == 1) launch_enc_latent<1>(s, g1, a, fvf, deep, ct, c->enc16);
-            else launch_enc_latent<0>(s, g1, a, fvf, deep, ct, c->enc16);
+            if (ho == 3) launch_enc_latent<3>(s, g1, a, fvf, deep, ct, c->enc16, c->enc16_at);
+            else if (ho == 1) launch_enc_latent<1>(s, g1, a, fvf, deep, ct, c->enc16, c->enc16_at);
+            else launch_enc_latent<0>(s, g1, a, fvf, deep, ct, c->enc16, c->enc16_at);
         }
         CHECK_LAUNCH();
         a.dbg = next_dbg(c);
@@ -1010,7 +1019,10 @@ int vaeb_create(const vaeb_config* cfg, vaeb_ctx** out) {
     if (const char* ah = getenv("VAEB_ATOMIC_HO")) c->atomic_ho = atoi(ah) != 0 ? 1 : 0;
     if (const char* er = getenv("VAEB_ENC_RED")) c->enc_red = atoi(er) != 0 ? 1 : 0;
     if (const char* dc = getenv("VAEB_DECOUT_CT")) c->decout_ct = atoi(dc) == 1 ? 1 : 2;
-    if (const char* e16 = getenv("VAEB_ENC16")) c->enc16 = atoi(e16) != 0;
+    if (const char* e16 = getenv("VAEB_ENC16")) {
+        c->enc16 = atoi(e16) != 0;
+        c->enc16_at = atoi(e16) >= 2;
+    }
     if (const char* gu = getenv("VAEB_GRAPH_UPLOAD")) c->graph_upload = atoi(gu) != 0;
     {
         const char* g8 = getenv("VAEB_BF_GEMM8");
