@@ -265,41 +265,10 @@ CONFIGS = {
 }
 
 
-def free_port():
-    import socket
-    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as so:
-        so.bind(("127.0.0.1", 0))
-        return so.getsockname()[1]
-
-
 def spawn_ranks(n, argv, poll_s=0.2, script=None):
-    """`bench.py --gpus N` without a launcher: start N rank processes of this script (one
-    per GPU, RANK = LOCAL_RANK = r, WORLD_SIZE = N, rendezvous on 127.0.0.1) and wait.
-    The parent makes no GPU call.  If one rank fails the others are stopped (they would
-    wait in a collective forever); returns the first non-zero exit code, else 0."""
-    import subprocess
-    port = free_port()
-    procs = []
-    for r in range(n):
-        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
-                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-        procs.append(subprocess.Popen([sys.executable, script or os.path.abspath(__file__)] + list(argv), env=env))
-    rc = 0
-    while True:
-        codes = [p.poll() for p in procs]
-        bad = [c for c in codes if c not in (None, 0)]
-        if bad:
-            rc = bad[0]
-            for p in procs:
-                if p.poll() is None:
-                    p.kill()
-            for p in procs:
-                p.wait()
-            return rc
-        if all(c == 0 for c in codes):
-            return 0
-        time.sleep(poll_s)
+    """`bench.py --gpus N` without a launcher: N rank processes of this script (vaeb_amd.dp)."""
+    from vaeb_amd.dp import spawn_ranks as _spawn
+    return _spawn(n, [sys.executable, script or os.path.abspath(__file__)] + list(argv), poll_s=poll_s)
 
 
 def make_context(C, D, H, Z, B, Bg, row_off, local, args, gauss, bf16, dist, rank, world):
@@ -312,12 +281,10 @@ def make_context(C, D, H, Z, B, Bg, row_off, local, args, gauss, bf16, dist, ran
                        use_graph=not args.no_graph, max_eval_rows=B if bf16 else 1000,
                        dtype=_lib.DTYPE_BF16 if bf16 else _lib.DTYPE_F32)
     if world > 1:
-        uid = [_lib.Context.comm_unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(uid, src=0)
-        ctx.comm_init(uid[0], rank, world)
-        n = ctx.comm_count()
-        if n != world or n != args.gpus:
-            raise SystemExit(f"rank {rank}: the RCCL communicator holds {n} ranks, expected {args.gpus}")
+        from vaeb_amd.dp import comm_setup
+        comm_setup(ctx, dist, rank, world)
+        if world != args.gpus:
+            raise SystemExit(f"rank {rank}: the RCCL communicator holds {world} ranks, expected {args.gpus}")
     return ctx
 
 

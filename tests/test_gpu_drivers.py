@@ -67,6 +67,39 @@ def test_reconstruction_driver_matches_reference_images(tmp_path):
             assert np.abs(orig - f[f"x_orig_z{z}"]).mean() <= 0.02
 
 
+def test_reconstruction_driver_bernoulli_models_with_mnist_split_data(tmp_path):
+    """VAEB.load of a Bernoulli (MNIST) model takes the data as VAEB.py:237-239
+    returns it -- ((x, y) train, valid, test) -- whose first element is a ragged pair.
+    reconstruction.main loads the discrete models first; each must load, reconstruct and
+    log its two MSE lines, the mean reconstruction equal to the oracle's decoder mean."""
+    from vaeb_amd import reconstruction as R
+    from vaeb_amd.model import VAEB
+    os.makedirs(tmp_path / "reconstruction_res")
+    x = O.synthetic_mnist(n=400, seed=3)
+    lab = np.zeros(100, np.int64)
+    data = ((x[:200], np.zeros(200, np.int64)), (x[200:300], lab), (x[300:], lab))
+    thetas = {}
+    for z in (2, 10, 20):
+        cfg = O.Config(D=784, H=500, Z=z)
+        rng = np.random.default_rng(z)   # away from the near-constant initial decoder
+        thetas[z] = [(a + rng.normal(0, 0.1, a.shape)).astype(np.float32) for a in O.init_params(cfg)]
+        m = VAEB(x[:200], False, 500, z, 100, 1, 0.01, False, False, params=thetas[z])
+        m.save(str(tmp_path / "reconstruction_res" / f"discrete_{z}.mdl"))
+        m.close()
+    res = R.main(root=str(tmp_path), data={"discrete": data}, data_types=("discrete",))
+    lines = open(tmp_path / "reconstruction_res" / "MSE.res").read().splitlines()
+    assert [l.split(",")[:3] for l in lines[1:]] == [["discrete", str(z), t] for z in (2, 10, 20)
+                                                     for t in ("mean", "sample")]
+    for z in (2, 10, 20):
+        cfg = O.Config(D=784, H=500, Z=z)
+        y, _ = O.reconstruct_full([p.astype(np.float64) for p in thetas[z]], x[300:].astype(np.float64), None, cfg)
+        want = float(np.mean(np.linalg.norm(y - x[300:], axis=1) ** 2))
+        assert abs(res[("discrete", z)][0] - want) <= 1e-4 * want, (z, res[("discrete", z)][0], want)
+        model, d = VAEB.load(str(tmp_path / "reconstruction_res" / f"discrete_{z}.mdl"), data=data)
+        assert model.N == 200 and d is data
+        model.close()
+
+
 def test_freyface_driver_matches_reference_faces(tmp_path, monkeypatch):
     from vaeb_amd import freyface
     m = np.load(os.path.join(GOLD, "frey_manifold.npz"))

@@ -467,4 +467,49 @@ def test_fixed_point_handoff_overflow_is_reported_not_silent():
         v = ctx.update(0)
         assert np.isfinite(v) and abs(v - good) < 0.05 * abs(good)
         assert ctx.epoch_elbo()[1] >= 1
+    # the BACKWARD hand-off alone (its guard word is blk[kBlkFxErr] too, not a
+    # padding word of the forward accumulators): encoder weights sane, the decoder's W6
+    # NaN or W2 huge, so only the dZ partials leave the range
+    for poison in ("w6_nan", "w2_huge"):
+        bad = theta0.copy()
+        if poison == "w6_nan":
+            bad[sl[5].ravel()] = np.nan
+        else:
+            bad[sl[4].ravel()] = 1e5
+        ctx.set_params(bad)
+        with pytest.raises(_lib.VaebError, match="fixed-point"):
+            ctx.update(1)
+        assert np.all(np.isfinite(ctx.activation("mu", 100 * 2)))   # the forward hand-off stayed in range
+        ctx.set_params(theta0)
+        ctx.set_adagrad_state(np.zeros_like(theta0))
+        v = ctx.update(0)
+        assert np.isfinite(v) and abs(v - good) < 0.05 * abs(good)
     ctx.close()
+
+
+def test_update_after_async_steps_returns_its_own_value():
+    """vaeb_update reads the mapped result slot the step's last kernel writes; steps
+    still queued from update_many / update_async would write it too.  update(j) right after
+    update_async(i) must return update(j)'s own value, as a fully synchronised run does."""
+    from vaeb_amd import _lib
+    cfg = O.Config(D=784, H=500, Z=20)
+    x = O.synthetic_mnist(n=800)
+    theta0 = O.flatten(O.init_params(cfg))
+
+    def run(sync):
+        ctx = _lib.Context(784, 500, 20, 100, max_eval_rows=100)
+        ctx.set_data(x)
+        ctx.set_params(theta0)
+        ctx.set_eps_mode(_lib.EPS_PHILOX, 10)
+        out = []
+        for i in range(3):
+            ctx.update_async(i)
+            ctx.update_many(np.array([3, 4, 5], np.int32))
+            if sync:
+                ctx.synchronize()
+            out.append(ctx.update(6 + i % 2))
+        ctx.epoch_elbo()
+        ctx.close()
+        return out
+
+    assert run(False) == run(True)

@@ -283,6 +283,10 @@ class Context:
         check(self.lib.vaeb_update(self.h, int(index), ctypes.byref(out)))
         return out.value
 
+    def update_async(self, index):
+        """One step enqueued without waiting (its value joins the epoch sums)."""
+        check(self.lib.vaeb_update_async(self.h, int(index)))
+
     def update_many(self, indices):
         idx = np.ascontiguousarray(indices, np.int32)
         check(self.lib.vaeb_update_many(self.h, idx.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), idx.size))

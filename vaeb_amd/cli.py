@@ -5,7 +5,17 @@ Same `command_line_args` / `command_line_flags` dicts (including the misspelt
 `full_varational`), the same `--name value` / `--flag` parsing with a warning (not an
 error) for unused arguments, the same stdout lines and trace CSV.  Keys ADDED (never
 renamed): device, rng, objective, max_eval_rows, trace_dedup, fv_sample, state_file,
-resume_file (args) and synthetic (flag).
+resume_file, world_size, dp_scaling, dtype (args) and synthetic (flag).
+
+Data parallelism: `--world_size N` runs N ranks, one process per GPU.
+Without a launcher the CLI starts them itself (`python -m vaeb_amd ...` per rank, RANK /
+LOCAL_RANK / WORLD_SIZE in the environment, before any GPU call); under torch.distributed.run
+the launcher's WORLD_SIZE is used.  Each rank takes its share of every minibatch
+(dp_scaling strong: the reference's batch_size split over the ranks, so the steps are the
+reference's; weak: batch_size rows per rank), the gradient is all-reduced over RCCL inside
+the library, validation is sharded and summed, and only rank 0 prints, traces and saves.
+`--dtype` chooses the engine the reference chose with THEANO_FLAGS floatX
+(run_on_gpu.sh:2): float32 (default) or bf16.
 """
 from __future__ import annotations
 
@@ -16,6 +26,8 @@ import sys
 import time
 
 import numpy as np
+
+from . import dp
 
 #   to add another command line argument, add its name as a key and a tuple of its
 #   default value and type as the value (VAEB.py:22-36)
@@ -39,7 +51,11 @@ command_line_args = {'seed': (15485863, int),
                      'fv_sample': (0, int),         # 1 (with --full_varational): weight-posterior sample
                                                     # theta~ = mu + |sigma| zeta (VAEB.py:127-129; extension)
                      'state_file': ('', str),       # native checkpoint (theta + Adagrad + RNG) written at the end
-                     'resume_file': ('', str)}      # native checkpoint to resume from
+                     'resume_file': ('', str),      # native checkpoint to resume from
+                     'world_size': (0, int),        # data-parallel ranks (0: one GPU, no communicator;
+                                                    # N >= 1: N ranks with the RCCL all-reduce step)
+                     'dp_scaling': ('strong', str), # strong: batch_size split over the ranks; weak: per rank
+                     'dtype': ('float32', str)}     # float32 (floatX, run_on_gpu.sh:2) | bf16
 #   to add a new flag, add its name (VAEB.py:37-38)
 command_line_flags = ['continuous', 'generic_estimator', 'full_varational',
                       'synthetic']                 # added: synthetic data when the pickles are absent
@@ -66,9 +82,9 @@ def get_flag(flag, args, prefix='--'):
     return have_flag
 
 
-def parse_args(argv=None, spec=None, flags=None, flag_prefix='--'):
+def parse_args(argv=None, spec=None, flags=None, flag_prefix='--', out=print):
     """VAEB.py:491-504 (spec / flags: another driver's tables, e.g. freyFace.py:20-30, whose
-    parse_args (:290-300) does not report unused arguments)."""
+    parse_args (:290-300) does not report unused arguments; out: where the report goes)."""
     args = copy.deepcopy(sys.argv[1:] if argv is None else list(argv))
     arg_dict = {}
     for arg_name, (default, type_) in (spec or command_line_args).items():
@@ -76,7 +92,7 @@ def parse_args(argv=None, spec=None, flags=None, flag_prefix='--'):
     for flag_name in (flags or command_line_flags):
         arg_dict[flag_name] = get_flag(flag_name, args, flag_prefix)
     if len(args) > 0 and spec is None:
-        print('Have unused args: {0}'.format(args))
+        out('Have unused args: {0}'.format(args))
     return arg_dict
 
 
@@ -127,10 +143,35 @@ def load_dataset(continuous, synthetic=False, splits=2):
     return x[:50000], x[50000:60000]
 
 
+def _quiet(*a, **k):
+    pass
+
+
+def dp_layout(args):
+    """(world, rank, local_rank, communicator wanted) from the args and the launcher's
+    environment: world_size 0 with no launcher is one GPU without a communicator (the fused
+    step); world_size N >= 1 asks for N ranks with the all-reduce step; a launcher's
+    WORLD_SIZE > 1 implies it."""
+    world_env, rank, local = dp.env_ranks()
+    ws = int(args.get('world_size', 0) or 0)
+    if ws < 0:
+        raise ValueError('world_size must be >= 0')
+    if ws == 0:
+        return world_env, rank, local, world_env > 1
+    if world_env != ws:
+        raise ValueError('--world_size {0} but the launcher started {1} rank(s)'.format(ws, world_env))
+    return ws, rank, local, True
+
+
 def train_model(args):
     """VAEB.py:524-598: build the model, then per epoch shuffle the batch order, run every
-    minibatch step (device-side, no per-step host sync), validate, trace and print."""
+    minibatch step (device-side, no per-step host sync), validate, trace and print.  With
+    data parallelism every rank runs this loop on its share of each minibatch (the same
+    seed, so the same batch order everywhere); rank 0 alone prints, traces and saves."""
     from .model import VAEB
+    world, rank, local, use_comm = dp_layout(args)
+    say = print if rank == 0 else _quiet
+    lead = rank == 0
     np.random.seed(args['seed'])
     n_latent = args['n_latent']
     n_epochs = args['n_epochs']
@@ -144,35 +185,47 @@ def train_model(args):
     full_varational = args['full_varational']
     save_file = args['save_file']
     vb_param_file = args['vb_param_file']
-    kw = dict(device=args.get('device', 0), rng=args.get('rng', 'philox'),
+    kw = dict(device=args.get('device', 0) + local, rng=args.get('rng', 'philox'),
               objective=args.get('objective', 'sum_prior'), max_eval_rows=args.get('max_eval_rows', 10000),
-              fv_sample=bool(args.get('fv_sample', 0)))
+              fv_sample=bool(args.get('fv_sample', 0)), dtype=args.get('dtype', 'float32'))
+    B_local = batch_size
+    if use_comm:
+        B_local, kw['row_offset'], kw['B_global'] = dp.row_split(batch_size, world, rank,
+                                                                 args.get('dp_scaling', 'strong'))
+        group = dp.init_host_group(world)
+        from . import _lib
+        kw['comm'] = (dp.comm_uid(group, rank, _lib.Context.comm_unique_id), rank, world)
 
-    print("loading data")
+    say("loading data")
     if hidden_unit < 0:
         hidden_unit = 200 if continuous else 500
     data = load_dataset(continuous, args.get('synthetic', False))
     x_train, x_valid = data
 
-    print("creating the model")
+    say("creating the model")
     params = None
     if full_varational:
         from .pickle_static import read_mdl
         _, params = read_mdl(vb_param_file)
-    model = VAEB(x_train, continuous, hidden_unit, n_latent, batch_size, L, learning_rate, generic_estimator,
+    model = VAEB(x_train, continuous, hidden_unit, n_latent, B_local, L, learning_rate, generic_estimator,
                  full_varational, params, **kw)
+    if use_comm and model._ctx.comm_count() != world:
+        raise RuntimeError('rank {0}: the RCCL communicator holds {1} ranks, expected {2}'.format(
+            rank, model._ctx.comm_count(), world))
 
     if args.get('resume_file'):
         model.load_state(args['resume_file'])
     # x_valid is uploaded once and evaluated on device each epoch (VAEB.py:582)
     model.set_validation_data(x_valid)
 
-    print("learning")
+    say("learning")
     dedup = bool(args.get('trace_dedup', 0))
-    if len(trace_file) > 0:
+    trace = len(trace_file) > 0 and lead
+    if trace:
         with open(trace_file, 'w') as f:
             f.write('num_samples,L,Lvalid\n')
-    batch_order = np.arange(int(model.N / model.batch_size))
+    # minibatches of the GLOBAL batch (= batch_size unless dp_scaling weak)
+    batch_order = np.arange(int(model.N / getattr(model, 'B_global', model.batch_size)))
     for epoch in range(n_epochs):
         start = time.time()
         np.random.shuffle(batch_order)
@@ -183,25 +236,37 @@ def train_model(args):
         LBvalidation = model.validate_resident()
         if model.objective != "mean_map":
             LBvalidation /= x_valid.shape[0]
-        if len(trace_file) > 0:
+        if trace:
             with open(trace_file, 'a') as f:
                 f.write('{0},{1},{2}\n'.format(model.N * (epoch + 1), LB, LBvalidation))
-        print("Epoch %s : [Lower bound: %s, time: %s]" % (epoch, LB, time.time() - start))
-        print("          [Lower bound on validation set: %s]" % LBvalidation)
-        if len(trace_file) > 0 and not dedup:  # the reference writes every row twice (VAEB.py:591-593)
+        say("Epoch %s : [Lower bound: %s, time: %s]" % (epoch, LB, time.time() - start))
+        say("          [Lower bound on validation set: %s]" % LBvalidation)
+        if trace and not dedup:  # the reference writes every row twice (VAEB.py:591-593)
             with open(trace_file, 'a') as f:
                 f.write('{0},{1},{2}\n'.format(model.N * (epoch + 1), LB, LBvalidation))
-    if len(save_file) > 0:
+    if len(save_file) > 0 and lead:
         model.save(save_file)
-    if args.get('state_file'):
+    if args.get('state_file') and lead:
         model.save_state(args['state_file'])
     return model, data
 
 
 def main(argv=None):
-    """VAEB.py:601-608."""
-    args = parse_args(argv)
-    print_args(args)
+    """VAEB.py:601-608.  `--world_size N` (N > 1) without a launcher: start the N rank
+    processes first (no GPU call in this one) and return their exit code."""
+    argv = sys.argv[1:] if argv is None else list(argv)
+    ws = get_arg('world_size', list(argv), 0, int)
+    if ws > 1 and 'WORLD_SIZE' not in os.environ:
+        rc = dp.spawn_ranks(ws, dp.module_cmd(argv),
+                            env_extra={'PYTHONPATH': os.pathsep.join(
+                                [os.path.dirname(os.path.dirname(os.path.abspath(__file__)))] +
+                                ([os.environ['PYTHONPATH']] if os.environ.get('PYTHONPATH') else []))})
+        if rc:
+            raise SystemExit(rc)
+        return None, None
+    say = print if dp.env_ranks()[1] == 0 else _quiet
+    args = parse_args(argv, out=say)
+    print_args(args, out=say)
     if len(args['load_file']) == 0:
         model, data = train_model(args)
     else:

@@ -114,15 +114,16 @@ DEV bool arrive_last(int* cnt, int target, int* sflag) {
 // or inf (a diverging run) -- adds the count plus a POISON unit 2^54 (bits 54..58) instead
 // of a value: the completer sees the poison and writes NaN, which then propagates through
 // the step as it would on the slab path, and the accumulator is still reset cleanly.  The
-// contributor also sets the sticky word err[0] = acc[-1] (read and cleared by the step's
-// ELBO reduction, which reports it as VAEB_ERR_NUMERIC to the host).
+// contributor also sets the sticky guard word (blk[kBlkFxErr] = acc_ml[-1], passed
+// explicitly by BOTH hand-offs: acc_dz[-1] is a padding word of acc_ml's range; read and
+// cleared by the step's ELBO reduction, which reports it as VAEB_ERR_NUMERIC to the host).
 typedef __attribute__((address_space(1))) unsigned long long gu64;
 constexpr double kFxScale = 4294967296.0;   // 2^32
 constexpr float kFxMax = 131072.f;          // 2^17
 constexpr int kFxCntShift = 59, kFxPoisonShift = 54;
-DEV uint64_t fx_inc(float v, uint64_t* acc) {
+DEV uint64_t fx_inc(float v, uint64_t* guard) {
     if (__builtin_expect(!(__builtin_fabsf(v) < kFxMax), 0)) {
-        __hip_atomic_fetch_or((gu64*)(acc - 1), 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_or((gu64*)guard, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         return (1ull << kFxCntShift) + (1ull << kFxPoisonShift);
     }
     const int64_t q = (int64_t)__builtin_rint((double)v * kFxScale);
@@ -160,7 +161,7 @@ struct FxSlots {
     uint64_t t[NS];
     bool ok[NS];
     int col[NS], row[NS];
-    DEV void add(uint64_t* acc, int64_t row0, int ncol, const float (*pm)[17], int ne) {
+    DEV void add(uint64_t* acc, uint64_t* guard, int64_t row0, int ncol, const float (*pm)[17], int ne) {
 #pragma unroll
         for (int u = 0; u < NS; ++u) {
             const int e = (int)threadIdx.x + NTH * u;
@@ -170,7 +171,7 @@ struct FxSlots {
         }
 #pragma unroll
         for (int u = 0; u < NS; ++u) {
-            const uint64_t inc = fx_inc(pm[col[u]][row[u]], acc);
+            const uint64_t inc = fx_inc(pm[col[u]][row[u]], guard);
             uint64_t* p = fx_at(acc, (row0 + row[u]) * ncol + col[u]);
             t[u] = 0;
             if (NS == 2 && u == 0) t[u] = fx_add(p, inc);   // always present when NS == 2
@@ -373,7 +374,7 @@ DEV void enc_latent_body(const StepArgs& a, const FvFold& fvf) {
     if constexpr (AT) {
         __syncthreads();
         FxSlots<NS, NTH> fx;
-        fx.add(a.acc_ml, m0, 2 * Z, pm, 32 * Z);
+        fx.add(a.acc_ml, a.acc_ml - 1, m0, 2 * Z, pm, 32 * Z);
         if (by == 0) {   // the row block's eps, while the adds are in flight
             // the row base comes from `next` (kCtlNext): cur_batch is written by tile (0,0)
             // of this same launch, which need not have run yet

@@ -153,7 +153,7 @@ DEV void dhd_dz_body(const PDhdT<V>& p0, int bx, int by, f32x4* red, int sid) {
         // column c < Z: S = sum_l dZ_l of latent c; c >= Z: E = sum_l dZ_l eps_l of latent c - Z
         __syncthreads();
         FxSlots<NCT> fx;
-        fx.add(a.acc_dz, rbl * 16, 2 * Z, pm, 32 * Z);
+        fx.add(a.acc_dz, a.acc_ml - 1, rbl * 16, 2 * Z, pm, 32 * Z);   // guard: blk[kBlkFxErr]
         const float sl = a.sc / (float)a.L;
 #pragma unroll
         for (int u = 0; u < NCT; ++u) {

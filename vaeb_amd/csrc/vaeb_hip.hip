@@ -138,6 +138,7 @@ struct vaeb_ctx {
     float* h_elbo = nullptr;
     double* h_d2 = nullptr;
     float* h_out = nullptr;       // mapped host [SGVB / B, flags] every training step's last kernel writes
+    bool async_pending = false;   // steps enqueued by vaeb_update_many / _async not yet synchronised
     hipEvent_t ctl_ev = nullptr;
     // graphs
     hipGraphExec_t g1[2] = {nullptr, nullptr};
@@ -1322,6 +1323,12 @@ int vaeb_update(vaeb_ctx* c, int32_t batch_index, float* out) {
     // 577-579).  That call is ONE eager step whose minibatch index rides the launch
     // arguments (no order upload, no graph launch), and its value is read from the mapped
     // host slot the step's last kernel writes: 65 -> ~55 us per call (scripts/call_ab.py).
+    // Steps still queued from vaeb_update_many / vaeb_update_async would write the mapped
+    // slot too: drain them first, so the value read below is this call's step.
+    if (c->async_pending) {
+        HIP_TRY(hipStreamSynchronize(c->s));
+        c->async_pending = false;
+    }
     volatile uint32_t* flag = reinterpret_cast<volatile uint32_t*>(&c->h_out[1]);
     *flag = 0u;
     if (int rc = step_eager(c, batch_index)) return rc;
@@ -1338,6 +1345,7 @@ int vaeb_update_many(vaeb_ctx* c, const int32_t* idx, int32_t n) {
     if (c->eps_mode == VAEB_EPS_HOST && n > 1)
         return fail(VAEB_ERR_STATE, "host eps mode: one step per call (push eps before each vaeb_update)");
     int32_t done = 0;
+    if (n > 0) c->async_pending = true;
     if (n >= 2 && c->c.use_graph && c->g1[0] && !c->graph_failed && flips(c)) {
         // the call's first step goes out eagerly with its minibatch index in the launch
         // arguments: the GPU starts it while the host still submits the order upload and the
@@ -1362,6 +1370,7 @@ int vaeb_epoch_elbo(vaeb_ctx* c, double* out_sum, int64_t* out_steps) {
     HIP_TRY(hipMemcpyAsync(c->h_d2, c->epoch, 3 * sizeof(double), hipMemcpyDeviceToHost, c->s));
     HIP_TRY(hipMemsetAsync(c->epoch, 0, 3 * sizeof(double), c->s));
     HIP_TRY(hipStreamSynchronize(c->s));
+    c->async_pending = false;
     if (out_sum) *out_sum = c->h_d2[0];
     if (out_steps) *out_steps = (int64_t)c->h_d2[1];
     uint64_t st;
@@ -1374,6 +1383,7 @@ int vaeb_epoch_elbo(vaeb_ctx* c, double* out_sum, int64_t* out_steps) {
 int vaeb_synchronize(vaeb_ctx* c) {
     if (!c) return fail(VAEB_ERR_ARG, "null ctx");
     HIP_TRY(hipStreamSynchronize(c->s));
+    c->async_pending = false;
     return 0;
 }
 

@@ -1,10 +1,22 @@
-"""Row partition of a global minibatch over data-parallel ranks.
+"""Data parallelism on the host side: the row partition of a global minibatch,
+the rank launcher, and the RCCL communicator set-up.
 
 The SGVB objective is a sum over batch rows (VAEB.py:340-344), so a step shards by rows:
 rank r takes a contiguous block of the global minibatch and the gradients are summed with
-one all-reduce.  Weak scaling gives every rank B rows (B_global = B * world); strong
-scaling splits a fixed global batch as evenly as possible, earlier ranks taking the
-remainder (100 over 8 ranks = 13,13,13,13,12,12,12,12)."""
+one all-reduce inside the library (RCCL over xGMI).  Weak scaling gives every rank B rows
+(B_global = B * world); strong scaling splits a fixed global batch as evenly as possible,
+earlier ranks taking the remainder (100 over 8 ranks = 13,13,13,13,12,12,12,12).
+
+One process per GPU: ranks come from RANK / LOCAL_RANK / WORLD_SIZE, set by a launcher
+(torch.distributed.run) or by `spawn_ranks` before any GPU call.  torch.distributed (gloo)
+is host-side coordination only: it carries the 128-byte RCCL id from rank 0 to the others.
+"""
+from __future__ import annotations
+
+import os
+import subprocess
+import sys
+import time
 
 
 def row_split(batch, world, rank, scaling="weak"):
@@ -20,3 +32,80 @@ def row_split(batch, world, rank, scaling="weak"):
     base, extra = divmod(batch, world)
     rows = [base + (1 if r < extra else 0) for r in range(world)]
     return rows[rank], sum(rows[:rank]), batch
+
+
+def env_ranks():
+    """(world, rank, local_rank) from the launcher's environment (1, 0, 0 without one)."""
+    return (int(os.environ.get("WORLD_SIZE", "1")), int(os.environ.get("RANK", "0")),
+            int(os.environ.get("LOCAL_RANK", "0")))
+
+
+def free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def spawn_ranks(n, cmd, poll_s=0.2, env_extra=None):
+    """Start n rank processes of `cmd` (an argv list; one per GPU, RANK = LOCAL_RANK = r,
+    WORLD_SIZE = n, rendezvous on 127.0.0.1) and wait.  The parent makes no GPU call.  If
+    one rank fails the others are stopped (they would wait in a collective forever);
+    returns the first non-zero exit code, else 0."""
+    port = free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), **(env_extra or {}))
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        procs.append(subprocess.Popen(list(cmd), env=env))
+    while True:
+        codes = [p.poll() for p in procs]
+        bad = [c for c in codes if c not in (None, 0)]
+        if bad:
+            for p in procs:
+                if p.poll() is None:
+                    p.kill()
+            for p in procs:
+                p.wait()
+            return bad[0]
+        if all(c == 0 for c in codes):
+            return 0
+        time.sleep(poll_s)
+
+
+def module_cmd(argv):
+    """`python -m vaeb_amd <argv>` with this interpreter (the CLI's rank processes)."""
+    return [sys.executable, "-m", "vaeb_amd"] + list(argv)
+
+
+def init_host_group(world):
+    """The gloo process group the ranks coordinate on (None at world 1)."""
+    if world <= 1:
+        return None
+    import torch.distributed as dist
+    if not dist.is_initialized():
+        dist.init_process_group("gloo")
+    return dist
+
+
+def comm_uid(dist, rank, unique_id):
+    """The RCCL id every rank passes to vaeb_comm_init: drawn by rank 0 (unique_id()), carried
+    to the others over the gloo group (dist None: world 1, no broadcast)."""
+    uid = [unique_id() if rank == 0 else None]
+    if dist is not None:
+        dist.broadcast_object_list(uid, src=0)
+    return uid[0]
+
+
+def comm_setup(ctx, dist, rank, world):
+    """The library's RCCL communicator for `ctx` (vaeb_comm_init): rank 0 draws the id, the
+    gloo group carries it.  At world 1 (dist None) a one-rank communicator: the data-parallel
+    step (all-reduce + Adagrad launch) on one GPU.  Checks ncclCommCount == world."""
+    if dist is None and world != 1:
+        raise ValueError("world > 1 needs the host process group")
+    ctx.comm_init(comm_uid(dist, rank, type(ctx).comm_unique_id), rank, world)
+    n = ctx.comm_count()
+    if n != world:
+        raise RuntimeError(f"rank {rank}: the RCCL communicator holds {n} ranks, expected {world}")
+    return n

@@ -43,6 +43,24 @@ def initial_params(D, H, Z, continuous):
     return out
 
 
+def dtype_name(dtype):
+    """The engine a dtype name selects: "float32" (aliases f32, fp32) or "bf16" (bfloat16).
+    fp16 is not an engine: bf16 runs at the same MFMA rate without a loss scale."""
+    d = str(dtype).lower()
+    if d in ("float32", "f32", "fp32"):
+        return "float32"
+    if d in ("bf16", "bfloat16"):
+        return "bf16"
+    raise ValueError(f"dtype {dtype!r}: float32 or bf16 (fp16 operands are served by the bf16 engine, DESIGN.md 4.2)")
+
+
+def train_rows(data):
+    """The training images of a dataset in either form VAEB.load returns (VAEB.py:229-239):
+    (x_train, x_valid) for Frey, or mnist.pkl.gz's ((x, y) train, valid, test) for MNIST.
+    (The tuple test comes first: np.ndim of the ragged (images, labels) pair raises.)"""
+    return data[0][0] if isinstance(data[0], tuple) else data[0]
+
+
 class SharedParam:
     """Stand-in for a Theano shared parameter of the reference (`.name`, `.get_value()`,
     `.set_value()`, `.eval()`), backed by the device arena of the owning model."""
@@ -92,13 +110,17 @@ class VAEB:
     Extra keyword-only arguments (not in the reference): device, rng ("philox": on-device
     counter-based normals keyed by (seed, step, row); "theano": host RandomStreams
     emulation), seed, objective ("sum_prior" = VAEB.py; "mean_map" = VAEBfullbayes.py),
-    use_graph, max_eval_rows, world/rank/B_global/row_offset for data parallelism."""
+    use_graph, max_eval_rows; B_global / row_offset / comm for data parallelism (this rank's
+    batch_size rows start at row_offset of each B_global-row global minibatch; comm = a
+    (uid, rank, world) RCCL id for vaeb_comm_init, see dp.comm_setup); dtype "float32" (the
+    reference's floatX, run_on_gpu.sh:2) or "bf16" (bf16 MFMA operands, fp32 master weights)."""
 
     def __init__(self, x_train, continuous, hidden_units, latent_size, batch_size, L, learning_rate,
                  genericEstimator, fullVariational, params=None, prng=None, sigmaInit=None, *,
                  device=0, rng="philox", seed=10, objective="sum_prior", use_graph=True, max_eval_rows=10000,
-                 B_global=None, row_offset=0, fv_sample=False, inf=None):
+                 B_global=None, row_offset=0, fv_sample=False, inf=None, dtype="float32", comm=None):
         x_train = np.asarray(x_train, np.float32)
+        self.dtype = dtype_name(dtype)
         if inf is not None:
             # optimizer plug-in (degenerate-vae/infalg.py contract): its eta is the step size
             learning_rate = inf.eta
@@ -130,7 +152,14 @@ class VAEB:
                                  estimator=est,
                                  objective=_lib.OBJ_MEAN_MAP if objective == "mean_map" else _lib.OBJ_SUM_PRIOR,
                                  lr=learning_rate, adagrad_eps=self.eps, device=device, B_global=B_global,
-                                 row_offset=row_offset, max_eval_rows=max_eval_rows, use_graph=use_graph)
+                                 row_offset=row_offset, max_eval_rows=max_eval_rows, use_graph=use_graph,
+                                 dtype=_lib.DTYPE_BF16 if self.dtype == "bf16" else _lib.DTYPE_F32)
+        self.B_global = B_global or batch_size
+        self.row_offset = row_offset
+        self.world, self.rank = 1, 0
+        if comm is not None:
+            uid, self.rank, self.world = comm
+            self._ctx.comm_init(uid, self.rank, self.world)
         self._shapes = param_shapes(self.input_size, hidden_units, latent_size, self.continuous)
         if params is None:
             arrs = initial_params(self.input_size, hidden_units, latent_size, self.continuous)
@@ -156,7 +185,7 @@ class VAEB:
         else:
             self._stream = None
             self._ctx.set_eps_mode(_lib.EPS_PHILOX, seed)
-        self._nb = self.N // (B_global or batch_size)
+        self._nb = self.N // self.B_global
 
     # ------------------------------------------------------------------ state helpers
     def _param_arrays(self):
@@ -325,9 +354,7 @@ class VAEB:
         if data is None:
             from .cli import load_dataset
             data = load_dataset(continuous, splits=3 if not continuous else 2)
-        # the reference returns (x_train, x_valid) for Frey and mnist.pkl.gz's three
-        # (images, labels) pairs for MNIST (VAEB.py:229-239)
-        x_train = data[0] if np.ndim(data[0]) == 2 and not isinstance(data[0], tuple) else data[0][0]
+        x_train = train_rows(data)
         model = VAEB(x_train, continuous, int(hdr["n_hidden_units"]), int(hdr["n_latent"]), int(hdr["batch_size"]),
                      int(hdr["L"]), float(hdr["learning_rate"]), bool(hdr.get("genericEstimator", False)), False,
                      params, **kw)
