@@ -214,8 +214,8 @@ def test_bf16_graph_epoch_matches_eager_and_tracks_oracle():
 
 
 def test_bf16_full_size_row_linearity_and_determinism():
-    """Config 5 at its full size (4096-2048-128, B = 8192), where the float64 oracle is too
-    slow for a test: size-independent properties instead.  The SGVB and the data gradient
+    """Config 5 at its full size (4096-2048-128, B = 8192): size-independent properties,
+    beside the oracle comparison at the same size (next test).  The SGVB and the data gradient
     are sums over rows (VAEB.py:340-344), so the full batch equals the sum of its two
     halves run as separate 4096-row steps (bf16 rounding is per element; only the fp32
     accumulation order differs: norm-wise <= 1e-3); and a repeated step is bit-identical."""
@@ -247,6 +247,44 @@ def test_bf16_full_size_row_linearity_and_determinism():
     assert rel(g_full, g_a + g_b) <= 1e-3, rel(g_full, g_a + g_b)
     s_again, g_again, p_again = run(x, eps)
     assert s_again == s_full and np.array_equal(g_again, g_full) and np.array_equal(p_again, p_full)
+
+
+def test_bf16_full_size_step_matches_rounded_oracle():
+    """Config 5 at the size BASELINE names (4096-2048-128, B = 8192, x ~ Bernoulli(0.5) as
+    bench.py's synth workload), one step against the float64 oracle with bf16 rounding at
+    the engine's rounding points (O.step(..., q=bf16_round): ~7e11 FLOP, ~15 s on 8 host
+    threads) at this module's tolerances: ELBO 1e-4, data gradients 2e-3 per tensor,
+    Adagrad accumulator 4e-3; and theta' is the fp32 Adagrad rule applied to the engine's
+    own gradient.  Complements the property test above."""
+    from vaeb_amd import _lib
+    D, H, Z, B = 4096, 2048, 128, 8192
+    cfg = O.Config(D=D, H=H, Z=Z)
+    rng = np.random.default_rng(11)
+    x = (rng.random((2 * B, D), dtype=np.float32) < 0.5).astype(np.float32)
+    params = O.init_params(cfg)
+    params = [p if p.ndim == 2 else (0.01 * rng.standard_normal(p.shape)).astype(np.float32) for p in params]
+    acc = [np.full_like(p, 1e-3) for p in params]
+    eps = rng.standard_normal((1, B, Z)).astype(np.float32)
+    ctx = _lib.Context(D, H, Z, B, keep_grads=True, max_eval_rows=B, dtype=_lib.DTYPE_BF16)
+    ctx.set_data(x)
+    ctx.set_params(O.flatten(params))
+    ctx.set_adagrad_state(O.flatten(acc))
+    ctx.set_eps_mode(_lib.EPS_HOST)
+    ctx.push_eps(eps)
+    elbo = ctx.update(1)
+    g, newa, newp = ctx.get_grads(), ctx.get_adagrad_state(), ctx.get_params()
+    ctx.close()
+    p64 = [p.astype(np.float64) for p in params]
+    q_elbo, _, q_a, q_aux = O.step(p64, [a.astype(np.float64) for a in acc], x[B:].astype(np.float64),
+                                   eps.astype(np.float64), cfg, q=O.bf16_round)
+    assert abs(elbo - q_elbo) <= 1e-4 * abs(q_elbo), (elbo, q_elbo)
+    for (n, s), gg, rq in zip(O.param_shapes(cfg), O.unflatten(g, cfg), q_aux["data_grads"]):
+        assert rel(gg.reshape(s), rq) <= 2e-3, (n, rel(gg.reshape(s), rq))
+    assert rel(newa, O.flatten(q_a)) <= 4e-3
+    th = O.flatten(params).astype(np.float64)
+    gt = g.astype(np.float64) - th
+    want = th + cfg.lr * gt / (np.sqrt(O.flatten(acc).astype(np.float64) + gt * gt) + cfg.eps)
+    assert np.abs(newp - want).max() <= 1e-6 + 1e-5 * np.abs(want).max()
 
 
 @pytest.mark.parametrize("overlap,fork", [("1", "1"), ("0", "1"), ("1", "0")])
