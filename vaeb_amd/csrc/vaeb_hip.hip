@@ -46,9 +46,11 @@ int fail(int code, const char* fmt, ...) {
 #define HIP_TRY(expr)                                                                      \
     do {                                                                                   \
         hipError_t e_ = (expr);                                                            \
-        if (e_ != hipSuccess)                                                              \
+        if (e_ != hipSuccess) {                                                            \
+            (void)hipGetLastError(); /* a failed call must not resurface at the next launch */ \
             return fail(VAEB_ERR_HIP, "%s failed: %s (%s:%d)", #expr, hipGetErrorString(e_), \
                         __FILE__, __LINE__);                                               \
+        }                                                                                  \
     } while (0)
 
 #define CHECK_LAUNCH()                                                                     \
@@ -1793,9 +1795,15 @@ int vaeb_get_activation(vaeb_ctx* c, const char* name, float* out, int64_t n) {
     if (strcmp(name, "dZ") == 0 && fused_latent(c) && c->fold_bwd && !is_bf16(c) && ho_dz(c) == 1)
         return fail(VAEB_ERR_STATE, "dZ is not stored by the atomic latent hand-off (fan-in <= 16, latent_bwd.hpp): "
                                     "create the context with VAEB_ATOMIC_HO=0 to read it");
+    const int64_t R = c->cap, RL = (int64_t)c->cap * c->c.L, D = c->c.D, H = c->c.H, Z = c->c.Z;
+    const int64_t cap[] = {R * H, R * Z, R * Z, RL * Z, RL * Z, RL * H, RL * D, RL * D, RL * H, RL * Z, R * 2 * Z,
+                           R * H, RL * D, RL * cdiv(Z, 16), RL * cdiv(D, 16)};
     for (auto& a : kActs)
         if (strcmp(a.name, name) == 0) {
             if (!ptrs[a.which]) return fail(VAEB_ERR_STATE, "activation %s not allocated", name);
+            if (n < 0 || n > cap[a.which])
+                return fail(VAEB_ERR_ARG, "activation %s holds %lld floats, %lld requested", name,
+                            (long long)cap[a.which], (long long)n);
             HIP_TRY(hipStreamSynchronize(c->s));
             HIP_TRY(hipMemcpy(out, ptrs[a.which], sizeof(float) * n, hipMemcpyDeviceToHost));
             return 0;
