@@ -4,7 +4,7 @@ set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 mkdir -p gpurun_out/ab
-for r in 1 2; do
+for r in $(seq ${AB_ROUNDS:-2}); do
   for v in base "$@"; do
     if [ $v = base ]; then unset VAEB_LIB_VARIANT; else export VAEB_LIB_VARIANT=$v; fi
     timeout -k 10 120 python3 bench.py --steps 4000 --warmup 500 --no-cpu-baseline > gpurun_out/ab/$v.json 2> gpurun_out/ab/$v.err || { tail -5 gpurun_out/ab/$v.err; exit 1; }

@@ -48,9 +48,12 @@ def test_vaeb_class_theano_rng_mode_is_reproducible():
     assert r[0] == r[1]
 
 
-@pytest.mark.parametrize("continuous,use_graph,overlap", [(False, True, "1"), (True, True, "1"), (False, False, "1"),
-                                                         (False, True, "0"), (True, True, "0")])
-def test_dp_path_world1_matches_fused_path(continuous, use_graph, overlap, monkeypatch):
+@pytest.mark.parametrize("continuous,use_graph,overlap,shard", [
+    (False, True, "1", "0"), (True, True, "1", "0"), (False, False, "1", "0"), (False, True, "0", "0"),
+    (True, True, "0", "0"),
+    # the sharded optimizer (reduce-scatter -> own shard of Adagrad -> all-gather), forced at world 1
+    (False, True, "0", "1"), (True, True, "1", "1"), (False, False, "1", "1")])
+def test_dp_path_world1_matches_fused_path(continuous, use_graph, overlap, shard, monkeypatch):
     """The data-parallel path (gradients stored; with VAEB_DP_OVERLAP=1 -- the bf16 engine's
     default -- bucket A = W2 [| W6] all-reduced and updated on the second stream while the
     backward continues, bucket B + SGVB after it; with 0 -- the fp32 default -- one
@@ -58,6 +61,7 @@ def test_dp_path_world1_matches_fused_path(continuous, use_graph, overlap, monke
     Bernoulli / Gaussian decoder, graph-replayed and eager."""
     from vaeb_amd import _lib
     monkeypatch.setenv("VAEB_DP_OVERLAP", overlap)
+    monkeypatch.setenv("VAEB_DP_SHARD", shard)
     cfg = O.Config(D=560, H=200, Z=2, continuous=True) if continuous else O.Config(D=784, H=500, Z=20)
     x = O.synthetic_frey(n=2000) if continuous else O.synthetic_mnist(n=2000)
     order = np.random.default_rng(1).permutation(20).astype(np.int32)
@@ -129,3 +133,36 @@ def test_vaeb_optimizer_plugin_binds_the_engine_rule():
     assert np.array_equal(acc.get_value(), a.ADA[0])
     acc.set_value(np.zeros_like(a.ADA[0]))
     assert not a.ADA[0].any() and a.ADA[1].any()
+
+
+@pytest.mark.parametrize("continuous,overlap", [(False, "0"), (True, "1"), (False, "1")])
+def test_sharded_dp_optimizer_world1_is_bitwise_the_replicated_one(continuous, overlap, monkeypatch):
+    """the sharded DP optimizer (vaeb_hip.hip dp_reduce_update: reduce-scatter of
+    each arena run's 64-aligned shards + all-reduce of the remainders and the SGVB slot, this
+    rank's shard of prior + Adagrad, all-gather of theta' shards) forced at world 1 equals the
+    replicated DP path (all-reduce, Adagrad over the whole arena) bit for bit: ELBO, theta and
+    the Adagrad state, graph-replayed and eager, with bucket A overlapped or not."""
+    from vaeb_amd import _lib
+    monkeypatch.setenv("VAEB_DP_OVERLAP", overlap)
+    cfg = O.Config(D=560, H=200, Z=2, continuous=True) if continuous else O.Config(D=784, H=500, Z=20)
+    x = O.synthetic_frey(n=2000) if continuous else O.synthetic_mnist(n=2000)
+    order = np.random.default_rng(2).permutation(20).astype(np.int32)
+    outs = {}
+    for shard in ("0", "1"):
+        for use_graph in (True, False):
+            monkeypatch.setenv("VAEB_DP_SHARD", shard)
+            ctx = _lib.Context(cfg.D, cfg.H, cfg.Z, 100, max_eval_rows=500, use_graph=use_graph,
+                               decoder=_lib.DEC_GAUSSIAN if continuous else _lib.DEC_BERNOULLI)
+            ctx.comm_init(_lib.Context.comm_unique_id(), 0, 1)
+            ctx.set_data(x)
+            ctx.set_params(O.flatten(O.init_params(cfg)))
+            ctx.set_eps_mode(_lib.EPS_PHILOX, 10)
+            ctx.update_many(order)
+            v = ctx.update(3)
+            s, n = ctx.epoch_elbo()
+            outs[shard, use_graph] = (s, v, ctx.get_params(), ctx.get_adagrad_state())
+            ctx.close()
+    ref = outs["0", True]
+    for key, o in outs.items():
+        assert o[0] == ref[0] and o[1] == ref[1], key
+        assert np.array_equal(o[2], ref[2]) and np.array_equal(o[3], ref[3]), key

@@ -287,8 +287,9 @@ def test_bf16_full_size_step_matches_rounded_oracle():
     assert np.abs(newp - want).max() <= 1e-6 + 1e-5 * np.abs(want).max()
 
 
-@pytest.mark.parametrize("overlap,fork", [("1", "1"), ("0", "1"), ("1", "0")])
-def test_bf16_dp_path_world1_matches_fused_optimizer(overlap, fork, monkeypatch):
+@pytest.mark.parametrize("overlap,fork,shard", [("1", "1", "0"), ("0", "1", "0"), ("1", "0", "0"),
+                                                ("1", "1", "1"), ("0", "1", "1"), ("1", "0", "1")])
+def test_bf16_dp_path_world1_matches_fused_optimizer(overlap, fork, shard, monkeypatch):
     """The data-parallel path of the bf16 engine (gradients stored, RCCL all-reduce of
     [grads | SGVB], replicated Adagrad + shadow rewrite in adagrad_bf16_kernel) at world
     size 1 against the fused-optimizer path, over 6 graph-replayed steps: forked (the
@@ -297,6 +298,7 @@ def test_bf16_dp_path_world1_matches_fused_optimizer(overlap, fork, monkeypatch)
     from vaeb_amd import _lib
     monkeypatch.setenv("VAEB_DP_OVERLAP", overlap)
     monkeypatch.setenv("VAEB_BF_FORK", fork)
+    monkeypatch.setenv("VAEB_DP_SHARD", shard)   # 1: the sharded optimizer forced at world 1
     cfg = O.Config(D=256, H=128, Z=32)
     B = 256
     x = data_for(cfg, 8 * B)

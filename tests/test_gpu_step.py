@@ -379,8 +379,10 @@ def test_atomic_and_slab_handoffs_agree(kw, monkeypatch):
     (VAEB_ATOMIC_HO=1: counted fixed-point atomics up to fan-in 16, slabs above), slabs +
     ticket + reducer everywhere (=0), the encoder slabs summed by the decoder launch
     (VAEB_ENC_RED=1), the unfolded latent backward (VAEB_FOLD_BWD=0: the P67 launches) and
-    one 16-column tile per Bernoulli decoder workgroup (VAEB_DECOUT_CT=1) and the encoders on
-    512-thread workgroups (VAEB_ENC16=0; =1: the atomic hand-off encoder only).
+    one 16-column tile per Bernoulli decoder workgroup (VAEB_DECOUT_CT=1), the encoders on
+    512-thread workgroups (VAEB_ENC16=0; =1: the atomic hand-off encoder only), the slab-form
+    latent backward finished in the dhd launch (VAEB_BWD_DEFER=0) instead of the last launch,
+    and each step's dW2 in its own dhd launch (VAEB_DW2_DEFER=0) instead of the next encoder's.
     They sum the same partials in different arithmetic (exact integer vs ordered fp32), so
     they agree to rounding, and each is bitwise deterministic (graph == eager)."""
     from vaeb_amd import _lib
@@ -393,9 +395,15 @@ def test_atomic_and_slab_handoffs_agree(kw, monkeypatch):
     # "dct1": one 16-column tile per Bernoulli decoder workgroup (default two)
     # "enc8": no encoder on 1024 threads (VAEB_ENC16=0); "enc16slab": only the slab-only one
     # (=1; default 2: the atomic hand-off encoder on 1024-thread workgroups too)
-    modes = {"atomic": ("1", "0", "1", "2", "2"), "slab": ("0", "0", "1", "2", "2"), "decred": ("1", "1", "1", "2", "2"),
-             "unfolded": ("1", "0", "0", "2", "2"), "dct1": ("1", "0", "1", "1", "2"), "enc8": ("1", "1", "1", "2", "0"),
-             "enc16slab": ("1", "0", "1", "2", "1")}
+    # "ticket": VAEB_BWD_DEFER=0, the slab-form latent backward finished by the dhd launch's last
+    # arriver (default 1: by reducer workgroups of the last launch, kernels_aux.hpp LatRed)
+    # "dw2now": VAEB_DW2_DEFER=0, each step's dW2 (| dW6) in its own dhd launch (default 1: in the
+    # next step's encoder launch, the last one flushed by get_params)
+    modes = {"atomic": ("1", "0", "1", "2", "2", "1", "1"), "slab": ("0", "0", "1", "2", "2", "1", "1"),
+             "decred": ("1", "1", "1", "2", "2", "1", "1"), "unfolded": ("1", "0", "0", "2", "2", "1", "1"),
+             "dct1": ("1", "0", "1", "1", "2", "1", "1"), "enc8": ("1", "1", "1", "2", "0", "1", "1"),
+             "enc16slab": ("1", "0", "1", "2", "1", "1", "1"), "ticket": ("0", "0", "1", "2", "2", "0", "1"),
+             "dw2now": ("1", "0", "1", "2", "2", "1", "0")}
     for mode in modes:
         for use_graph in (True, False):
             monkeypatch.setenv("VAEB_ATOMIC_HO", modes[mode][0])
@@ -403,6 +411,8 @@ def test_atomic_and_slab_handoffs_agree(kw, monkeypatch):
             monkeypatch.setenv("VAEB_FOLD_BWD", modes[mode][2])
             monkeypatch.setenv("VAEB_DECOUT_CT", modes[mode][3])
             monkeypatch.setenv("VAEB_ENC16", modes[mode][4])
+            monkeypatch.setenv("VAEB_BWD_DEFER", modes[mode][5])
+            monkeypatch.setenv("VAEB_DW2_DEFER", modes[mode][6])
             ctx = _lib.Context(cfg.D, cfg.H, cfg.Z, B, L=cfg.L,
                                decoder=_lib.DEC_GAUSSIAN if cfg.continuous else _lib.DEC_BERNOULLI,
                                max_eval_rows=B, use_graph=use_graph)
@@ -419,7 +429,7 @@ def test_atomic_and_slab_handoffs_agree(kw, monkeypatch):
         assert np.array_equal(out[mode, True][1], out[mode, False][1])
     es = out["slab", True][0]
     frac = {}
-    for mode in ("atomic", "decred", "unfolded", "dct1", "enc8", "enc16slab"):
+    for mode in ("atomic", "decred", "unfolded", "dct1", "enc8", "enc16slab", "ticket", "dw2now"):
         ea = out[mode, True][0]
         assert abs(ea - es) <= 1e-5 * abs(es), (mode, ea, es)
         d = np.abs(out[mode, True][1] - out["slab", True][1])
@@ -429,6 +439,51 @@ def test_atomic_and_slab_handoffs_agree(kw, monkeypatch):
     # take Adagrad steps that follow that rounding; a different K split of the encoder (enc8:
     # 8 instead of 16 partials) moves ~0.13 % of MNIST's parameters by more than 1e-3 lr.
     assert max(frac.values()) <= 2e-3, frac
+
+
+@pytest.mark.parametrize("kw", [dict(D=784, H=500, Z=20), dict(D=560, H=200, Z=2, continuous=True)],
+                         ids=["mnist20", "frey2"])
+def test_deferred_dw2_is_bitwise_the_same_step(kw, monkeypatch):
+    """The deferred dW2 (step t's dW2 | dW6 + Adagrad in step t+1's encoder launch, the last
+    one flushed when the host reads the state) runs the same tiles with the same K split as
+    the in-step form (VAEB_DW2_DEFER=0): parameters, Adagrad state and ELBO bit for bit, with
+    host reads, a validation and a checkpoint round trip between calls, the synchronous
+    update() among them, and graph replay as well as eager steps."""
+    from vaeb_amd import _lib
+    cfg = O.Config(**kw)
+    x = data_for(cfg, 800)
+    res = {}
+    for defer in ("1", "0"):
+        for use_graph in (True, False):
+            monkeypatch.setenv("VAEB_DW2_DEFER", defer)
+            ctx = _lib.Context(cfg.D, cfg.H, cfg.Z, 100, decoder=int(cfg.continuous), max_eval_rows=200,
+                               use_graph=use_graph)
+            ctx.set_data(x)
+            ctx.set_params(O.flatten(O.init_params(cfg)))
+            ctx.set_eps_mode(_lib.EPS_PHILOX, 10)
+            out = []
+            ctx.update_many(np.array([3, 1, 4, 1, 5], np.int32))
+            out.append(ctx.get_params())                       # flush
+            out.append(ctx.update(2))                          # sync step after a flush
+            out.append(ctx.update(6))                          # sync step with a pending dW2
+            out.append(ctx.validate(x[:200]))                  # flush inside the evaluation
+            ctx.update_many(np.array([0, 7, 2], np.int32))
+            ckpt = f"/tmp/vaeb_dw2_{defer}_{int(use_graph)}.ckpt"
+            ctx.checkpoint_save(ckpt)
+            ctx.update_many(np.array([5, 5], np.int32))
+            out.append(ctx.get_params())
+            ctx.checkpoint_load(ckpt)                          # the pending dW2 must not land on it
+            ctx.update_many(np.array([5, 5], np.int32))
+            out.append(ctx.get_params())
+            out.append(ctx.get_adagrad_state())
+            out.append(ctx.epoch_elbo()[0])
+            ctx.close()
+            res[defer, use_graph] = out
+    ref = res["0", True]
+    for key, out in res.items():
+        for a, b in zip(out, ref):
+            assert np.array_equal(np.asarray(a), np.asarray(b)), key
+    assert np.array_equal(ref[4], ref[5])   # resume: the same two steps from the checkpoint
 
 
 def test_fixed_point_handoff_overflow_is_reported_not_silent():

@@ -250,11 +250,145 @@ struct WGroup {
 // dA3 = ([dMu | dLv] [W4 | W5]^T) (1 - h^2) computed inside the dW3 workgroups (the
 // folded latent backward, latent_bwd.hpp): the B panel of dW3 = [X | 1]^T dA3 is formed
 // from dMuLv, W4 / W5 (pre-update arena) and h instead of being loaded.
+// Deferred latent backward (VAEB_BWD_DEFER, default where the slab form is chosen: fan-in >
+// 16).  The dhd tiles of the previous launch stored their partial dZ slabs with plain stores
+// and ended (the kernel boundary publishes them: no drain, no ticket in that launch); here
+// `nred` reducer workgroups -- dispatched right after the ELBO one -- each sum one (row block,
+// latent column group) of the slabs in fixed order, form [dMu | dLv] and publish it
+// write-through (sc1), every storing wave drained, behind ONE agent-scope add per workgroup
+// on one counter.  The consumers (the dW3 workgroups' dA3 panel and the dW4 | dW5 group)
+// poll that counter with sc1 loads from one lane, join a workgroup barrier and read [dMu |
+// dLv] with sc1 loads only: MI355X_MICROARCH.md's hand-off table row 1, the four conditions
+// latent.hpp arrive_last cites.  The counter is zeroed by the dhd launch (a plain store the
+// boundary publishes).  The poll is bounded: a timeout sets the guard word (reported as a
+// step status) instead of hanging the GPU.
+struct LatRed {
+    const float* slab;                 // [L][nrb][nctH][Z][16] partial dZ slabs
+    const float *mu, *lv, *eps, *z;    // [Mbp][Z]; [L][Mbp][Z]
+    float* dZ;                         // [L][Mbp][Z] (kept for inspection, as the ticketed form)
+    float* dml;                        // [Mbp][2Z] [dMu | dLv]: the handed-off bytes
+    int* cnt;                          // completion counter
+    uint64_t* guard;                   // blk[kBlkFxErr]: timeout bit
+    int nred, ngrp, zg, nctH, L, est, Mb, Mbp, Z;
+    float sc;
+};
 struct Da3Src {
     const float *dml, *W4, *W5, *h;
     float* dA3;           // the column slice is also stored (by the D-row tile 0 workgroups)
     int Z, H, Mb, Mbp;
+    LatRed red;           // red.nred > 0: [dMu | dLv] is produced in this launch (deferred form)
 };
+constexpr uint64_t kGuardHandoffTimeout = 4;
+
+// One reducer workgroup (256 threads): row block rb, latent columns [j0, j0 + nj).  Element
+// thread t < 16 nj owns (row rb * 16 + t / nj, column j0 + t % nj).
+DEV void lat_reduce_wg(const LatRed& r, int wi, f32x4* red, float (*dzs)[17]) {
+    const int Z = r.Z, nrb = r.Mbp >> 4;
+    const int rb = wi / r.ngrp, cg = wi - rb * r.ngrp;
+    const int j0 = cg * r.zg, nj = min(r.zg, Z - j0);
+    const int nf = 4 * nj, np = 256 / nf;   // float4 per slab group (column, row quad); partitions
+    const int t = threadIdx.x, f = t % nf, part = t / nf;
+    const bool el = t < 16 * nj;
+    const int ml = el ? t / nj : 0, jj = el ? t - (t / nj) * nj : 0;
+    const int m = rb * 16 + ml, j = j0 + jj;
+    const bool valid = el && m < r.Mb;
+    // the element's own operands ride the round trip of the first slab loads
+    const uint32_t oj = valid ? (uint32_t)(m * Z + j) * 4u : kOOB;
+    const float mu = bld(mkbuf(r.mu, (int64_t)r.Mbp * Z * 4), oj);
+    const float lv = bld(mkbuf(r.lv, (int64_t)r.Mbp * Z * 4), oj);
+    float epre[kLP], zpre[kLP];
+    const rsrc_t be = mkbuf(r.eps, (int64_t)r.L * r.Mbp * Z * 4), bz = mkbuf(r.z, (int64_t)r.L * r.Mbp * Z * 4);
+#pragma unroll
+    for (int l = 0; l < kLP; ++l) {
+        const uint32_t o = (valid && l < r.L) ? (uint32_t)((l * r.Mbp + m) * Z + j) * 4u : kOOB;
+        epre[l] = bld(be, o);
+        zpre[l] = r.est == EST_LA ? bld(bz, o) : 0.f;
+    }
+    const rsrc_t bs = mkbuf(r.slab, (int64_t)r.L * r.Mbp * r.nctH * Z * 4);
+    float dzsum = 0.f, dzes = 0.f;
+    for (int l = 0; l < r.L; ++l) {
+        const int64_t first = (int64_t)(l * nrb + rb) * r.nctH;
+        constexpr int SV = 8;
+        f32x4 sum = zero4();
+        for (int c0 = part; c0 < r.nctH; c0 += SV * np) {
+            f32x4 v[SV];
+#pragma unroll
+            for (int u = 0; u < SV; ++u) {
+                const int ct = c0 + u * np;
+                v[u] = bld4(bs, (part < np && ct < r.nctH) ? (uint32_t)((((first + ct) * Z + j0) * 4 + f) * 16) : kOOB);
+            }
+#pragma unroll
+            for (int u = 0; u < SV; ++u) sum += v[u];
+        }
+        red[t] = sum;
+        __syncthreads();
+        if (t < nf) {   // the np partition sums in order: deterministic
+            f32x4 s4 = red[t];
+            for (int pp = 1; pp < np; ++pp) s4 += red[pp * nf + t];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) dzs[t >> 2][4 * (t & 3) + k] = s4[k];
+        }
+        __syncthreads();
+        const float dz = valid ? dzs[jj][ml] : 0.f;
+        const float e = l < kLP ? epre[l] : (valid ? r.eps[((int64_t)l * r.Mbp + m) * Z + j] : 0.f);
+        dzsum += dz;
+        dzes += dz * e;
+        if (el) r.dZ[((int64_t)l * r.Mbp + m) * Z + j] = dz;
+        __syncthreads();   // red / dzs are reused by the next plane
+    }
+    // [dMu | dLv] (VAEB.py:315-346): LB / FV the KL direct terms, LA the
+    // prior - logQ direct terms (latent_bwd.hpp latent_bwd_elem)
+    const float sl = r.sc / (float)r.L, sd = fexp(0.5f * lv);
+    float dmu = 0.f, dlv = 0.f;
+    if (valid) {
+        if (r.est == EST_LA) {
+            float tm = 0.f, tv = 0.f;
+            for (int l = 0; l < r.L; ++l) {
+                const int64_t ol = ((int64_t)l * r.Mbp + m) * Z + j;
+                const float zz = l < kLP ? zpre[l] : r.z[ol];
+                const float e = l < kLP ? epre[l] : r.eps[ol];
+                tm += -zz;
+                tv += 0.5f - 0.5f * zz * sd * e;
+            }
+            dmu = dzsum + sl * tm;
+            dlv = dzes * 0.5f * sd + sl * tv;
+        } else {
+            dmu = dzsum - r.sc * mu;
+            dlv = dzes * 0.5f * sd + r.sc * 0.5f * (1.f - fexp(lv));
+        }
+    }
+    // publish: sc1 stores by the storing waves (waves 0, 1 at 16 nj <= 128), each drained, the
+    // barrier, one counter add
+    if (el) {
+        const rsrc_t bd = mkbuf(r.dml, (int64_t)r.Mbp * 2 * Z * 4);
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, dmu), bd, (uint32_t)(m * 2 * Z + j) * 4u, 0, 16);
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, dlv), bd, (uint32_t)(m * 2 * Z + Z + j) * 4u, 0, 16);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (t == 0) __hip_atomic_fetch_add((__attribute__((address_space(1))) int*)r.cnt, 1, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Consumer side: one lane polls the counter (sc1 loads, s_sleep between polls, bounded), the
+// workgroup joins a barrier; every later load of [dMu | dLv] in the workgroup is an sc1 load.
+DEV void lat_wait(int* cnt, int nred, uint64_t* const* guard) {
+    if (threadIdx.x == 0) {
+        typedef __attribute__((address_space(1))) int gi32;
+        uint32_t spins = 0;
+        while (__hip_atomic_load((gi32*)cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < nred) {
+            __builtin_amdgcn_s_sleep(2);
+            if (++spins >= (1u << 20)) {   // ~1 s: never a hang; the step reports a status instead
+                __hip_atomic_fetch_or((__attribute__((address_space(1))) unsigned long long*)*guard,
+                                      (unsigned long long)kGuardHandoffTimeout, __ATOMIC_RELAXED,
+                                      __HIP_MEMORY_SCOPE_AGENT);
+                break;
+            }
+        }
+    }
+    __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // keeps the sc1 loads below the poll
+}
 
 // Kernel arguments of a weight-gradient launch: up to two groups (WGradArgs), or the three
 // groups + dA3 source of the folded latent backward's last launch (WGradArgs3).  Separate
@@ -270,17 +404,31 @@ struct WGradArgs {
     int64_t P;
     uint64_t* dbg;
 };
+// The first 64 bytes of WGradArgs3: every kernel argument a workgroup needs before its first
+// operand load (its role, its group, the batch pointer), read as ONE scalar load at entry --
+// read field by field, each branch on the previous one cost a dependent scalar round trip
+// to the kernarg segment (the deferred reducers' count added one: last launch 10.2 -> 11.4 us).
+struct W3Head {
+    const float* xbase; const int* cur_batch; int64_t batch_stride;
+    int with_elbo, total_wgs, ngroups, nred;   // nred: LatRed reducers ahead of the tiles
+    int gb1, gb2;                              // first workgroup of groups 1 and 2
+    int* red_cnt;                              // LatRed counter (the consumers' poll)
+};
 struct WGradArgs3 {
+    W3Head hd;
     WGroup g[3];
-    int ngroups, total_wgs;
     OptArgs opt;
     ElboArgs elbo;
-    int with_elbo;
-    const float* xbase; const int* cur_batch; int64_t batch_stride;
     int64_t P;
     uint64_t* dbg;
     Da3Src da3;
 };
+DEV const float* wa_xbase(const WGradArgs& p) { return p.xbase; }
+DEV const int* wa_cur_batch(const WGradArgs& p) { return p.cur_batch; }
+DEV int64_t wa_batch_stride(const WGradArgs& p) { return p.batch_stride; }
+DEV const float* wa_xbase(const WGradArgs3& p) { return p.hd.xbase; }
+DEV const int* wa_cur_batch(const WGradArgs3& p) { return p.hd.cur_batch; }
+DEV int64_t wa_batch_stride(const WGradArgs3& p) { return p.hd.batch_stride; }
 
 // [W4 | W5]^T element block B(k, n) = W4[n][k] (k < Z) | W5[n][k - Z] (Z <= k < 2Z), four
 // consecutive k at row n (16-byte loads when vz: Z % 4 == 0 and both bases aligned).
@@ -301,8 +449,10 @@ DEV f32x4 ld_w45(rsrc_t bw4, rsrc_t bw5, int Z, int H, int n, int k, bool vz) {
 // w of NWV takes the 16-row blocks w, w + NWV, ... (NR = kWKB / 16 / NWV of them); K = 2Z
 // <= 64.  Every operand of all NR blocks is issued before the first MFMA (one round trip;
 // a per-block load -> MFMA loop cost the launch a second one), the [W4 | W5]^T slice once.
-template <int NWV, int TS>
-DEV void da3_panel(const Da3Src& d, int kb, int j0, bool store, float (*sb)[kWP]) {
+// DEFER (the deferred latent backward, LatRed): [dMu | dLv] is produced in this launch, so its
+// loads wait for the reducers' counter and are sc1; the W4 / W5 and h loads go out first.
+template <int NWV, int TS, bool DEFER = false>
+DEV void da3_panel(const Da3Src& d, int kb, int j0, bool store, float (*sb)[kWP], int* cnt = nullptr, int nred = 0) {
     constexpr int NR = kWKB / 16 / NWV;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int li = lane & 15, q = lane >> 4;
@@ -322,8 +472,9 @@ DEV void da3_panel(const Da3Src& d, int kb, int j0, bool store, float (*sb)[kWP]
     for (int u = 0; u < NR; ++u) {
         const int r0 = kb + 16 * (wv + NWV * u);
         const int rl = r0 < d.Mbp ? d.Mbp : 0;   // blocks past the padded batch load nothing
+        if constexpr (!DEFER)
 #pragma unroll
-        for (int c = 0; c < 4; ++c) av[u][c] = kc4(bd, K2, r0 + li, c * 16 + 4 * q, c < nkc ? rl : 0, K2, vd);
+            for (int c = 0; c < 4; ++c) av[u][c] = kc4(bd, K2, r0 + li, c * 16 + 4 * q, c < nkc ? rl : 0, K2, vd);
 #pragma unroll
         for (int ts = 0; ts < TS; ++ts) {
             const int n = j0 + 16 * ts + li;
@@ -332,6 +483,16 @@ DEV void da3_panel(const Da3Src& d, int kb, int j0, bool store, float (*sb)[kWP]
                 const int mm = r0 + 4 * q + r;
                 hv[u][ts][r] = bld(bh, (n < H && mm < d.Mb) ? (uint32_t)(mm * H + n) * 4u : kOOB);
             }
+        }
+    }
+    if constexpr (DEFER) {
+        lat_wait(cnt, nred, &d.red.guard);
+#pragma unroll
+        for (int u = 0; u < NR; ++u) {
+            const int r0 = kb + 16 * (wv + NWV * u);
+            const int rl = r0 < d.Mbp ? d.Mbp : 0;
+#pragma unroll
+            for (int c = 0; c < 4; ++c) av[u][c] = kc4x<16>(bd, K2, r0 + li, c * 16 + 4 * q, c < nkc ? rl : 0, K2, vd);
         }
     }
 #pragma unroll
@@ -362,24 +523,34 @@ DEV void da3_panel(const Da3Src& d, int kb, int j0, bool store, float (*sb)[kWP]
 // per-lane vector loads).  NWV = 4 waves (standalone launch) or 8 (a 512-thread fused
 // launch): waves w and w + 4 then take alternate K chunks and are summed through LDS.
 // DA3: the B panel is dA3, formed in the workgroup (da3_panel) instead of loaded.
-template <bool VEC, int NWV, int TS, bool DA3 = false, class WA>
-DEV void wgrad_body(const WA& p, const WGroup& g, int bid, float (*sa)[kWP], float (*sb)[kWP]) {
+// DEFER: the B panel ([dMu | dLv]: dW4 | dW5) or dA3's [dMu | dLv] operand is produced in this
+// launch by the deferred latent backward (LatRed): its loads wait for the counter and are sc1.
+// gate (the deferred dW2 workers, latent.hpp enc_latent16_w2_kernel): a device flag read at
+// entry, whose 0 drops the tile before its stores -- the operand loads go out speculatively
+// instead of one scalar round trip after it.
+template <bool VEC, int NWV, int TS, bool DA3 = false, bool DEFER = false, class WA>
+DEV void wgrad_body(const WA& p, const WGroup& g, int bid, float (*sa)[kWP], float (*sb)[kWP],
+                    const int* gate = nullptr) {
+    const int gv = gate ? ld_launch_const(gate) : 1;
     static_assert(NWV == 4 || NWV == 8, "wgrad: 4 or 8 waves");
     static_assert(TS == 1 || TS == 2 || TS == 4, "wgrad: 16, 32 or 64 columns per tile");
     constexpr int kWTS = TS, kWTJ = 16 * TS;
     constexpr int NTH = 64 * NWV;
+    // the thread's index in its tile worker (a 1024-thread workgroup can run two 512-thread
+    // workers side by side: enc_latent16_w2_kernel)
+    const int tid = (int)threadIdx.x % NTH;
     // resolve the batch pointer first: its load must not queue behind the prefetches below
-    const float* at = g.at_is_x ? p.xbase + (int64_t)ld_launch_const(p.cur_batch) * p.batch_stride : g.at;
+    const float* at = g.at_is_x ? wa_xbase(p) + (int64_t)ld_launch_const(wa_cur_batch(p)) * wa_batch_stride(p) : g.at;
     const rsrc_t ba = mkbuf(at, (int64_t)g.klim_at * g.ld_at * 4);
 #ifdef VAEB_TIMELINE
-    if (VAEB_DBG_ON(p.dbg) && threadIdx.x == 0) {   // the batch pointer resolved
+    if (VAEB_DBG_ON(p.dbg) && tid == 0) {   // the batch pointer resolved
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         p.dbg[bid * 8 + 4] = __builtin_amdgcn_s_memrealtime();
     }
 #endif
     const int lt = bid - g.wg_begin;
     const int i0 = (lt / g.tiles_j) * kWT, j0 = (lt % g.tiles_j) * kWTJ;
-    const int lane = threadIdx.x & 63, wave = (threadIdx.x >> 6) & 3, kh = threadIdx.x >> 8;
+    const int lane = tid & 63, wave = (tid >> 6) & 3, kh = tid >> 8;
     const int li = lane & 15, q = lane >> 4;
     const int NT = g.N0 + g.N1;
 
@@ -452,7 +623,7 @@ DEV void wgrad_body(const WA& p, const WGroup& g, int bid, float (*sa)[kWP], flo
         f32x4 ra[NU], rb[NU];
 #pragma unroll
         for (int u = 0; u < NU; ++u) {
-            const int e = threadIdx.x + NTH * u;
+            const int e = tid + NTH * u;
             const int kr = e >> 4, c4 = e & 15;
             const int k = kb + kr;
             const int i = i0 + 4 * c4, j = j0 + 4 * c4;
@@ -464,8 +635,8 @@ DEV void wgrad_body(const WA& p, const WGroup& g, int bid, float (*sa)[kWP], flo
                 for (int s = 0; s < 4; ++s)
                     ra[u][s] = bld(ba, (k < g.klim_at && i + s < g.rowsW) ? (uint32_t)(k * g.ld_at + i + s) * 4u : kOOB);
             }
-            if (DA3) {
-                rb[u] = zero4();
+            if (DA3 || DEFER) {
+                rb[u] = zero4();   // (DEFER: loaded below, after the counter poll)
             } else if (vb) {
                 const bool in0 = j < g.N0;
                 const uint32_t o0 = (jt && k < g.K && in0) ? (uint32_t)(k * g.ld0 + j) * 4u : kOOB;
@@ -484,16 +655,43 @@ DEV void wgrad_body(const WA& p, const WGroup& g, int bid, float (*sa)[kWP], flo
 #ifdef VAEB_TIMELINE
         if (VAEB_DBG_ON(p.dbg) && kb == 0) {   // the stage's panel loads landed
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            if (threadIdx.x == 0) p.dbg[bid * 8 + 5] = __builtin_amdgcn_s_memrealtime();
+            if (tid == 0) p.dbg[bid * 8 + 5] = __builtin_amdgcn_s_memrealtime();
         }
 #endif
-        if constexpr (DA3) da3_panel<NWV, TS>(p.da3, kb, j0, i0 == 0, sb);
+        if constexpr (DEFER && !DA3) {
+            // B panel = [dMu | dLv] of this launch's reducers: poll, then sc1 loads only
+            if (kb == 0) lat_wait(p.hd.red_cnt, p.hd.nred, &p.da3.red.guard);
+#pragma unroll
+            for (int u = 0; u < NU; ++u) {
+                const int e = tid + NTH * u;
+                const int kr = e >> 4, c4 = e & 15;
+                const int k = kb + kr;
+                const int j = j0 + 4 * c4;
+                const bool jt = 4 * c4 < kWTJ;
+                if (vb) {
+                    const bool in0 = j < g.N0;
+                    const uint32_t o0 = (jt && k < g.K && in0) ? (uint32_t)(k * g.ld0 + j) * 4u : kOOB;
+                    const uint32_t o1 = (jt && k < g.K && !in0 && j - g.N0 < g.N1) ? (uint32_t)(k * g.ld1 + j - g.N0) * 4u : kOOB;
+                    rb[u] = in0 ? bld4x<16>(bb0, o0) : bld4x<16>(bb1, o1);
+                } else {
+#pragma unroll
+                    for (int s = 0; s < 4; ++s) {
+                        const int jj = j + s;
+                        const bool in0 = jj < g.N0;
+                        rb[u][s] = in0 ? bldx<16>(bb0, (jt && k < g.K) ? (uint32_t)(k * g.ld0 + jj) * 4u : kOOB)
+                                       : bldx<16>(bb1, (jt && k < g.K && jj - g.N0 < g.N1) ? (uint32_t)(k * g.ld1 + jj - g.N0) * 4u : kOOB);
+                    }
+                }
+            }
+        }
+        if constexpr (DA3 && DEFER) da3_panel<NWV, TS, true>(p.da3, kb, j0, i0 == 0, sb, p.hd.red_cnt, p.hd.nred);
+        else if constexpr (DA3) da3_panel<NWV, TS>(p.da3, kb, j0, i0 == 0, sb);
 #ifdef VAEB_TIMELINE
-        if (VAEB_DBG_ON(p.dbg) && kb == 0 && threadIdx.x == 0) p.dbg[bid * 8 + 2] = __builtin_amdgcn_s_memrealtime();
+        if (VAEB_DBG_ON(p.dbg) && kb == 0 && tid == 0) p.dbg[bid * 8 + 2] = __builtin_amdgcn_s_memrealtime();
 #endif
 #pragma unroll
         for (int u = 0; u < NU; ++u) {
-            const int e = threadIdx.x + NTH * u;
+            const int e = tid + NTH * u;
             const int kr = e >> 4, c4 = e & 15;
             const int i = i0 + 4 * c4;
             // the all-ones row (bias gradient) for every batch row of the padded K
@@ -505,7 +703,7 @@ DEV void wgrad_body(const WA& p, const WGroup& g, int bid, float (*sa)[kWP], flo
         }
         __syncthreads();
 #ifdef VAEB_TIMELINE
-        if (VAEB_DBG_ON(p.dbg) && kb == 0 && threadIdx.x == 0) p.dbg[bid * 8 + 6] = __builtin_amdgcn_s_memrealtime();
+        if (VAEB_DBG_ON(p.dbg) && kb == 0 && tid == 0) p.dbg[bid * 8 + 6] = __builtin_amdgcn_s_memrealtime();
 #endif
         const int nch = min(kWKB, g.K - kb) >> 4;
         for (int c = kh; c < nch; c += NWV / 4) {
@@ -534,7 +732,8 @@ DEV void wgrad_body(const WA& p, const WGroup& g, int bid, float (*sa)[kWP], flo
 #pragma unroll
         for (int t = 0; t < kWTS; ++t) acc[t] += red[(wave * 4 + t) * 64 + lane];
     }
-    if (VAEB_DBG_ON(p.dbg) && threadIdx.x == 0) p.dbg[bid * 8 + 1] = __builtin_amdgcn_s_memrealtime();
+    if (VAEB_DBG_ON(p.dbg) && tid == 0) p.dbg[bid * 8 + 1] = __builtin_amdgcn_s_memrealtime();
+    if (gv == 0) return;   // (wave-uniform; no barrier follows)
 
     // ---- epilogue: out-of-range byte offsets make masked buffer stores no-ops
     const rsrc_t bto = mkbuf(p.opt.theta_out, p.P * 4), bgr = mkbuf(p.opt.grad, p.P * 4);
@@ -566,7 +765,7 @@ DEV void wgrad_body(const WA& p, const WGroup& g, int bid, float (*sa)[kWP], flo
                 __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, nt4), bto, off4[t], 0, kStWT);
             }
         }
-        if (VAEB_DBG_ON(p.dbg) && threadIdx.x == 0) p.dbg[bid * 8 + 3] = __builtin_amdgcn_s_memrealtime();
+        if (VAEB_DBG_ON(p.dbg) && tid == 0) p.dbg[bid * 8 + 3] = __builtin_amdgcn_s_memrealtime();
         return;
     }
 #pragma unroll
@@ -582,7 +781,7 @@ DEV void wgrad_body(const WA& p, const WGroup& g, int bid, float (*sa)[kWP], flo
                 bst_opt(bto, off[t][r], nt);
             }
         }
-    if (VAEB_DBG_ON(p.dbg) && threadIdx.x == 0) p.dbg[bid * 8 + 3] = __builtin_amdgcn_s_memrealtime();
+    if (VAEB_DBG_ON(p.dbg) && tid == 0) p.dbg[bid * 8 + 3] = __builtin_amdgcn_s_memrealtime();
 }
 
 template <bool VEC, int TS>
@@ -608,25 +807,55 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WGradArgs p) {
     else wgrad_body<VEC, 4, TS>(p, p.g[0], bid, sa, sb);
 }
 
+// The deferred dW2's flush (vaeb_hip.hip w2_flush): the pending step's dW2 (| dW6) tiles as
+// their own launch, when the host reads or replaces the state before another step ran them.
+// (512-thread tiles, as in the encoder launch: the same K split, so the same sums bit for bit)
+template <bool VEC, int TS>
+__global__ __launch_bounds__(512) void w2_flush_kernel(WGradArgs p, const int* pend) {
+    __shared__ float sa[kWKB][kWP];
+    __shared__ float sb[kWKB][kWP];
+    if (ld_launch_const(pend) == 0) return;
+    wgrad_body<VEC, 8, TS>(p, p.g[0], xcd_remap(blockIdx.x, p.total_wgs), sa, sb);
+}
+
 // The folded latent backward's last launch: dW3 (dA3 formed in the workgroup) | dW4 | dW5
 // | dW1, and the ELBO workgroup first.  VM: bit g = group g's panels take 16-byte loads.
-template <int VM, int TS>
+// DEFER (LatRed, p.da3.red.nred reducers): blocks [ELBO][reducers][tiles], the reducers
+// dispatched ahead of every tile that waits for them (and 2 workgroups per CU hold the whole
+// grid at MNIST: 1 + 21 + 448 <= 512).  Stamps: reducers at logical ids total_wgs + 1 + r.
+template <int VM, int TS, bool DEFER>
 __global__ __launch_bounds__(256) void wgrad3_kernel(WGradArgs3 p) {
     __shared__ float sa[kWKB][kWP];
     __shared__ float sb[kWKB][kWP];
-    int bid;
-    if (p.with_elbo)
-        bid = blockIdx.x == 0 ? p.total_wgs : xcd_remap((int)blockIdx.x - 1, p.total_wgs);
-    else
-        bid = xcd_remap(blockIdx.x, p.total_wgs);
-    if (VAEB_DBG_ON(p.dbg) && threadIdx.x == 0) p.dbg[bid * 8 + 0] = __builtin_amdgcn_s_memrealtime();
-    if (bid >= p.total_wgs) {
-        elbo_reduce(p.elbo, reinterpret_cast<double*>(&sa[0][0]));
-        return;
+    const W3Head h = p.hd;   // one scalar load: the role and group boundaries
+    // (the empty asm makes every field live here, so the loads go out together, before the
+    // first branch, instead of one dependent round trip per branch)
+    asm volatile("" ::"s"(h.with_elbo), "s"(h.total_wgs), "s"(h.nred), "s"(h.gb1), "s"(h.gb2), "s"(h.xbase),
+                 "s"(h.cur_batch), "s"(h.batch_stride), "s"(h.red_cnt));
+    int b = (int)blockIdx.x;
+    if (h.with_elbo) {
+        if (b == 0) {
+            if (VAEB_DBG_ON(p.dbg) && threadIdx.x == 0) p.dbg[h.total_wgs * 8 + 0] = __builtin_amdgcn_s_memrealtime();
+            elbo_reduce(p.elbo, reinterpret_cast<double*>(&sa[0][0]));
+            return;
+        }
+        --b;
     }
-    if (bid >= p.g[2].wg_begin) wgrad_body<(VM & 4) != 0, 4, TS>(p, p.g[2], bid, sa, sb);
-    else if (bid >= p.g[1].wg_begin) wgrad_body<(VM & 2) != 0, 4, TS>(p, p.g[1], bid, sa, sb);
-    else wgrad_body<(VM & 1) != 0, 4, TS, true>(p, p.g[0], bid, sa, sb);
+    if constexpr (DEFER) {
+        if (b < h.nred) {
+            const int sid = h.total_wgs + 1 + b;
+            if (VAEB_DBG_ON(p.dbg) && threadIdx.x == 0) p.dbg[sid * 8 + 0] = __builtin_amdgcn_s_memrealtime();
+            lat_reduce_wg(p.da3.red, b, reinterpret_cast<f32x4*>(&sa[0][0]), reinterpret_cast<float(*)[17]>(&sb[0][0]));
+            if (VAEB_DBG_ON(p.dbg) && threadIdx.x == 0) p.dbg[sid * 8 + 3] = __builtin_amdgcn_s_memrealtime();
+            return;
+        }
+        b -= h.nred;
+    }
+    const int bid = xcd_remap(b, h.total_wgs);
+    if (VAEB_DBG_ON(p.dbg) && threadIdx.x == 0) p.dbg[bid * 8 + 0] = __builtin_amdgcn_s_memrealtime();
+    if (bid >= h.gb2) wgrad_body<(VM & 4) != 0, 4, TS>(p, p.g[2], bid, sa, sb);
+    else if (bid >= h.gb1) wgrad_body<(VM & 2) != 0, 4, TS, false, DEFER>(p, p.g[1], bid, sa, sb);
+    else wgrad_body<(VM & 1) != 0, 4, TS, true, DEFER>(p, p.g[0], bid, sa, sb);
 }
 
 // ----------------------------------------------------------------- DP optimizer
@@ -635,14 +864,30 @@ __global__ __launch_bounds__(256) void wgrad3_kernel(WGradArgs3 p) {
 // buckets (vaeb_hip.hip: dp_bucket_*): a DpRange names the arena elements one launch
 // updates, as up to two index runs [lo0, lo0 + n0) and [lo1, lo1 + n1); `book` = this
 // launch also publishes the step's SGVB and advances the cursor / step counter.
+// Up to kDpRuns index runs [lo[k], lo[k] + n[k]) -- sharded DP (vaeb_hip.hip dp_reduce_update):
+// this rank's shard and the replicated tail of each of the arena's three runs.
+constexpr int kDpRuns = 6;
 struct DpRange {
-    int64_t lo0, n0, lo1, n1;
+    int64_t lo[kDpRuns], n[kDpRuns];
     int book;
-    DEV int64_t at(int64_t v) const { return v < n0 ? lo0 + v : lo1 + (v - n0); }
+    DEV int64_t total() const {
+        int64_t t = 0;
+#pragma unroll
+        for (int k = 0; k < kDpRuns; ++k) t += n[k];
+        return t;
+    }
+    DEV int64_t at(int64_t v) const {
+#pragma unroll
+        for (int k = 0; k < kDpRuns - 1; ++k) {
+            if (v < n[k]) return lo[k] + v;
+            v -= n[k];
+        }
+        return lo[kDpRuns - 1] + v;
+    }
 };
 __global__ __launch_bounds__(256) void adagrad_kernel(OptArgs o, int64_t P, DpRange r, ElboArgs e) {
     const int64_t stride = (int64_t)gridDim.x * 256;
-    const int64_t n = r.n0 + r.n1;
+    const int64_t n = r.total();
     const rsrc_t bti = mkbuf(o.theta_in, P * 4), bto = mkbuf(o.theta_out, P * 4);
     const rsrc_t bac = mkbuf(o.acc, P * 4), bgr = mkbuf(o.grad, P * 4);
     // U grid-stride elements per memory round trip: every load is issued before any store

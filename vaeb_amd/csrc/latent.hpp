@@ -28,6 +28,7 @@
 #pragma once
 #include <type_traits>
 #include "fused.hpp"
+#include "kernels_aux.hpp"   // wgrad_body: the deferred dW2 workers of enc_latent16_w2_kernel
 
 namespace vaeb {
 
@@ -250,13 +251,21 @@ struct PEncCT : PEnc {
 // CT: h column tiles per workgroup (1, or 2: half the contributors per latent element).
 // NWV: waves splitting K (8; or 16 -- 1024-thread workgroups -- on the slab-only path HO = 3
 // and the atomic hand-off HO = 1; the ticketed reducer HO = 0 keeps its 512-thread layout).
-template <int NCT, int GCH, bool FV, int HO, int CT = 1, int NWV = 8>
-DEV void enc_latent_body(const StepArgs& a, const FvFold& fvf) {
+// red_ext (EXTRED): the K-slice reduction buffer (64 NWV CT f32x4) from the caller -- the
+// deferred-dW2 encoder carves it from the LDS its dW2 workers use (enc_latent16_w2_kernel).
+template <int NCT, int GCH, bool FV, int HO, int CT = 1, int NWV = 8, bool EXTRED = false>
+DEV void enc_latent_body(const StepArgs& a, const FvFold& fvf, f32x4* red_ext = nullptr) {
     static_assert(NWV == 8 || (HO != 0 && !FV), "16 waves: no ticketed reducer, no FV stream");
     constexpr bool AT = HO == 1;
     constexpr int NTH = 64 * NWV;
     constexpr int NS = NWV == 16 ? 1 : NCT;   // atomic-add slots per thread: 32 Z <= 1024
-    __shared__ f32x4 red[64 * NWV * CT];
+    f32x4* red;
+    if constexpr (EXTRED) {
+        red = red_ext;
+    } else {
+        __shared__ f32x4 red_own[64 * NWV * CT];
+        red = red_own;
+    }
     __shared__ float hs[16][16 * CT + 4];
     __shared__ int sflag;
     __shared__ float pm[HO == 1 ? 64 : 1][17];   // the tile's [mu | lv] partials, [column][row]
@@ -504,6 +513,29 @@ __global__ __launch_bounds__(512) void enc_latent_fv_kernel(StepArgs a, FvFold f
 template <int NCT, int GCH, int HO, int CT>
 __global__ __launch_bounds__(1024) void enc_latent16_kernel(StepArgs a) {
     enc_latent_body<NCT, GCH, false, HO, CT, 16>(a, FvFold{});
+}
+
+// The same encoder with the PREVIOUS step's dW2 (| dW6) tiles + Adagrad on the CUs it leaves
+// idle (the deferred dW2, vaeb_hip.hip vaeb_ctx::dw2_defer): the encoder's 112 workgroups
+// take 112 of 256 CUs at MNIST, and W2 is first read again by this step's decoder launch.
+// Grid rows >= rows_enc are dW2 workers, two 64 x (16 TS) tiles each (waves 0-7 and 8-15,
+// wgrad_body's 512-thread tile on its own half of the LDS); they read hd / dA2 of the previous
+// step (intact until this step's decoder launch) and theta from the other arena, and write
+// W2' into the arena this step reads (which the encoder does not touch).  *pend == 0
+// (nothing pending: the first step, or a flush since) drops their stores.  LDS: two tiles' (sa,
+// sb) = 139 KB, the encoder's K-slice reduction buffer (32 KB) carved from the same block.
+template <int NCT, int GCH, int HO, int CT, bool VEC, int TS>
+__global__ __launch_bounds__(1024) void enc_latent16_w2_kernel(StepArgs a, WGradArgs w, const int* pend, int rows_enc) {
+    __shared__ __attribute__((aligned(16))) float lds[4 * kWKB * kWP];
+    static_assert(sizeof(float) * 4 * kWKB * kWP >= sizeof(f32x4) * 64 * 16 * CT, "LDS union");
+    if ((int)blockIdx.y >= rows_enc) {
+        const int half = (int)threadIdx.x >> 9;
+        const int bid = 2 * (((int)blockIdx.y - rows_enc) * (a.Mbp >> 4) + (int)blockIdx.x) + half;
+        float (*sa)[kWP] = reinterpret_cast<float(*)[kWP]>(lds + half * 2 * kWKB * kWP);
+        wgrad_body<VEC, 8, TS>(w, w.g[0], bid, sa, sa + kWKB, pend);
+        return;
+    }
+    enc_latent_body<NCT, GCH, false, HO, CT, 16, true>(a, FvFold{}, reinterpret_cast<f32x4*>(lds));
 }
 
 // ----------------------------------------------------------------------------- P4'

@@ -53,6 +53,8 @@ DEV void latent_bwd_elem(const StepArgs& a, bool valid, int m, int j, float mu, 
 // One dhd tile (bx = row block of the L * Mbp decoder rows, by = H column tile) + its dZ
 // slab; the last arriver of latent row block bx % (Mbp / 16) finishes the latent backward.
 // red: >= 512 f32x4 of LDS.
+// HO 2 (deferred, VAEB_BWD_DEFER): the tile stores its slab plainly and ends; the last
+// launch's reducer workgroups sum the slabs (kernels_aux.hpp LatRed).
 // AT (atomic hand-off, latent.hpp fx_*): instead of a dZ slab, the tile adds its partial
 // dZ_l(m, j) into S(m, j) = sum_l dZ_l and dZ_l eps_l(m, j) into E(m, j) = sum_l dZ_l eps_l
 // (acc_dz; L * H/16 contributors each); the add completing S stores dMu(m, j), the one
@@ -62,7 +64,7 @@ DEV void dhd_dz_body(const PDhdT<V>& p0, int bx, int by, f32x4* red, int sid) {
     constexpr bool AT = HO == 1;
     __shared__ float ts[16][20];
     __shared__ int sflag;
-    __shared__ float pm[HO ? 64 : 1][17];   // HO: [dZ | dZ eps] partials, [column][row]
+    __shared__ float pm[AT ? 64 : 1][17];   // AT: [dZ | dZ eps] partials, [column][row]
     PDhdT<V> p = p0;
     p.prepare();
     const StepArgs& a = p.a;
@@ -91,7 +93,7 @@ DEV void dhd_dz_body(const PDhdT<V>& p0, int bx, int by, f32x4* red, int sid) {
         const rsrc_t bw1 = mkbuf(a.W1, (int64_t)Z * H * 4);
         const bool vh = (H & 3) == 0 && aligned16(a.W1);
         w1v = kc4(bw1, H, wave * 16 + li, n0 + 4 * q, Z, H, vh);
-        if constexpr (HO != 0) {
+        if constexpr (AT) {
             const rsrc_t be = mkbuf(a.eps, (int64_t)a.Me * Z * 4);
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
@@ -136,7 +138,7 @@ DEV void dhd_dz_body(const PDhdT<V>& p0, int bx, int by, f32x4* red, int sid) {
         for (int s = 0; s < 4; ++s) av[s] = ts[li][4 * q + s];
         const f32x4 sv = mfma4(av, w1v, zero4());
         const int j = wave * 16 + li;
-        if constexpr (HO != 0) {
+        if constexpr (AT) {
             if (j < Z)
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
@@ -146,7 +148,11 @@ DEV void dhd_dz_body(const PDhdT<V>& p0, int bx, int by, f32x4* red, int sid) {
         } else {
             const rsrc_t bs = mkbuf(a.slab_dz, (int64_t)a.L * a.Mbp * nctH * Z * 4);
             const int64_t blk = ((int64_t)l * nrb + rbl) * nctH + by;
-            st4_sc1(bs, j < Z ? (uint32_t)(((blk * Z + j) * 16 + 4 * q) * 4) : kOOB, sv);
+            const uint32_t so = j < Z ? (uint32_t)(((blk * Z + j) * 16 + 4 * q) * 4) : kOOB;
+            // HO 2 (deferred): plain stores, published by the kernel boundary to the reducers
+            // of the last launch (kernels_aux.hpp LatRed); HO 0: write-through for the ticket
+            if constexpr (HO == 2) __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, sv), bs, so, 0, 0);
+            else st4_sc1(bs, so, sv);
         }
     }
     if constexpr (AT) {
@@ -183,6 +189,11 @@ DEV void dhd_dz_body(const PDhdT<V>& p0, int bx, int by, f32x4* red, int sid) {
         return;
     }
     VAEB_STAMP_AT(a, sid, 2);
+    if constexpr (HO == 2) {
+        // the last launch's reducers count their arrivals on cnt_dz[0] (zeroed here, before it)
+        if (sid == 0 && threadIdx.x == 0) *a.cnt_dz = 0;
+        return;
+    }
     if (!arrive_last<NCT>(a.cnt_dz + rbl, nctH * a.L, &sflag)) return;
     VAEB_STAMP_AT(a, sid, 3);
 
@@ -252,11 +263,14 @@ DEV void dhd_dz_body(const PDhdT<V>& p0, int bx, int by, f32x4* red, int sid) {
 // grid.  The dhd tiles are dispatched first: with the latent backward behind them they are
 // the launch's critical path (tile_wgrad_kernel, without it, puts the dW2 blocks first).
 template <int NCT, int GCH, bool VEC, int TS, int HO>
-__global__ __launch_bounds__(512) void dhd_dz_wgrad_kernel(PDhdT<VEC> p, WGradArgs w, int ntile, int gx) {
+// pend (the deferred dW2: no dW2 tiles in this grid): set to 1 -- the next step's encoder
+// launch, or the host's flush, runs this step's dW2 (| dW6) (latent.hpp enc_latent16_w2_kernel)
+__global__ __launch_bounds__(512) void dhd_dz_wgrad_kernel(PDhdT<VEC> p, WGradArgs w, int ntile, int gx, int* pend) {
     __shared__ float sa[kWKB][kWP];
     __shared__ float sb[kWKB][kWP];
     const int nwg = w.total_wgs - ntile;   // grid = w.total_wgs (no implicit-argument load)
     const int b0 = blockIdx.x;
+    if (pend && b0 == 0 && threadIdx.x == 0) *pend = 1;
     const int bid = b0 < ntile ? xcd_remap(b0, ntile) : ntile + xcd_remap(b0 - ntile, nwg);
     if (bid < ntile) {
         dhd_dz_body<NCT, GCH, VEC, HO>(p, bid % gx, bid / gx, reinterpret_cast<f32x4*>(&sa[0][0]), bid);

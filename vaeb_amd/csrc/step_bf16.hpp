@@ -47,6 +47,16 @@ struct ShadowMap {
     }
 };
 
+// Sharded DP (vaeb_hip.hip dp_reduce_update): after the all-gather of theta', the bf16 shadow
+// entries of the elements other ranks updated
+__global__ __launch_bounds__(256) void shadow_runs_kernel(const float* th, bf16_t* sh, ShadowMap m, DpRange r) {
+    const int64_t stride = (int64_t)gridDim.x * 256, n = r.total();
+    for (int64_t v = (int64_t)blockIdx.x * 256 + threadIdx.x; v < n; v += stride) {
+        const int64_t i = r.at(v), si = m.at(i);
+        if (si >= 0) sh[si] = (bf16_t)f2bf(th[i]);
+    }
+}
+
 // theta (fp32 arena) -> bf16 shadow
 __global__ __launch_bounds__(256) void make_shadow_kernel(const float* th, bf16_t* sh, ShadowMap m) {
     const int64_t stride = (int64_t)gridDim.x * 256;
@@ -545,7 +555,7 @@ __global__ __launch_bounds__(256) void bias_opt_kernel(BiasArgs b) {
 // whole arena, rewriting the bf16 shadow.
 __global__ __launch_bounds__(256) void adagrad_bf16_kernel(Opt o, int64_t P, DpRange r, ShadowMap m, ElboArgs e) {
     const int64_t stride = (int64_t)gridDim.x * 256;
-    const int64_t n = r.n0 + r.n1;
+    const int64_t n = r.total();
     const rsrc_t bti = mkbuf(o.th_in, P * 4), bto = mkbuf(o.th_out, P * 4);
     const rsrc_t bac = mkbuf(o.accum, P * 4), bgr = mkbuf(o.grad, P * 4);
     // U grid-stride elements per memory round trip (loads before stores), the rule of

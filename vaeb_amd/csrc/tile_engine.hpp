@@ -120,6 +120,11 @@ DEV rsrc_t mkbuf(const void* p, int64_t nbytes) {
 }
 DEV float bld(rsrc_t b, uint32_t off) { return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(b, off, 0, 0)); }
 DEV f32x4 bld4(rsrc_t b, uint32_t off) { return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(b, off, 0, 0)); }
+// AUX = 16: sc1 (loads bypass L1; stores write through) -- the in-launch hand-off form
+template <int AUX>
+DEV float bldx(rsrc_t b, uint32_t off) { return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(b, off, 0, AUX)); }
+template <int AUX>
+DEV f32x4 bld4x(rsrc_t b, uint32_t off) { return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(b, off, 0, AUX)); }
 DEV void bst(rsrc_t b, uint32_t off, float v) { __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), b, off, 0, 0); }
 // Optimizer stores (theta', accumulator) are written through (sc1): the next launch reads
 // them from other XCDs anyway, and a launch that ends with megabytes of dirty L2 lines pays
@@ -144,6 +149,20 @@ DEV f32x4 kc4(rsrc_t b, int ld, int r, int k, int rlim, int klim, bool vec) {
     v.y = bld(b, (rok && k + 1 < klim) ? base + 4 : kOOB);
     v.z = bld(b, (rok && k + 2 < klim) ? base + 8 : kOOB);
     v.w = bld(b, (rok && k + 3 < klim) ? base + 12 : kOOB);
+    return v;
+}
+
+// kc4 with a cache-policy operand (AUX 16: the sc1 loads of an in-launch hand-off)
+template <int AUX>
+DEV f32x4 kc4x(rsrc_t b, int ld, int r, int k, int rlim, int klim, bool vec) {
+    const bool rok = r < rlim;
+    const uint32_t base = (uint32_t)(r * ld + k) * 4u;
+    if (vec) return bld4x<AUX>(b, (rok && k < klim) ? base : kOOB);
+    f32x4 v;
+    v.x = bldx<AUX>(b, (rok && k + 0 < klim) ? base + 0 : kOOB);
+    v.y = bldx<AUX>(b, (rok && k + 1 < klim) ? base + 4 : kOOB);
+    v.z = bldx<AUX>(b, (rok && k + 2 < klim) ? base + 8 : kOOB);
+    v.w = bldx<AUX>(b, (rok && k + 3 < klim) ? base + 12 : kOOB);
     return v;
 }
 

@@ -157,7 +157,19 @@ struct vaeb_ctx {
     hipStream_t s2 = nullptr;     // DP: the gradient buckets' all-reduces and their Adagrad
     hipEvent_t dp_ev[3] = {};     // fork after dW2, bucket A reduced, bucket A updated
     bool dp_overlap = false;      // bucket A on s2 (bf16 engine; VAEB_DP_OVERLAP=0/1 overrides)
+    bool dp_shard = false;        // reduce-scatter -> this rank's shard of Adagrad -> all-gather (world > 1)
     bool fold_bwd = true;         // Z <= 32: latent backward folded into the dhd launch (VAEB_FOLD_BWD=0: P67)
+    // slab form of the folded backward (fan-in > 16): the dZ slab sum and [dMu | dLv] by
+    // reducer workgroups of the LAST launch (kernels_aux.hpp LatRed) instead of a ticket and
+    // a last-arriver reducer in the dhd launch.  VAEB_BWD_DEFER=0: the ticketed form.
+    bool bwd_defer = true;
+    // the deferred dW2: dW2 (| dW6) + Adagrad of step t run in step t+1's encoder launch, on
+    // the CUs the encoder leaves idle (latent.hpp enc_latent16_w2_kernel), so the dhd launch
+    // holds the dhd tiles alone; host reads of the state flush a pending one first (w2_flush).
+    // fp32 LB / LA, no communicator, 16-wave encoder.  VAEB_DW2_DEFER=0: dW2 in the dhd launch.
+    bool dw2_defer = true;
+    int* w2pend = nullptr;        // device: 1 = a step's dW2 is pending (set by its dhd launch)
+    bool w2_dirty = false;        // host: a step was enqueued since the last flush
     int atomic_ho = 1;            // folded latent hand-offs: 1 by fan-in (ho_mode), 0 slabs
     bool graph_upload = true;     // hipGraphUpload at capture (VAEB_GRAPH_UPLOAD=0: at first launch)
     // the slab-only encoder on 1024-thread workgroups (16 waves splitting K: twice the loads in
@@ -249,6 +261,30 @@ void launch_bigk(hipStream_t s, const P& p) {
 }
 
 bool fused_latent(const vaeb_ctx* c) { return c->c.Z <= 32; }
+// Weight-gradient tile widths (columns; rows are kWT = 64).  Narrower tiles mean more
+// workgroups, each streaming fewer theta / accumulator / panel bytes through its CU: at
+// MNIST-20, 64 -> 32 wide took the dW2 launch 11.7 -> 9.5 us and the dW3 | dW45 launch
+// 10.9 -> 8.1 us; 16 wide takes the latter to 7.5 us but the dW2 launch (beside 224 dhd
+// tiles) back up to 11.1 us.
+#ifndef VAEB_WTJ_P5
+#define VAEB_WTJ_P5 32
+#endif
+constexpr int kWTJ_P5 = VAEB_WTJ_P5;    // dW2 (| dW6), beside the dhd tiles
+#ifndef VAEB_W3_TS
+#define VAEB_W3_TS 1
+#endif
+constexpr int kW3TS = VAEB_W3_TS;       // 16-column groups per tile of the last launch (dW3 | dW45 | dW1)
+constexpr int kWTJ_P67 = 16;   // dW1, beside the dz / dh phase
+constexpr int kWTJ_W = 16;     // standalone launches: dW3 | dW45 (+ ELBO), non-fused dW1
+constexpr int kDzSplit = 8;    // P67 column splits per row block (fused.hpp dz_dh_body)
+
+// The deferred dW2's launch arguments (the previous step's dW2 (| dW6) group; vaeb_ctx::dw2_defer)
+struct W2Launch {
+    WGradArgs w;
+    bool vec;
+    const int* pend;
+};
+
 // The folded latent hand-offs: counted fixed-point atomics (latent.hpp fx_*) or slabs +
 // ticket + reducer.  The returning adds to one accumulator serialise at the memory side, so
 // the atomic form wins only at a small fan-in (contributors per element): Frey 560-200-2
@@ -262,7 +298,11 @@ int ho_mode(const vaeb_ctx* c, int fan_in) {
     return fan_in <= kFxMaxFanIn ? 1 : 0;   // the count field holds <= 16 contributors (latent.hpp)
 }
 int ho_ml(const vaeb_ctx* c, int ct) { return ho_mode(c, cdiv(c->c.H, 16 * ct)); }
-int ho_dz(const vaeb_ctx* c) { return ho_mode(c, cdiv(c->c.H, 16) * c->c.L); }
+// backward: 1 atomic, else 2 (deferred to the last launch's reducers, VAEB_BWD_DEFER) or 0 (ticket)
+int ho_dz(const vaeb_ctx* c) {
+    const int m = ho_mode(c, cdiv(c->c.H, 16) * c->c.L);
+    return m == 0 && c->bwd_defer ? 2 : m;
+}
 
 // Measurement brackets: mark(id) records an event before launch slot `id`.  With
 // reps > 1 (vaeb_profile_steps) every launch of the step is issued `reps` times back to
@@ -323,22 +363,22 @@ void launch_decout_z(hipStream_t s, dim3 grid, const StepArgs& a, int ct = 1) {
 // dhd_dz_wgrad_kernel at compile-time NCT (latent col tiles), GCH, load width, AT
 template <int TS, int HO>
 void launch_dhd_dz(hipStream_t s, dim3 grid, const PDhdT<true>& p5, const PDhdT<false>& p5s, const WGradArgs& w,
-                   int ntile, int gx, bool vec, bool deep) {
+                   int ntile, int gx, bool vec, bool deep, int* pend) {
     if (p5.a.Z <= 16) {
         if (deep) {
-            if (vec) hipLaunchKernelGGL((dhd_dz_wgrad_kernel<1, 8, true, TS, HO>), grid, dim3(512), 0, s, p5, w, ntile, gx);
-            else hipLaunchKernelGGL((dhd_dz_wgrad_kernel<1, 8, false, TS, HO>), grid, dim3(512), 0, s, p5s, w, ntile, gx);
+            if (vec) hipLaunchKernelGGL((dhd_dz_wgrad_kernel<1, 8, true, TS, HO>), grid, dim3(512), 0, s, p5, w, ntile, gx, pend);
+            else hipLaunchKernelGGL((dhd_dz_wgrad_kernel<1, 8, false, TS, HO>), grid, dim3(512), 0, s, p5s, w, ntile, gx, pend);
         } else {
-            if (vec) hipLaunchKernelGGL((dhd_dz_wgrad_kernel<1, 4, true, TS, HO>), grid, dim3(512), 0, s, p5, w, ntile, gx);
-            else hipLaunchKernelGGL((dhd_dz_wgrad_kernel<1, 4, false, TS, HO>), grid, dim3(512), 0, s, p5s, w, ntile, gx);
+            if (vec) hipLaunchKernelGGL((dhd_dz_wgrad_kernel<1, 4, true, TS, HO>), grid, dim3(512), 0, s, p5, w, ntile, gx, pend);
+            else hipLaunchKernelGGL((dhd_dz_wgrad_kernel<1, 4, false, TS, HO>), grid, dim3(512), 0, s, p5s, w, ntile, gx, pend);
         }
     } else {
         if (deep) {
-            if (vec) hipLaunchKernelGGL((dhd_dz_wgrad_kernel<2, 8, true, TS, HO>), grid, dim3(512), 0, s, p5, w, ntile, gx);
-            else hipLaunchKernelGGL((dhd_dz_wgrad_kernel<2, 8, false, TS, HO>), grid, dim3(512), 0, s, p5s, w, ntile, gx);
+            if (vec) hipLaunchKernelGGL((dhd_dz_wgrad_kernel<2, 8, true, TS, HO>), grid, dim3(512), 0, s, p5, w, ntile, gx, pend);
+            else hipLaunchKernelGGL((dhd_dz_wgrad_kernel<2, 8, false, TS, HO>), grid, dim3(512), 0, s, p5s, w, ntile, gx, pend);
         } else {
-            if (vec) hipLaunchKernelGGL((dhd_dz_wgrad_kernel<2, 4, true, TS, HO>), grid, dim3(512), 0, s, p5, w, ntile, gx);
-            else hipLaunchKernelGGL((dhd_dz_wgrad_kernel<2, 4, false, TS, HO>), grid, dim3(512), 0, s, p5s, w, ntile, gx);
+            if (vec) hipLaunchKernelGGL((dhd_dz_wgrad_kernel<2, 4, true, TS, HO>), grid, dim3(512), 0, s, p5, w, ntile, gx, pend);
+            else hipLaunchKernelGGL((dhd_dz_wgrad_kernel<2, 4, false, TS, HO>), grid, dim3(512), 0, s, p5s, w, ntile, gx, pend);
         }
     }
 }
@@ -363,11 +403,28 @@ void launch_enc_latent_ct(hipStream_t s, dim3 g1, const StepArgs& a, const FvFol
         else hipLaunchKernelGGL((enc_latent_kernel<2, 4, HO, CT>), g1, dim3(512), 0, s, a);
     }
 }
+// The 16-wave encoder with the deferred dW2 workers (w2: the previous step's dW2 group) in
+// ceil(ntile / 2 / (Mbp / 16)) extra grid rows.
+template <int HO, int CT>
+void launch_enc16_w2(hipStream_t s, dim3 g1, const StepArgs& a, const W2Launch& w2) {
+    const int rows = (int)g1.y;
+    const dim3 g(g1.x, g1.y + cdiv(cdiv(w2.w.total_wgs, 2), (int)g1.x));
+    constexpr int TS = kWTJ_P5 / 16;
+    if (a.Z <= 16) {
+        if (w2.vec) hipLaunchKernelGGL((enc_latent16_w2_kernel<1, 4, HO, CT, true, TS>), g, dim3(1024), 0, s, a, w2.w, w2.pend, rows);
+        else hipLaunchKernelGGL((enc_latent16_w2_kernel<1, 4, HO, CT, false, TS>), g, dim3(1024), 0, s, a, w2.w, w2.pend, rows);
+    } else {
+        if (w2.vec) hipLaunchKernelGGL((enc_latent16_w2_kernel<2, 4, HO, CT, true, TS>), g, dim3(1024), 0, s, a, w2.w, w2.pend, rows);
+        else hipLaunchKernelGGL((enc_latent16_w2_kernel<2, 4, HO, CT, false, TS>), g, dim3(1024), 0, s, a, w2.w, w2.pend, rows);
+    }
+}
+
 template <int HO>
 void launch_enc_latent(hipStream_t s, dim3 g1, const StepArgs& a, const FvFold& fvf, bool deep, int ct, bool e16,
-                       bool c16) {
+                       bool c16, const W2Launch* w2 = nullptr) {
     if constexpr (HO == 3) {   // slabs summed by the decoder launch: CT = 2 only, no FV stream
         if (e16) {   // 1024-thread workgroups, 16 waves splitting K (vaeb_ctx::enc16)
+            if (w2) { launch_enc16_w2<3, 2>(s, g1, a, *w2); return; }
             if (a.Z <= 16) hipLaunchKernelGGL((enc_latent16_kernel<1, 4, 3, 2>), g1, dim3(1024), 0, s, a);
             else hipLaunchKernelGGL((enc_latent16_kernel<2, 4, 3, 2>), g1, dim3(1024), 0, s, a);
             return;
@@ -382,6 +439,7 @@ void launch_enc_latent(hipStream_t s, dim3 g1, const StepArgs& a, const FvFold& 
         return;
     }
     if (HO == 1 && e16 && c16 && fvf.rows == 0 && ct == 1) {   // the atomic hand-off on 16 waves
+        if constexpr (HO == 1) if (w2) { launch_enc16_w2<1, 1>(s, g1, a, *w2); return; }
         if (a.Z <= 16) hipLaunchKernelGGL((enc_latent16_kernel<1, 4, 1, 1>), g1, dim3(1024), 0, s, a);
         else hipLaunchKernelGGL((enc_latent16_kernel<2, 4, 1, 1>), g1, dim3(1024), 0, s, a);
         return;
@@ -397,7 +455,21 @@ bool folded_latent(const vaeb_ctx* c, const StepArgs& a) {
 }
 
 // Forward phases P1..P4 for any mode.
-int enqueue_forward(vaeb_ctx* c, const StepArgs& a0, Prof& pr, const FvFold& fvf = FvFold{}) {
+// The encoder form the folded forward takes for `a` (enqueue_forward): ho (3 slabs summed by
+// the decoder, 1 counted atomics, 0 ticket), ct column tiles per workgroup; true when that
+// form runs on 16-wave workgroups (enc_latent16_kernel), the one that can carry the deferred dW2.
+bool enc_form(const vaeb_ctx* c, const StepArgs& a, const FvFold& fvf, int* ho_out, int* ct_out, bool* red_out) {
+    const bool red = (c->enc_red < 0 ? ho_ml(c, 1) == 0 : c->enc_red == 1) && fvf.rows == 0 && cdiv(a.H, 32) <= 32;
+    const int ct = (red || fvf.rows > 0) ? 2 : 1;
+    const int ho = red ? 3 : ho_ml(c, ct);
+    if (ho_out) *ho_out = ho;
+    if (ct_out) *ct_out = ct;
+    if (red_out) *red_out = red;
+    return (ho == 3 && c->enc16) || (ho == 1 && c->enc16 && c->enc16_at && fvf.rows == 0 && ct == 1);
+}
+
+int enqueue_forward(vaeb_ctx* c, const StepArgs& a0, Prof& pr, const FvFold& fvf = FvFold{},
+                    const W2Launch* w2 = nullptr) {
     hipStream_t s = c->s;
     StepArgs a = a0;
     a.dbg = next_dbg(c);
@@ -410,16 +482,16 @@ int enqueue_forward(vaeb_ctx* c, const StepArgs& a0, Prof& pr, const FvFold& fvf
         // ceil(H / 32) slabs (decout_z_kernel<.., ZM = 2>)
         // auto: where the slab + ticket form would be chosen (fan-in > 16; MNIST 784-500-20
         // 43.8 -> 42.5 us); at a small fan-in the counted atomics stay (Frey 30.8 vs 32.7 us)
-        const bool red = (c->enc_red < 0 ? ho_ml(c, 1) == 0 : c->enc_red == 1) && fvf.rows == 0 && cdiv(a.H, 32) <= 32;
-        const int ct = (red || fvf.rows > 0) ? 2 : 1;
+        int ho, ct;
+        bool red;
+        enc_form(c, a, fvf, &ho, &ct, &red);
         const dim3 g1(a.Mbp / 16, cdiv(a.H, 16 * ct) + fvf.rows);
         const bool deep = cdiv(cdiv(a.D, 16), 8) > 4;
-        const int ho = red ? 3 : ho_ml(c, ct);
         const int at = red ? 2 : (ho == 1 ? 1 : 0);
         pr.mark(16);
         REP(pr) {
-            if (ho == 3) launch_enc_latent<3>(s, g1, a, fvf, deep, ct, c->enc16, c->enc16_at);
-            else if (ho == 1) launch_enc_latent<1>(s, g1, a, fvf, deep, ct, c->enc16, c->enc16_at);
+            if (ho == 3) launch_enc_latent<3>(s, g1, a, fvf, deep, ct, c->enc16, c->enc16_at, w2);
+            else if (ho == 1) launch_enc_latent<1>(s, g1, a, fvf, deep, ct, c->enc16, c->enc16_at, w2);
             else launch_enc_latent<0>(s, g1, a, fvf, deep, ct, c->enc16, c->enc16_at);
         }
         CHECK_LAUNCH();
@@ -492,22 +564,18 @@ bool dhd_vec(const StepArgs& a) {
     return (a.D & 3) == 0 && al(a.dA2) && al(a.W2);
 }
 
-// Weight-gradient tile widths (columns; rows are kWT = 64).  Narrower tiles mean more
-// workgroups, each streaming fewer theta / accumulator / panel bytes through its CU: at
-// MNIST-20, 64 -> 32 wide took the dW2 launch 11.7 -> 9.5 us and the dW3 | dW45 launch
-// 10.9 -> 8.1 us; 16 wide takes the latter to 7.5 us but the dW2 launch (beside 224 dhd
-// tiles) back up to 11.1 us.
-#ifndef VAEB_WTJ_P5
-#define VAEB_WTJ_P5 32
-#endif
-constexpr int kWTJ_P5 = VAEB_WTJ_P5;    // dW2 (| dW6), beside the dhd tiles
-#ifndef VAEB_W3_TS
-#define VAEB_W3_TS 1
-#endif
-constexpr int kW3TS = VAEB_W3_TS;       // 16-column groups per tile of the last launch (dW3 | dW45 | dW1)
-constexpr int kWTJ_P67 = 16;   // dW1, beside the dz / dh phase
-constexpr int kWTJ_W = 16;     // standalone launches: dW3 | dW45 (+ ELBO), non-fused dW1
-constexpr int kDzSplit = 8;    // P67 column splits per row block (fused.hpp dz_dh_body)
+
+void set_head(WGradArgs& w, int n, int total, bool elbo, const float* xb, const int* cb, int64_t bs) {
+    w.ngroups = n; w.total_wgs = total; w.with_elbo = elbo; w.xbase = xb; w.cur_batch = cb; w.batch_stride = bs;
+}
+void set_head(WGradArgs3& w, int n, int total, bool elbo, const float* xb, const int* cb, int64_t bs) {
+    W3Head& h = w.hd;
+    h.ngroups = n; h.total_wgs = total; h.with_elbo = elbo; h.xbase = xb; h.cur_batch = cb; h.batch_stride = bs;
+    h.gb1 = n > 1 ? w.g[1].wg_begin : total; h.gb2 = n > 2 ? w.g[2].wg_begin : total;
+    h.nred = 0; h.red_cnt = nullptr;
+}
+int total_wgs(const WGradArgs& w) { return w.total_wgs; }
+int total_wgs(const WGradArgs3& w) { return w.hd.total_wgs; }
 
 // Weight-gradient arguments over `n` groups whose tiles start at block `base` of the
 // launch (+ the ELBO workgroup when e != nullptr).  *vec: 16-byte panel loads are legal.
@@ -526,12 +594,10 @@ int prep_wgrad(vaeb_ctx* c, const WGroup* groups, int n, const OptArgs& opt, con
         G.wg_end = begin + cdiv(G.rowsW + 1, kWT) * G.tiles_j;
         begin = G.wg_end;
     }
-    w.ngroups = n;
-    w.total_wgs = begin;
+    set_head(w, n, begin, e != nullptr, a.xbase, c->ictl + 1, a.batch_stride);
     w.opt = opt;
-    w.with_elbo = e != nullptr;
     if (e) w.elbo = *e;
-    w.xbase = a.xbase; w.cur_batch = c->ictl + 1; w.batch_stride = a.batch_stride; w.P = c->P;
+    w.P = c->P;
     w.dbg = a.dbg;
     // 16-byte panel loads need every panel row aligned with widths % 4 == 0 (the
     // activation buffers are hipMalloc'd; X rows are D floats apart)
@@ -565,13 +631,26 @@ int launch_wgrad(vaeb_ctx* c, hipStream_t s, const WGroup* groups, int n, const 
         int vm = 0;   // 16-byte panel loads per group (Frey: dW3 yes, dW4 | dW5 and dW1 not)
         if (int rc = prep_wgrad(c, groups, n, opt, e, a, 0, w, vec, 16 * kW3TS, &vm)) return rc;
         w.da3 = *da3;
-        const dim3 grid(w.total_wgs + (e ? 1 : 0));
-        switch (vm) {
-            case 7: hipLaunchKernelGGL((wgrad3_kernel<7, kW3TS>), grid, dim3(256), 0, s, w); break;
-            case 1: hipLaunchKernelGGL((wgrad3_kernel<1, kW3TS>), grid, dim3(256), 0, s, w); break;
-            case 3: hipLaunchKernelGGL((wgrad3_kernel<3, kW3TS>), grid, dim3(256), 0, s, w); break;
-            case 5: hipLaunchKernelGGL((wgrad3_kernel<5, kW3TS>), grid, dim3(256), 0, s, w); break;
-            default: hipLaunchKernelGGL((wgrad3_kernel<0, kW3TS>), grid, dim3(256), 0, s, w); break;
+        const int nred = da3->red.nred;
+        w.hd.nred = nred;
+        w.hd.red_cnt = da3->red.cnt;
+        const dim3 grid(w.hd.total_wgs + (e ? 1 : 0) + nred);
+        if (nred > 0) {
+            switch (vm) {
+                case 7: hipLaunchKernelGGL((wgrad3_kernel<7, kW3TS, true>), grid, dim3(256), 0, s, w); break;
+                case 1: hipLaunchKernelGGL((wgrad3_kernel<1, kW3TS, true>), grid, dim3(256), 0, s, w); break;
+                case 3: hipLaunchKernelGGL((wgrad3_kernel<3, kW3TS, true>), grid, dim3(256), 0, s, w); break;
+                case 5: hipLaunchKernelGGL((wgrad3_kernel<5, kW3TS, true>), grid, dim3(256), 0, s, w); break;
+                default: hipLaunchKernelGGL((wgrad3_kernel<0, kW3TS, true>), grid, dim3(256), 0, s, w); break;
+            }
+        } else {
+            switch (vm) {
+                case 7: hipLaunchKernelGGL((wgrad3_kernel<7, kW3TS, false>), grid, dim3(256), 0, s, w); break;
+                case 1: hipLaunchKernelGGL((wgrad3_kernel<1, kW3TS, false>), grid, dim3(256), 0, s, w); break;
+                case 3: hipLaunchKernelGGL((wgrad3_kernel<3, kW3TS, false>), grid, dim3(256), 0, s, w); break;
+                case 5: hipLaunchKernelGGL((wgrad3_kernel<5, kW3TS, false>), grid, dim3(256), 0, s, w); break;
+                default: hipLaunchKernelGGL((wgrad3_kernel<0, kW3TS, false>), grid, dim3(256), 0, s, w); break;
+            }
         }
     } else {
         WGradArgs w;
@@ -594,6 +673,42 @@ WGroup make_group(vaeb_ctx* c, const float* at, int ld_at, int klim, int at_is_x
     return G;
 }
 
+// The dW2 (| dW6) weight-gradient group -- [hd | 1]^T [dA2 (| dA6)] -- as launch arguments
+// whose tiles start at block `base`, with the optimizer `opt`.
+int w2_args(vaeb_ctx* c, const StepArgs& a, const OptArgs& opt, int base, WGradArgs& w, bool& vec) {
+    const bool gs = gaussian(c);
+    const int bo = gs ? 6 : 5;
+    WGroup g4 = make_group(c, c->hd, a.H, a.Me, 0, a.H, c->dA2, a.D, a.D, gs ? c->dA6 : nullptr, a.D, gs ? a.D : 0,
+                           a.Me, 4, bo + 4, gs ? 5 : -1, gs ? bo + 5 : -1);
+    return prep_wgrad(c, &g4, 1, opt, nullptr, a, base, w, vec, kWTJ_P5);
+}
+
+// Whether the step on `a` defers its dW2 into the next step's encoder launch (vaeb_ctx::dw2_defer).
+bool dw2_deferred(const vaeb_ctx* c, const StepArgs& a) {
+    const int est = c->c.estimator;
+    return c->dw2_defer && c->c.dtype == VAEB_DTYPE_F32 && c->comm == nullptr && est != VAEB_EST_FV && est != VAEB_EST_FVS &&
+           fused_latent(c) && c->fold_bwd && folded_latent(c, a) && enc_form(c, a, FvFold{}, nullptr, nullptr, nullptr);
+}
+
+// Run the pending step's dW2 (| dW6) + Adagrad now (their own launch; the device flag makes it
+// a no-op when a later step's encoder already ran them): every host read or write of the
+// parameters, the Adagrad state or the gradient, every evaluation, comes after it.
+int w2_flush(vaeb_ctx* c) {
+    if (!c || !c->w2_dirty) return 0;
+    c->w2_dirty = false;
+    const int par = c->par;   // the arena the next step reads: the pending dW2 writes W2' there
+    StepArgs a = make_args(c, par, c->c.B, MODE_TRAIN, c->data, true);
+    WGradArgs w;
+    bool vec;
+    if (int rc = w2_args(c, a, make_opt(c, par ^ 1, true, c->c.keep_grads != 0), 0, w, vec)) return rc;
+    w.dbg = nullptr;
+    if (vec) hipLaunchKernelGGL((w2_flush_kernel<true, kWTJ_P5 / 16>), dim3(w.total_wgs), dim3(512), 0, c->s, w, c->w2pend);
+    else hipLaunchKernelGGL((w2_flush_kernel<false, kWTJ_P5 / 16>), dim3(w.total_wgs), dim3(512), 0, c->s, w, c->w2pend);
+    CHECK_LAUNCH();
+    HIP_TRY(hipMemsetAsync(c->w2pend, 0, sizeof(int), c->s));
+    return 0;
+}
+
 // ------------------------------------------------------------------ DP gradient buckets
 // Arena order W3 W4 W5 W1 W2 [W6] b3 b4 b5 b1 b2 [b6] | SGVB.  Bucket A = W2 [| W6] is final
 // once the dW2 (| dW6) launch has run, early in the backward; bucket B = the rest plus the
@@ -608,56 +723,154 @@ WGroup make_group(vaeb_ctx* c, const float* at, int ld_at, int klim, int at_is_x
 // with a second branch; 78 vs 60 us) -- more than a 1.6-MB bucket's all-reduce can hide --
 // so it is the bf16 engine's default only, where bucket A is 34 MB (config 5) and its
 // Adagrad alone (37 us) pays for the fork already at world 1 (933 vs ~940 us).
-DpRange dp_range_a(const vaeb_ctx* c) {
+// Sharded form (vaeb_ctx::dp_shard, world > 1): instead of all-reducing the
+// whole bucket and running the replicated Adagrad over all of it on every rank, each rank
+// reduce-scatters the bucket, updates ITS 1/W shard (prior + Adagrad; bf16: + shadow), and the
+// shards of theta' are all-gathered: the same xGMI bytes as the all-reduce (a ring all-reduce
+// is a reduce-scatter + all-gather), the optimizer stream per rank W times shorter, and every
+// replica bitwise identical (theta' comes from one owner).  Shards are 64-element aligned; the
+// remainder of each run (< 64 W elements, and the SGVB slot) is all-reduced and updated on
+// every rank.  The arena is always partitioned into the same three runs -- B0 = [0, W2),
+// A = [W2, b3) (W2 | W6), B1 = [b3, P) -- so an element's owner (and its Adagrad state, kept
+// on the owner only) is the same whichever bucket form a step takes.
+struct DpBucket {
+    int nrun;
+    int64_t lo[3], n[3];
+    bool slot;   // + grad[P] (the SGVB), right after the run that ends at P (the last one)
+};
+DpBucket dp_bucket_a_runs(const vaeb_ctx* c) {
     const int bo = gaussian(c) ? 6 : 5;
-    return DpRange{c->off[4], c->off[bo] - c->off[4], 0, 0, 0};
+    return DpBucket{1, {c->off[4], 0, 0}, {c->off[bo] - c->off[4], 0, 0}, false};
 }
-DpRange dp_range_b(const vaeb_ctx* c) {
+DpBucket dp_bucket_b_runs(const vaeb_ctx* c) {
     const int bo = gaussian(c) ? 6 : 5;
-    return DpRange{0, c->off[4], c->off[bo], c->P - c->off[bo], 1};
+    return DpBucket{2, {0, c->off[bo], 0}, {c->off[4], c->P - c->off[bo], 0}, true};
 }
-DpRange dp_range_all(const vaeb_ctx* c) { return DpRange{0, c->P, 0, 0, 1}; }
+DpBucket dp_bucket_all_runs(const vaeb_ctx* c) {
+    const int bo = gaussian(c) ? 6 : 5;
+    return DpBucket{3, {0, c->off[4], c->off[bo]}, {c->off[4], c->off[bo] - c->off[4], c->P - c->off[bo]}, true};
+}
+// elements per rank of a run of n (0: the run is all-reduced and updated everywhere)
+int64_t dp_shard_len(const vaeb_ctx* c, int64_t n) { return c->dp_shard ? (n / c->world) & ~(int64_t)63 : 0; }
+// what this rank's optimizer launch updates: each run's own shard and its replicated remainder
+DpRange dp_opt_range(const vaeb_ctx* c, const DpBucket& bk) {
+    DpRange r{};
+    int k = 0;
+    for (int j = 0; j < bk.nrun; ++j) {
+        const int64_t S = dp_shard_len(c, bk.n[j]), tail = bk.n[j] - c->world * S;
+        if (S) { r.lo[k] = bk.lo[j] + c->rank * S; r.n[k++] = S; }
+        if (tail) { r.lo[k] = bk.lo[j] + c->world * S; r.n[k++] = tail; }
+    }
+    r.book = bk.slot ? 1 : 0;
+    return r;
+}
+// the elements of the bucket other ranks updated (their shards): the bf16 shadow fix
+DpRange dp_foreign_range(const vaeb_ctx* c, const DpBucket& bk) {
+    DpRange r{};
+    int k = 0;
+    for (int j = 0; j < bk.nrun; ++j) {
+        const int64_t S = dp_shard_len(c, bk.n[j]);
+        if (!S) continue;
+        if (c->rank > 0) { r.lo[k] = bk.lo[j]; r.n[k++] = c->rank * S; }
+        if (c->rank < c->world - 1) { r.lo[k] = bk.lo[j] + (c->rank + 1) * S; r.n[k++] = (c->world - c->rank - 1) * S; }
+    }
+    return r;
+}
 
+int nccl_ok(ncclResult_t r, const char* what) {
+    return r == ncclSuccess ? 0 : fail(VAEB_ERR_COMM, "%s: %s", what, ncclGetErrorString(r));
+}
 int nccl_sum(vaeb_ctx* c, float* p, int64_t n, hipStream_t st) {
-    ncclResult_t r = ncclAllReduce(p, p, (size_t)n, ncclFloat, ncclSum, c->comm, st);
-    if (r != ncclSuccess) return fail(VAEB_ERR_COMM, "ncclAllReduce: %s", ncclGetErrorString(r));
+    return nccl_ok(ncclAllReduce(p, p, (size_t)n, ncclFloat, ncclSum, c->comm, st), "ncclAllReduce");
+}
+
+// One bucket on stream st: the reduction (reduce-scatter of each run's shards + all-reduce of
+// the remainders and the slot, one RCCL group), this rank's optimizer launch, then (sharded)
+// the all-gather of theta' shards and fix(st, foreign range) for the bf16 shadow.  comm_done
+// (if any) is recorded after the bucket's last collective: another stream's collectives wait
+// for it (RCCL calls on one communicator stay serialised, in the same order on every rank).
+template <class Opt, class Fix>
+int dp_reduce_update(vaeb_ctx* c, hipStream_t st, const DpBucket& bk, float* theta_out, Opt opt, Fix fix,
+                     hipEvent_t comm_done, Prof* pr = nullptr, int opt_mark = -1) {
+    const int W = c->world, rk = c->rank;
+    bool sharded = false;
+    if (pr) pr->mark(8);
+    for (int rep = 0; rep < (pr ? pr->reps : 1); ++rep) {
+        if (int rc = nccl_ok(ncclGroupStart(), "ncclGroupStart")) return rc;
+        int rc = 0;
+        for (int j = 0; j < bk.nrun && !rc; ++j) {
+            const int64_t S = dp_shard_len(c, bk.n[j]);
+            const int64_t tail = bk.n[j] - W * S + ((bk.slot && j == bk.nrun - 1) ? 1 : 0);
+            float* g = c->grad + bk.lo[j];
+            if (S) {
+                sharded = true;
+                rc = nccl_ok(ncclReduceScatter(g, g + rk * S, (size_t)S, ncclFloat, ncclSum, c->comm, st),
+                             "ncclReduceScatter");
+            }
+            if (!rc && tail) rc = nccl_sum(c, g + W * S, tail, st);
+        }
+        const int re = nccl_ok(ncclGroupEnd(), "ncclGroupEnd");
+        if (rc) return rc;
+        if (re) return re;
+    }
+    if (comm_done && !sharded) HIP_TRY(hipEventRecord(comm_done, st));
+    if (pr) pr->mark(opt_mark);
+    for (int rep = 0; rep < (pr ? pr->reps : 1); ++rep)
+        if (int rc = opt(st, dp_opt_range(c, bk))) return rc;
+    if (!sharded) return 0;
+    if (int rc = nccl_ok(ncclGroupStart(), "ncclGroupStart")) return rc;
+    int rc = 0;
+    for (int j = 0; j < bk.nrun && !rc; ++j) {
+        const int64_t S = dp_shard_len(c, bk.n[j]);
+        float* t = theta_out + bk.lo[j];
+        if (S) rc = nccl_ok(ncclAllGather(t + rk * S, t, (size_t)S, ncclFloat, c->comm, st), "ncclAllGather");
+    }
+    const int re = nccl_ok(ncclGroupEnd(), "ncclGroupEnd");
+    if (rc) return rc;
+    if (re) return re;
+    if (comm_done) HIP_TRY(hipEventRecord(comm_done, st));
+    return fix(st, dp_foreign_range(c, bk));
+}
+
+// Sharded Adagrad keeps each element's accumulator on its owner only: gather the shards before
+// the host reads the state (vaeb_get_adagrad_state, vaeb_checkpoint_save; every rank calls it).
+int dp_gather_acc(vaeb_ctx* c) {
+    if (!c->comm || !c->dp_shard) return 0;
+    const DpBucket bk = dp_bucket_all_runs(c);
+    if (int rc = nccl_ok(ncclGroupStart(), "ncclGroupStart")) return rc;
+    int rc = 0;
+    for (int j = 0; j < bk.nrun && !rc; ++j) {
+        const int64_t S = dp_shard_len(c, bk.n[j]);
+        float* t = c->acc + bk.lo[j];
+        if (S) rc = nccl_ok(ncclAllGather(t + c->rank * S, t, (size_t)S, ncclFloat, c->comm, c->s), "ncclAllGather");
+    }
+    const int re = nccl_ok(ncclGroupEnd(), "ncclGroupEnd");
+    if (rc) return rc;
+    if (re) return re;
+    HIP_TRY(hipStreamSynchronize(c->s));
     return 0;
 }
 
-// after the dW2 (| dW6) launch: opt(stream, range) enqueues the optimizer over a range
-template <class Opt>
-int dp_bucket_a(vaeb_ctx* c, const Prof& pr, Opt opt) {
+// after the dW2 (| dW6) launch: opt(stream, range) enqueues the optimizer over a range,
+// fix(stream, range) the bf16 shadow of other ranks' shards (fp32: nothing)
+template <class Opt, class Fix>
+int dp_bucket_a(vaeb_ctx* c, const Prof& pr, float* theta_out, Opt opt, Fix fix) {
     if (pr.on || !c->dp_overlap) return 0;
-    const DpRange r = dp_range_a(c);
     HIP_TRY(hipEventRecord(c->dp_ev[0], c->s));
     HIP_TRY(hipStreamWaitEvent(c->s2, c->dp_ev[0], 0));
-    if (int rc = nccl_sum(c, c->grad + r.lo0, r.n0, c->s2)) return rc;
-    HIP_TRY(hipEventRecord(c->dp_ev[1], c->s2));
-    if (int rc = opt(c->s2, r)) return rc;
+    if (int rc = dp_reduce_update(c, c->s2, dp_bucket_a_runs(c), theta_out, opt, fix, c->dp_ev[1])) return rc;
     HIP_TRY(hipEventRecord(c->dp_ev[2], c->s2));
     return 0;
 }
 
 // after the last weight-gradient launch (the SGVB slot written)
-template <class Opt>
-int dp_bucket_b(vaeb_ctx* c, Prof& pr, int opt_mark, Opt opt) {
-    if (pr.on || !c->dp_overlap) {
-        pr.mark(8);
-        REP(pr) if (int rc = nccl_sum(c, c->grad, c->P + 1, c->s)) return rc;
-        pr.mark(opt_mark);
-        REP(pr) if (int rc = opt(c->s, dp_range_all(c))) return rc;
-        return 0;
-    }
-    const DpRange r = dp_range_b(c);
+template <class Opt, class Fix>
+int dp_bucket_b(vaeb_ctx* c, Prof& pr, int opt_mark, float* theta_out, Opt opt, Fix fix) {
+    if (pr.on || !c->dp_overlap)
+        return dp_reduce_update(c, c->s, dp_bucket_all_runs(c), theta_out, opt, fix, nullptr, pr.on ? &pr : nullptr,
+                                opt_mark);
     HIP_TRY(hipStreamWaitEvent(c->s, c->dp_ev[1], 0));
-    ncclResult_t g0 = ncclGroupStart();
-    if (g0 != ncclSuccess) return fail(VAEB_ERR_COMM, "ncclGroupStart: %s", ncclGetErrorString(g0));
-    int rc = nccl_sum(c, c->grad + r.lo0, r.n0, c->s);
-    rc = rc ? rc : nccl_sum(c, c->grad + r.lo1, r.n1 + 1, c->s);   // + the SGVB slot grad[P]
-    ncclResult_t g1 = ncclGroupEnd();
-    if (rc) return rc;
-    if (g1 != ncclSuccess) return fail(VAEB_ERR_COMM, "ncclGroupEnd: %s", ncclGetErrorString(g1));
-    if (int rc2 = opt(c->s, r)) return rc2;
+    if (int rc = dp_reduce_update(c, c->s, dp_bucket_b_runs(c), theta_out, opt, fix, nullptr)) return rc;
     HIP_TRY(hipStreamWaitEvent(c->s, c->dp_ev[2], 0));
     return 0;
 }
@@ -709,7 +922,18 @@ int enqueue_train_step(vaeb_ctx* c, int par, bool prof, bool fresh = true, int d
         n_fv = fvf.rows * (a.Mbp / 16);
         if (n_fv > kFvParts) return fail(VAEB_ERR_ARG, "internal: %d FV partials > %d", n_fv, kFvParts);
     }
-    if (int rc = enqueue_forward(c, a, pr, fvf)) return rc;
+    // the deferred dW2: the PREVIOUS step's dW2 (| dW6) rides this step's encoder launch --
+    // theta from the other arena, theta' into this step's (make_opt(par ^ 1)); this step's own
+    // dW2 is left pending for the next step (or a flush)
+    const bool w2d = dw2_deferred(c, a);
+    W2Launch w2{};
+    if (w2d) {
+        if (int rc = w2_args(c, a, make_opt(c, par ^ 1, true, g.keep_grads != 0), 0, w2.w, w2.vec)) return rc;
+        // (timeline build: the dW2 tiles stamp at logical ids 256 + tile of the encoder launch)
+        w2.w.dbg = c->dbg ? c->dbg + (size_t)c->dbg_slot * kDbgWG * 8 + 256 * 8 : nullptr;
+        w2.pend = c->w2pend;
+    }
+    if (int rc = enqueue_forward(c, a, pr, fvf, w2d ? &w2 : nullptr)) return rc;
     ElboArgs e = base_elbo(c, a);
     e.elbo_out = c->elbo_out; e.epoch = c->epoch; e.cursor = direct >= 0 ? nullptr : c->ictl; e.step = c->step;
 
@@ -736,7 +960,10 @@ int enqueue_train_step(vaeb_ctx* c, int par, bool prof, bool fresh = true, int d
     const bool gs = gaussian(c);
     const OptArgs dopt = make_opt(c, par, true, false);
     auto dp_opt = [&](hipStream_t st, const DpRange& r) -> int {
-        hipLaunchKernelGGL(adagrad_kernel, dim3(r.book ? 512 : 256), dim3(256), 0, st, dopt, c->P, r, e);
+        // (sharded: a 1/W share of the arena; the grid scales down with it)
+        const int64_t n = [&] { int64_t t = 0; for (int k = 0; k < kDpRuns; ++k) t += r.n[k]; return t; }();
+        const int nb = (int)std::max<int64_t>(1, std::min<int64_t>(r.book ? 512 : 256, cdiv(n, 256 * 8)));
+        hipLaunchKernelGGL(adagrad_kernel, dim3(nb), dim3(256), 0, st, dopt, c->P, r, e);
         CHECK_LAUNCH();
         return 0;
     };
@@ -757,16 +984,23 @@ int enqueue_train_step(vaeb_ctx* c, int par, bool prof, bool fresh = true, int d
         if (int rc = prep_wgrad(c, &g4, 1, opt, nullptr, a, ntile, w, vec, kWTJ_P5)) return rc;
         // the dhd loaders' 16-byte form needs D % 4 == 0 and aligned dA2 / W2 too
         vec = vec && dhd_vec(a);
+        int* pend = nullptr;
+        if (w2d) {   // no dW2 tiles here: the next step's encoder launch (or a flush) runs them
+            w.total_wgs = ntile;
+            pend = c->w2pend;
+        }
         const dim3 grid(w.total_wgs);
         const bool deep = cdiv(cdiv(p5.K, 16), 8) > 4;
         pr.mark(39);
         REP(pr) {
             switch (ho_dz(c)) {
-                case 1: launch_dhd_dz<kWTJ_P5 / 16, 1>(s, grid, p5, p5s, w, ntile, gx, vec, deep); break;
-                default: launch_dhd_dz<kWTJ_P5 / 16, 0>(s, grid, p5, p5s, w, ntile, gx, vec, deep); break;
+                case 1: launch_dhd_dz<kWTJ_P5 / 16, 1>(s, grid, p5, p5s, w, ntile, gx, vec, deep, pend); break;
+                case 2: launch_dhd_dz<kWTJ_P5 / 16, 2>(s, grid, p5, p5s, w, ntile, gx, vec, deep, pend); break;
+                default: launch_dhd_dz<kWTJ_P5 / 16, 0>(s, grid, p5, p5s, w, ntile, gx, vec, deep, pend); break;
             }
         }
         CHECK_LAUNCH();
+        if (w2d) c->w2_dirty = true;
     } else {
         WGroup g4 = make_group(c, c->hd, a.H, a.Me, 0, a.H, c->dA2, a.D, a.D, gs ? c->dA6 : nullptr, a.D, gs ? a.D : 0,
                                a.Me, 4, bo + 4, gs ? 5 : -1, gs ? bo + 5 : -1);
@@ -788,7 +1022,8 @@ int enqueue_train_step(vaeb_ctx* c, int par, bool prof, bool fresh = true, int d
         }
         CHECK_LAUNCH();
     }
-    if (dp) if (int rc = dp_bucket_a(c, pr, dp_opt)) return rc;
+    auto no_fix = [](hipStream_t, const DpRange&) -> int { return 0; };
+    if (dp) if (int rc = dp_bucket_a(c, pr, dopt.theta_out, dp_opt, no_fix)) return rc;
     // P67 (+ dW1 = [z|1]^T dA1 on the fused path): both need only P5's output
     if (!fold) {
         a.dbg = next_dbg(c);
@@ -833,7 +1068,15 @@ int enqueue_train_step(vaeb_ctx* c, int par, bool prof, bool fresh = true, int d
         if (dp || fvs) { e1.dp_slot = c->grad + c->P; e1.elbo_out = nullptr; e1.cursor = nullptr; e1.step = nullptr; }
         a.dbg = next_dbg(c);
         if (fold) {
-            const Da3Src d3{c->dMuLv, a.W4, a.W5, c->h, c->dA3, a.Z, a.H, a.Mb, a.Mbp};
+            Da3Src d3{c->dMuLv, a.W4, a.W5, c->h, c->dA3, a.Z, a.H, a.Mb, a.Mbp, LatRed{}};
+            if (ho_dz(c) == 2) {
+                // the deferred latent backward: ceil(Z / 8) column groups per 16-row block
+                LatRed& r = d3.red;
+                r.slab = c->slab_dz; r.mu = c->mu; r.lv = c->lv; r.eps = c->eps; r.z = c->z;
+                r.dZ = c->dZ; r.dml = c->dMuLv; r.cnt = c->cnt_dz; r.guard = c->blk + kBlkFxErr;
+                r.ngrp = cdiv(a.Z, 8); r.zg = cdiv(a.Z, r.ngrp); r.nred = (a.Mbp / 16) * r.ngrp;
+                r.nctH = cdiv(a.H, 16); r.L = a.L; r.est = a.est; r.Mb = a.Mb; r.Mbp = a.Mbp; r.Z = a.Z; r.sc = a.sc;
+            }
             pr.mark(40);
             REP(pr) if (int rc = launch_wgrad(c, s, g12, 3, opt, &e1, a, &d3)) return rc;
         } else {
@@ -854,7 +1097,7 @@ int enqueue_train_step(vaeb_ctx* c, int par, bool prof, bool fresh = true, int d
         hipLaunchKernelGGL(elbo_kernel, dim3(1), dim3(256), 0, s, e);
         CHECK_LAUNCH();
     }
-    if (dp) if (int rc = dp_bucket_b(c, pr, 9, dp_opt)) return rc;
+    if (dp) if (int rc = dp_bucket_b(c, pr, 9, dopt.theta_out, dp_opt, no_fix)) return rc;
     pr.mark(-1);
     c->prof_n = pr.k;
     return 0;
@@ -1017,6 +1260,8 @@ int vaeb_create(const vaeb_config* cfg, vaeb_ctx** out) {
     if (e != hipSuccess) { delete c; return fail(VAEB_ERR_HIP, "hipSetDevice(%d): %s", g.device, hipGetErrorString(e)); }
     e = hipStreamCreateWithFlags(&c->s, hipStreamNonBlocking);
     if (const char* fb = getenv("VAEB_FOLD_BWD")) c->fold_bwd = atoi(fb) != 0;
+    if (const char* bd = getenv("VAEB_BWD_DEFER")) c->bwd_defer = atoi(bd) != 0;
+    if (const char* wd = getenv("VAEB_DW2_DEFER")) c->dw2_defer = atoi(wd) != 0;
     if (const char* bk = getenv("VAEB_BF_FORK")) c->bf_fork = atoi(bk) != 0;
     if (const char* bt = getenv("VAEB_BF_THIN")) c->bf_thin = atoi(bt) & 3;
     if (const char* ah = getenv("VAEB_ATOMIC_HO")) c->atomic_ho = atoi(ah) != 0 ? 1 : 0;
@@ -1084,6 +1329,7 @@ int vaeb_create(const vaeb_config* cfg, vaeb_ctx** out) {
         rc = rc ? rc : dalloc(&c->slab_dz, (size_t)(g.L * Bp * nctH * 32));
         rc = rc ? rc : dalloc(&c->cnt_ml, (size_t)(Bp / 16));
         rc = rc ? rc : dalloc(&c->cnt_dz, (size_t)(Bp / 16));
+        rc = rc ? rc : dalloc(&c->w2pend, 1);
         // one allocation: the guard word the contributors set sits at acc_ml[-1] (latent.hpp fx_inc)
         const size_t nacc = (size_t)(Bp * 2 * Z * kFxStride);
         rc = rc ? rc : dalloc(&c->blk, kBlkAcc + 2 * nacc);
@@ -1196,6 +1442,7 @@ static int xfer(vaeb_ctx* c, float* dev, const float* hin, float* hout, int64_t 
     if (!c || (!hin && !hout)) return fail(VAEB_ERR_ARG, "null argument");
     if (!dev) return fail(VAEB_ERR_STATE, "state not allocated for this estimator");
     if (n != want) return fail(VAEB_ERR_ARG, "size mismatch: got %lld, expected %lld", (long long)n, (long long)want);
+    if (int rc = w2_flush(c)) return rc;   // a pending deferred dW2 first: the state is whole
     HIP_TRY(hipStreamSynchronize(c->s));
     if (hin) HIP_TRY(hipMemcpy(dev, hin, sizeof(float) * n, hipMemcpyHostToDevice));
     else HIP_TRY(hipMemcpy(hout, dev, sizeof(float) * n, hipMemcpyDeviceToHost));
@@ -1212,7 +1459,10 @@ int vaeb_set_params(vaeb_ctx* c, const float* f, int64_t n) {
 }
 int vaeb_get_params(vaeb_ctx* c, float* f, int64_t n) { return xfer(c, c ? c->theta2[c->par] : nullptr, nullptr, f, n, c ? c->P : 0); }
 int vaeb_set_adagrad_state(vaeb_ctx* c, const float* f, int64_t n) { return xfer(c, c ? c->acc : nullptr, f, nullptr, n, c ? c->P : 0); }
-int vaeb_get_adagrad_state(vaeb_ctx* c, float* f, int64_t n) { return xfer(c, c ? c->acc : nullptr, nullptr, f, n, c ? c->P : 0); }
+int vaeb_get_adagrad_state(vaeb_ctx* c, float* f, int64_t n) {
+    if (c) if (int rc = dp_gather_acc(c)) return rc;   // sharded DP: a collective (every rank calls)
+    return xfer(c, c ? c->acc : nullptr, nullptr, f, n, c ? c->P : 0);
+}
 int vaeb_get_grads(vaeb_ctx* c, float* f, int64_t n) { return xfer(c, c ? c->grad : nullptr, nullptr, f, n, c ? c->P : 0); }
 
 int vaeb_set_fv_state(vaeb_ctx* c, const float* mu, const float* sg, const float* am, const float* as, int64_t n) {
@@ -1393,6 +1643,7 @@ int vaeb_synchronize(vaeb_ctx* c) {
 // reads: the current theta, or for VAEB_EST_FVS the posterior mean mu_theta (copied into
 // the spare arena once per call).
 static int eval_arena(vaeb_ctx* c, int* epar) {
+    if (int rc = w2_flush(c)) return rc;
     *epar = c->par;
     if (c->c.estimator == VAEB_EST_FVS) {
         *epar = c->par ^ 1;
@@ -1572,6 +1823,8 @@ struct FileCloser { FILE* f; ~FileCloser() { if (f) fclose(f); } };
 
 int vaeb_checkpoint_save(vaeb_ctx* c, const char* path) {
     if (!c || !path) return fail(VAEB_ERR_ARG, "null argument");
+    if (int rc = w2_flush(c)) return rc;   // a pending deferred dW2 (vaeb_ctx::dw2_defer)
+    if (int rc = dp_gather_acc(c)) return rc;   // sharded DP: the whole Adagrad state (every rank calls)
     const vaeb_config& g = c->c;
     CkptHeader h{};
     memcpy(h.magic, kCkptMagic, 8);
@@ -1601,6 +1854,7 @@ int vaeb_checkpoint_save(vaeb_ctx* c, const char* path) {
 
 int vaeb_checkpoint_load(vaeb_ctx* c, const char* path) {
     if (!c || !path) return fail(VAEB_ERR_ARG, "null argument");
+    if (int rc = w2_flush(c)) return rc;   // a pending deferred dW2 (vaeb_ctx::dw2_defer)
     const vaeb_config& g = c->c;
     FileCloser fc{fopen(path, "rb")};
     if (!fc.f) return fail(VAEB_ERR_ARG, "checkpoint: cannot open %s", path);
@@ -1755,6 +2009,7 @@ int vaeb_comm_unique_id(uint8_t out_id[128]) {
 
 int vaeb_comm_init(vaeb_ctx* c, const uint8_t id_bytes[128], int32_t rank, int32_t world) {
     if (!c || !id_bytes || world <= 0 || rank < 0 || rank >= world) return fail(VAEB_ERR_ARG, "bad comm arguments");
+    if (int rc = w2_flush(c)) return rc;   // a pending deferred dW2 (vaeb_ctx::dw2_defer)
     if ((c->c.estimator == VAEB_EST_FV && world > 1) || c->c.estimator == VAEB_EST_FVS)
         return fail(VAEB_ERR_ARG, "the full-variational paths are single-rank");
     if (c->comm) return fail(VAEB_ERR_STATE, "communicator already initialised");
@@ -1769,6 +2024,9 @@ int vaeb_comm_init(vaeb_ctx* c, const uint8_t id_bytes[128], int32_t rank, int32
     // world 1 already (933 vs ~940 us per step), so it always forks.
     c->dp_overlap = is_bf16(c);
     if (const char* ov = getenv("VAEB_DP_OVERLAP")) c->dp_overlap = atoi(ov) != 0;
+    // sharded optimizer at world > 1 (dp_reduce_update); VAEB_DP_SHARD=1 forces it at world 1 (tests)
+    c->dp_shard = world > 1;
+    if (const char* sh = getenv("VAEB_DP_SHARD")) c->dp_shard = atoi(sh) != 0;
     if (!c->s2) {
         HIP_TRY(hipStreamCreateWithFlags(&c->s2, hipStreamNonBlocking));
         for (auto& ev : c->dp_ev) HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
@@ -1814,6 +2072,7 @@ int vaeb_get_activation(vaeb_ctx* c, const char* name, float* out, int64_t n) {
 int vaeb_profile_steps(vaeb_ctx* c, int32_t n_steps, float* out_ms, int32_t* out_ids, int32_t max_k,
                        int32_t* out_nk) {
     if (!c || !out_ms || n_steps <= 0) return fail(VAEB_ERR_ARG, "bad arguments");
+    if (int rc = w2_flush(c)) return rc;
     if (!c->data) return fail(VAEB_ERR_STATE, "no data");
     constexpr int kReps = 8;   // each launch issued 8x back to back inside its event bracket
     std::vector<int32_t> order((size_t)n_steps * kReps);
@@ -1848,6 +2107,7 @@ int vaeb_profile_steps(vaeb_ctx* c, int32_t n_steps, float* out_ms, int32_t* out
 
 int vaeb_debug_timeline(vaeb_ctx* c, int32_t batch_index, uint64_t* out, int64_t cap, int32_t* out_launches) {
     if (!c || !out) return fail(VAEB_ERR_ARG, "bad arguments");
+    if (int rc = w2_flush(c)) return rc;
     if (int rc = check_batches(c, &batch_index, 1)) return rc;
     const size_t n = (size_t)kMaxProfKernels * kDbgWG * 8;
     if (!c->dbg)

@@ -109,3 +109,37 @@ def comm_setup(ctx, dist, rank, world):
     if n != world:
         raise RuntimeError(f"rank {rank}: the RCCL communicator holds {n} ranks, expected {world}")
     return n
+
+
+def arena_runs(offsets, P, gaussian=False):
+    """The three runs the DP optimizer partitions the parameter arena into (vaeb_hip.hip
+    dp_bucket_all_runs): B0 = [0, W2), A = [W2, b3) (W2 | W6), B1 = [b3, P); `offsets` are
+    the arena offsets in reference order (W3 W4 W5 W1 W2 [W6] b3 ...)."""
+    bo = 6 if gaussian else 5
+    return [(0, offsets[4]), (offsets[4], offsets[bo] - offsets[4]), (offsets[bo], P - offsets[bo])]
+
+
+def shard_len(n, world, sharded=True):
+    """Elements per rank of a run of n (vaeb_hip.hip dp_shard_len): 64-aligned floor(n / world)."""
+    return (n // world) & ~63 if sharded else 0
+
+
+def shard_plan(runs, world, rank, sharded=True):
+    """Host mirror of the sharded optimizer's index plan (vaeb_hip.hip dp_reduce_update,
+    dp_opt_range, dp_foreign_range), for tests and the cost model.  Per run (lo, n):
+    reduce-scatter of world * S elements (this rank's shard [lo + rank S, +S)), all-reduce of
+    the remainder [lo + world S, lo + n); the optimizer updates the shard and the remainder;
+    the all-gather brings the other ranks' shards.  Returns (own, tails, foreign) as lists of
+    (lo, n) index runs."""
+    own, tails, foreign = [], [], []
+    for lo, n in runs:
+        S = shard_len(n, world, sharded)
+        if S:
+            own.append((lo + rank * S, S))
+            if rank > 0:
+                foreign.append((lo, rank * S))
+            if rank < world - 1:
+                foreign.append((lo + (rank + 1) * S, (world - rank - 1) * S))
+        if n - world * S:
+            tails.append((lo + world * S, n - world * S))
+    return own, tails, foreign
