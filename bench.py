@@ -76,6 +76,10 @@ def phase_flops(D, H, Z, B, L=1, gaussian=False):
         # last launch dW3 (dA3 formed in-workgroup) | dW45 | dW1
         "p5_dhd_dz_w2": 2 * L * B * D * H * g + 2 * L * B * H * Z + 2 * L * B * H * D * g,
         "p8_wgrad_w3w45w1": 2 * B * (D * H + H * 2 * Z) + 2 * B * 2 * Z * H + 2 * L * B * Z * H,
+        # deferred dW2 (round 4): the encoder launch also runs the previous step's dW2 tiles,
+        # the dhd launch has none
+        "p1_enc_latent_w2": 2 * B * D * H + 2 * B * H * 2 * Z + 2 * L * B * H * D * g,
+        "p5_dhd_dz": 2 * L * B * D * H * g + 2 * L * B * H * Z,
     }
 
 
@@ -98,8 +102,10 @@ KERNEL_SYMBOLS = {"p1_enc": "PEnc", "p23_heads_dechid": "heads_dechid_kernel", "
                   "bf_enc": ("gemm_kernel<0, 1,", "EpiBiasAct>"), "bf_decout": ("EpiDecOut<false>",),
                   "bf_dhd": ("gemm_kernel<0, 0,", "EpiDTanh>"), "bf_dW26": ("EpiAdagrad",),
                   "bf_dW3": ("EpiAdagrad",), "bf_dhd_dW26": ("gemm2_kernel",),
-                  "p5_dhd_dz_w2": "vaeb::dhd_dz_wgrad_kernel", "p8_wgrad_w3w45w1": "vaeb::wgrad3_kernel"}
-PMC_FILES = {c: os.path.join(ROOT, "profiles", "r3", f"pmc_{c}_per_launch.json")
+                  "p5_dhd_dz_w2": "vaeb::dhd_dz_wgrad_kernel", "p8_wgrad_w3w45w1": "vaeb::wgrad3_kernel",
+                  "p1_enc_latent_w2": ("vaeb::enc_latent16_w2",), "p5_dhd_dz": "vaeb::dhd_dz_wgrad_kernel"}
+PMC_ROUND = "r4"   # the round whose committed PMC passes give roofline.traffic (traffic_source)
+PMC_FILES = {c: os.path.join(ROOT, "profiles", PMC_ROUND, f"pmc_{c}_per_launch.json")
              for c in ("mnist", "frey", "fv", "fvs", "synth")}
 
 
@@ -491,6 +497,10 @@ def main(argv=None):
         "kernels_ms": {k: round(v, 5) for k, v in prof},
         "roofline": {"bound": bound, "kernel": dom[0], "achieved": achieved, "peak": peak,
                      "unit": unit, "frac": achieved / peak, "traffic": traffic,
+                     # traffic is not measured in this run: it is the committed rocprofv3 PMC pass
+                     # (FETCH_SIZE x 2 + WRITE_SIZE per launch, MI355X_MICROARCH.md) of this build
+                     "traffic_source": (os.path.relpath(PMC_FILES[args.config], ROOT)
+                                        if traffic is not None else None),
                      ("bytes_per_launch" if bound == "hbm" else "flops_per_launch"): fl[dom[0]],
                      "avg_launch_ms": dom[1]},
     }

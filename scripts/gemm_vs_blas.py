@@ -38,13 +38,15 @@ def blas_ms(M, N, K, ako, bko, reps=10):
 ctx = _lib.Context(64, 32, 8, 16, dtype=_lib.DTYPE_BF16)
 for name, M, N, K, ako, bko in SHAPES:
     fl = 2.0 * M * N * K
-    ours = {bn: [] for bn in (128, 256, 8)}
+    modes = (128, 256, 8, 9) if ako and bko else (128, 256, 8)   # 9: 8-phase, two K slices combined
+    ours = {bn: [] for bn in modes}
     blas = []
     for rnd in range(3):
-        for bn in (128, 256, 8):
+        for bn in modes:
             ours[bn].append(fl / (ctx.bench_gemm_bf16(ako, bko, M, N, K, bn, reps=10) * 1e-3) / 1e12)
         blas.append(fl / (blas_ms(M, N, K, ako, bko) * 1e-3) / 1e12)
     print(f"{name:14s} M={M} N={N} K={K}: ours bn128 {np.median(ours[128]):6.0f}  bn256 {np.median(ours[256]):6.0f}"
           f"  8-phase 256 {np.median(ours[8]):6.0f}"
+          + (f"  8-phase 2-slice {np.median(ours[9]):6.0f}" if 9 in ours else "") +
           f"  hipBLASLt {np.median(blas):6.0f} TF/s", flush=True)
 ctx.close()

@@ -412,3 +412,56 @@ def test_bf16_gemm8_step_matches_ring_step(monkeypatch):
     monkeypatch.setenv("VAEB_BF_GEMM8", "0")
     assert abs(out["0"][0] - out["1"][0]) <= 1e-6 * abs(out["0"][0])
     assert np.abs(out["0"][1] - out["1"][1]).max() <= 1e-6
+
+
+@pytest.mark.parametrize("ako,bko", [(1, 1), (0, 0), (0, 1)])
+@pytest.mark.parametrize("M,N,K", [(512, 512, 4096), (296, 520, 328), (768, 256, 1000), (200, 136, 64)])
+def test_gemm8_two_slices_combined_in_launch(gctx, ako, bko, M, N, K):
+    """Two K slices of every 256 x 256 tile combined inside the launch (split2_combine: the
+    first slice to finish publishes its fp32 partial, the second adds it and runs the
+    epilogue): partial tiles, K tails and an empty second slice (K = 64), same bound as the
+    other GEMM tests; the library also checks that every ticket is back at zero."""
+    rng = np.random.default_rng(7 * M + 3 * N + K + 10 * ako + 20 * bko)
+    A = rng.standard_normal((M, K)).astype(np.float32)
+    B = rng.standard_normal((K, N)).astype(np.float32)
+    As = A.T.copy() if ako else A
+    Bs = B if bko else B.T.copy()
+    C = gctx.test_gemm_bf16(As, Bs, ako, bko, M, N, K, -22)
+    Aq = O.bf16_round(A).astype(np.float64)
+    Bq = O.bf16_round(B).astype(np.float64)
+    ref = Aq @ Bq
+    bound = 1e-5 * (np.abs(Aq) @ np.abs(Bq)) + 1e-30
+    assert np.all(np.abs(C - ref) <= bound), float(np.max(np.abs(C - ref) / bound))
+    assert np.array_equal(C, gctx.test_gemm_bf16(As, Bs, ako, bko, M, N, K, -22))
+
+
+def test_bf16_split2_weight_gradients_agree(monkeypatch):
+    """The forked dW2 | dW6 and dW3 as two K slices combined in their launch
+    (VAEB_BF_SPLIT2=1; K = B = 4096 >= 2 x 32 K-tiles) against one full-depth slice: the
+    same products in another fp32 order, so 4 Philox steps agree to 1e-5 on the ELBO and to
+    a few Adagrad steps where a near-zero gradient's sign flips; the combined sum does not
+    depend on which slice finishes first, so graph replay and eager launches agree bitwise."""
+    from vaeb_amd import _lib
+    cfg = O.Config(D=512, H=256, Z=32)
+    B = 4096
+    x = (np.random.default_rng(8).random((4 * B, cfg.D)) < 0.4).astype(np.float32)
+    order = np.array([3, 1, 0, 2], np.int32)
+    out = {}
+    for s2 in ("1", "0"):
+        for use_graph in ((True, False) if s2 == "1" else (True,)):
+            monkeypatch.setenv("VAEB_BF_SPLIT2", s2)
+            ctx = _lib.Context(cfg.D, cfg.H, cfg.Z, B, max_eval_rows=B, dtype=_lib.DTYPE_BF16, use_graph=use_graph)
+            ctx.set_data(x)
+            ctx.set_params(O.flatten(O.init_params(cfg)))
+            ctx.set_eps_mode(_lib.EPS_PHILOX, 10)
+            ctx.set_step(0)
+            ctx.update_many(order)
+            s_, n_ = ctx.epoch_elbo()
+            out[s2, use_graph] = (s_ / n_, ctx.get_params())
+            ctx.close()
+    monkeypatch.setenv("VAEB_BF_SPLIT2", "0")
+    a, b = out["1", True], out["1", False]
+    assert a[0] == b[0] and np.array_equal(a[1], b[1])
+    u = out["0", True]
+    assert abs(a[0] - u[0]) <= 1e-5 * abs(u[0]), (a[0], u[0])
+    assert np.abs(a[1] - u[1]).max() <= 2 * len(order) * cfg.lr

@@ -382,7 +382,9 @@ def test_atomic_and_slab_handoffs_agree(kw, monkeypatch):
     one 16-column tile per Bernoulli decoder workgroup (VAEB_DECOUT_CT=1), the encoders on
     512-thread workgroups (VAEB_ENC16=0; =1: the atomic hand-off encoder only), the slab-form
     latent backward finished in the dhd launch (VAEB_BWD_DEFER=0) instead of the last launch,
-    and each step's dW2 in its own dhd launch (VAEB_DW2_DEFER=0) instead of the next encoder's.
+    each step's dW2 in its own dhd launch (VAEB_DW2_DEFER=0) instead of the next encoder's, and
+    the encoder's [mu | lv] partials as fp32 slabs summed by every decoder workgroup
+    (VAEB_ENC_FX=0) instead of exact fixed-point sums.
     They sum the same partials in different arithmetic (exact integer vs ordered fp32), so
     they agree to rounding, and each is bitwise deterministic (graph == eager)."""
     from vaeb_amd import _lib
@@ -403,7 +405,7 @@ def test_atomic_and_slab_handoffs_agree(kw, monkeypatch):
              "decred": ("1", "1", "1", "2", "2", "1", "1"), "unfolded": ("1", "0", "0", "2", "2", "1", "1"),
              "dct1": ("1", "0", "1", "1", "2", "1", "1"), "enc8": ("1", "1", "1", "2", "0", "1", "1"),
              "enc16slab": ("1", "0", "1", "2", "1", "1", "1"), "ticket": ("0", "0", "1", "2", "2", "0", "1"),
-             "dw2now": ("1", "0", "1", "2", "2", "1", "0")}
+             "dw2now": ("1", "0", "1", "2", "2", "1", "0"), "encslab": ("1", "0", "1", "2", "2", "1", "1", "0")}
     for mode in modes:
         for use_graph in (True, False):
             monkeypatch.setenv("VAEB_ATOMIC_HO", modes[mode][0])
@@ -413,6 +415,7 @@ def test_atomic_and_slab_handoffs_agree(kw, monkeypatch):
             monkeypatch.setenv("VAEB_ENC16", modes[mode][4])
             monkeypatch.setenv("VAEB_BWD_DEFER", modes[mode][5])
             monkeypatch.setenv("VAEB_DW2_DEFER", modes[mode][6])
+            monkeypatch.setenv("VAEB_ENC_FX", modes[mode][7] if len(modes[mode]) > 7 else "1")
             ctx = _lib.Context(cfg.D, cfg.H, cfg.Z, B, L=cfg.L,
                                decoder=_lib.DEC_GAUSSIAN if cfg.continuous else _lib.DEC_BERNOULLI,
                                max_eval_rows=B, use_graph=use_graph)
@@ -429,7 +432,7 @@ def test_atomic_and_slab_handoffs_agree(kw, monkeypatch):
         assert np.array_equal(out[mode, True][1], out[mode, False][1])
     es = out["slab", True][0]
     frac = {}
-    for mode in ("atomic", "decred", "unfolded", "dct1", "enc8", "enc16slab", "ticket", "dw2now"):
+    for mode in ("atomic", "decred", "unfolded", "dct1", "enc8", "enc16slab", "ticket", "dw2now", "encslab"):
         ea = out[mode, True][0]
         assert abs(ea - es) <= 1e-5 * abs(es), (mode, ea, es)
         d = np.abs(out[mode, True][1] - out["slab", True][1])

@@ -36,6 +36,7 @@
 // Epilogues are functors applied to the wave's accumulator block (128 x 64 or 64 x 64) in
 // registers.
 #pragma once
+#include <type_traits>
 #include "tile_engine.hpp"
 
 namespace vaeb {
@@ -182,6 +183,10 @@ struct GemmArgs {
     int M, N, K;
     int tiles_m, tiles_n;
     int kslice;    // K per split-K slice (multiple of BK); gridDim.y slices
+    // two-slice split-K combined in the launch (gemm8_body only, gridDim.y == 2): the first
+    // slice of a tile to finish stores its fp32 partial at part + tile * 65536, the second
+    // adds it and runs the epilogue; ticket[tile] orders them (zero between launches)
+    float* part; int* ticket;
 };
 
 // Bijective XCD-contiguous remap of the linear tile id (guide §5 template), then a
@@ -768,6 +773,55 @@ struct EpiAdagrad {
 //    tiles j = 0, 1 at columns wc 32 + 16 j, j = 2, 3 at 128 + wc 32 + 16 (j - 2)).
 DEV void vm_wait8() { asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); }
 
+// Two-slice split-K of one 256 x 256 tile, combined in the launch: a weight gradient with
+// only 128 tiles (config 5: dW2 | dW6, dW3; K = 8192) runs as 256 half-depth blocks, the
+// whole chip, instead of 128 full-depth ones.  No block ever waits for one that has not
+// reached this point: the first slice to arrive (ticket 0 -> 1) publishes its fp32 partial
+// and exits; the second (ticket 1 or 5) waits only for that publication (bit 4) and adds
+// it.  The sum is the same bits whichever slice comes first (fp32 a + b == b + a).
+// Hand-off (MI355X_MICROARCH.md, inter-workgroup visibility table, row 1): the partial is
+// stored sc1 (16 B per lane, each wave's registers as they stand: lane l of wave w holds the
+// same accumulator elements in both slices), every wave drains (vmcnt(0)), the workgroup
+// barrier, then one agent-scope add; the consumer polls from one lane, barrier, sc1 loads.
+// The consumer resets the ticket.  Returns true in the block that runs the epilogue.
+constexpr int kSplitFlag = 139264;   // LDS byte offset past the epilogue tile (lds8_bytes)
+DEV bool split2_combine(const GemmArgs& g, int tile, f32x4* acc, int wave, int lane, char* lds_flag) {
+    int* sflag = reinterpret_cast<int*>(lds_flag);
+    gint* tk = (gint*)(g.ticket + tile);
+    const rsrc_t pb = mkbuf(g.part + (int64_t)tile * 65536, 65536 * 4);
+    const uint32_t base = ((uint32_t)wave * 32 * 64 + (uint32_t)lane) * 16u;   // element q at base + q KiB
+    if (threadIdx.x == 0) *sflag = __hip_atomic_fetch_add(tk, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    const int old = *sflag;
+    if (old == 0) {
+#pragma unroll
+        for (int q = 0; q < 32; ++q) bst4x<16>(pb, base + q * 1024u, acc[q]);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (threadIdx.x == 0) __hip_atomic_fetch_add(tk, 4, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return false;
+    }
+    if (threadIdx.x == 0 && !(old & 4)) {
+        // bounded: the producer is past its main loop, storing 256 KiB
+        for (int n = 0; n < (1 << 22); ++n) {
+            if (__hip_atomic_load(tk, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 4) break;
+            __builtin_amdgcn_s_sleep(2);
+        }
+    }
+    __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // keep the partial's loads below the poll
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {   // two rounds of 16 loads in flight (register budget)
+        f32x4 p[16];
+#pragma unroll
+        for (int q = 0; q < 16; ++q) p[q] = bld4x<16>(pb, base + (16 * h + q) * 1024u);
+#pragma unroll
+        for (int q = 0; q < 16; ++q) acc[16 * h + q] += p[q];
+    }
+    if (threadIdx.x == 0) __hip_atomic_store(tk, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return true;
+}
+
 template <int LA, int LB, class Epi>
 DEV void gemm8_body(const GemmArgs& g, const Epi& e, int bid, int kz, char* smem) {
     constexpr int BK8 = 64, kBlock = 8192, kOperand = 4 * kBlock, kBuf = 2 * kOperand;
@@ -880,19 +934,27 @@ DEV void gemm8_body(const GemmArgs& g, const Epi& e, int bid, int kz, char* smem
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the out-of-range tail DMAs
     if (wr == 0) __builtin_amdgcn_s_barrier();          // re-align the groups' barrier counts
     __syncthreads();
+    if (g.part) {
+        if (!split2_combine(g, bid, &acc[0][0][0][0], wave, lane, smem + kSplitFlag)) return;
+        kz = 0;
+    }
     if constexpr (Epi::kIn) {
         e.template load_in<256>(m0, n0, smem);
         __syncthreads();
     }
-#pragma unroll
-    for (int ah = 0; ah < 2; ++ah) {
+    // the two row halves with compile-time indices (a runtime `ah` put the whole
+    // accumulator in scratch for the large epilogues)
+    auto half = [&](auto AH) {
+        constexpr int ah = decltype(AH)::value;
         f32x4 blk[4][4];
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
             for (int j = 0; j < 4; ++j) blk[i][j] = acc[ah][j >> 1][i][j & 1];
         e.template apply<256, Col8>(m0 + ah * 128 + wr * 64, n0 + wc * 32, blk, kz, smem);
-    }
+    };
+    half(std::integral_constant<int, 0>{});
+    half(std::integral_constant<int, 1>{});
     if constexpr (Epi::kOut) {
         __syncthreads();
         e.template store_out<256>(m0, n0, smem);
@@ -913,7 +975,9 @@ __global__ __launch_bounds__(NTHR, 2) void gemm8x2_kernel(GemmArgs g1, E1 e1, Ge
     else gemm8_body<LA2, LB2, E2>(g2, e2, b - nb1, 0, smem);
 }
 // dynamic LDS of gemm8_kernel: the two K-tile buffers, or the 256-wide epilogue tile
-constexpr int lds8_bytes() { return (2 * 65536 > BM * epitch<256>()) ? 2 * 65536 : BM * epitch<256>(); }
+// (+ 16 B: the split-K ticket value, kSplitFlag)
+constexpr int lds8_bytes() { return ((2 * 65536 > BM * epitch<256>()) ? 2 * 65536 : BM * epitch<256>()) + 16; }
+static_assert(BM * epitch<256>() == kSplitFlag && 2 * 65536 <= kSplitFlag, "split-K flag slot");
 
 }  // namespace bf
 }  // namespace vaeb

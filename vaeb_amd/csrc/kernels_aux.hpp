@@ -853,9 +853,23 @@ __global__ __launch_bounds__(256) void wgrad3_kernel(WGradArgs3 p) {
     }
     const int bid = xcd_remap(b, h.total_wgs);
     if (VAEB_DBG_ON(p.dbg) && threadIdx.x == 0) p.dbg[bid * 8 + 0] = __builtin_amdgcn_s_memrealtime();
-    if (bid >= h.gb2) wgrad_body<(VM & 4) != 0, 4, TS>(p, p.g[2], bid, sa, sb);
-    else if (bid >= h.gb1) wgrad_body<(VM & 2) != 0, 4, TS, false, DEFER>(p, p.g[1], bid, sa, sb);
-    else wgrad_body<(VM & 1) != 0, 4, TS, true, DEFER>(p, p.g[0], bid, sa, sb);
+    if (bid >= h.gb2) {
+        wgrad_body<(VM & 4) != 0, 4, TS>(p, p.g[2], bid, sa, sb);
+    } else if (bid >= h.gb1) {
+        wgrad_body<(VM & 2) != 0, 4, TS, false, DEFER>(p, p.g[1], bid, sa, sb);
+    } else {
+#ifdef VAEB_W3_HOIST
+        // the dW3 group's addressing fields and the optimizer's pointers as one burst of scalar
+        // loads (A/B build: the compiler otherwise fetches them in dependent waves)
+        const WGroup g0 = p.g[0];
+        asm volatile("" ::"s"(g0.ld_at), "s"(g0.klim_at), "s"(g0.rowsW), "s"(g0.b0), "s"(g0.ld0), "s"(g0.N0),
+                     "s"(g0.K), "s"(g0.offW0), "s"(g0.offb0), "s"(g0.tiles_j), "s"(g0.wg_begin), "s"(p.opt.theta_in),
+                     "s"(p.opt.acc), "s"(p.opt.theta_out), "s"(p.da3.dml), "s"(p.da3.h), "s"(p.da3.W4), "s"(p.da3.W5));
+        wgrad_body<(VM & 1) != 0, 4, TS, true, DEFER>(p, g0, bid, sa, sb);
+#else
+        wgrad_body<(VM & 1) != 0, 4, TS, true, DEFER>(p, p.g[0], bid, sa, sb);
+#endif
+    }
 }
 
 // ----------------------------------------------------------------- DP optimizer

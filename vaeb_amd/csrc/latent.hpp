@@ -33,7 +33,6 @@
 namespace vaeb {
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-typedef __attribute__((address_space(1))) int gint;
 
 DEV void st4_sc1(rsrc_t b, uint32_t off, f32x4 v) {
     __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), b, off, 0, 16);
@@ -151,6 +150,29 @@ DEV void fx_reset(uint64_t* p) { __hip_atomic_store((gu64*)p, 0ull, __ATOMIC_REL
 constexpr int kFxStride = 33;
 constexpr int kFxMaxFanIn = 16;
 DEV uint64_t* fx_at(uint64_t* base, int64_t e) { return base + e * kFxStride; }
+
+// The encoder -> decoder form at fan-in > 16 (HO 4): every contributor adds round(v 2^32) to a
+// plain 64-bit sum with a NO-RETURN atomic (contiguous [row][2Z] words, 128-B segments per
+// wave instruction) and the kernel boundary publishes the sums: exact and order-independent
+// like the counted form, but nobody waits for a count -- the decoder launch decodes them
+// (fx_sum_get) and a later launch of the step zeroes them.  Range: |v| < 2^17, so <= 16 ... 32
+// contributors stay below 2^54; an out-of-range / NaN partial adds POISON = 2^58 instead (and
+// sets the guard word), which decodes to NaN: 32 of them still fit below 2^63.
+constexpr int64_t kFxSumPoison = (int64_t)1 << 58;
+DEV void fx_sum_add(uint64_t* p, uint64_t* guard, float v) {
+    int64_t q;
+    if (__builtin_expect(!(__builtin_fabsf(v) < kFxMax), 0)) {
+        __hip_atomic_fetch_or((gu64*)guard, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        q = kFxSumPoison;
+    } else {
+        q = (int64_t)__builtin_rint((double)v * kFxScale);
+    }
+    __hip_atomic_fetch_add((gu64*)p, (unsigned long long)q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+DEV float fx_sum_get(uint64_t w) {
+    const int64_t q = (int64_t)w;
+    return (q >= kFxSumPoison / 2 || q <= -kFxSumPoison / 2) ? __builtin_nanf("") : (float)((double)q * (1.0 / kFxScale));
+}
 
 // A tile's 16 rows x 2Z partials (Z <= 32) are handed off by all 512 threads of its
 // workgroup, repacked through LDS so that no lane adds for a padding column: thread t takes
@@ -371,12 +393,19 @@ DEV void enc_latent_body(const StepArgs& a, const FvFold& fvf, f32x4* red_ext = 
                 // made visible by the kernel boundary
                 __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, sv), bs,
                                                        nz < Z ? (uint32_t)(((base + (w & 1) * Z + nz) * 16 + 4 * q) * 4) : kOOB, 0, 0);
+            } else if constexpr (HO == 4) {
+                // no-return fixed-point adds into the row block's [mu | lv] sums (fx_sum_inc), the
+                // decoder launch reads the exact sums (decout_z_kernel<.., ZM = 3>)
+                if (nz < Z)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r)
+                        fx_sum_add(a.acc_ml + (int64_t)(m0 + 4 * q + r) * 2 * Z + (w & 1) * Z + nz, a.acc_ml - 1, sv[r]);
             } else {
                 st4_sc1(bs, nz < Z ? (uint32_t)(((base + (w & 1) * Z + nz) * 16 + 4 * q) * 4) : kOOB, sv);
             }
         }
     }
-    if constexpr (HO == 3) {
+    if constexpr (HO == 3 || HO == 4) {
         VAEB_STAMP(a, 2);
         return;
     }
@@ -617,6 +646,14 @@ DEV void decout_z_body(const StepArgs& a) {
     // its own loads, not for the 25 weight-block loads behind them.
     constexpr int kSlabPer = 6;
     f32x4 sv0[ZM == 2 ? kSlabPer : 1];
+    // ZM 3: the row block's fixed-point [mu | lv] sums, [16 rows][2Z] 64-bit words: thread t <
+    // 16 Z loads one pair (16 bytes), issued before the weight block as the slab loads are
+    u32x4 fxp = {0u, 0u, 0u, 0u};
+    if constexpr (ZM == 3) {
+        const rsrc_t bfx = mkbuf(a.acc_ml, (int64_t)a.Mbp * 2 * a.Z * 8);
+        const uint32_t o = (int)threadIdx.x < 16 * a.Z ? (uint32_t)(((m0 % a.Mbp) * 2 * a.Z) * 8 + threadIdx.x * 16) : kOOB;
+        fxp = __builtin_amdgcn_raw_buffer_load_b128(bfx, o, 0, 0);
+    }
     const int nctS = (H + 31) >> 5, nf4S = 8 * Z;
     const int npS = 512 / nf4S;   // nf4 <= 256 (Z <= 32): np >= 2
     const int fS = (int)threadIdx.x % nf4S, partS = (int)threadIdx.x / nf4S;
@@ -640,7 +677,7 @@ DEV void decout_z_body(const StepArgs& a) {
         // and eps of one element (coalesced), the waves then read their fragments from LDS
         __shared__ float zs[16][33];
         __shared__ float gs[16][33];
-        __shared__ float msum[ZM == 2 ? 64 : 1][17];   // ZM 2: summed [mu | lv] slab, [column][row]
+        __shared__ float msum[ZM >= 2 ? 64 : 1][17];   // ZM 2 / 3: summed [mu | lv], [column][row]
         __shared__ f32x4 spart[ZM == 2 ? 512 : 1];      // ZM 2: per-partition slab sums
         const int per = 16 * Z;
         const int l = m0 / a.Mbp;                 // a 16-row block never straddles two planes
@@ -650,7 +687,7 @@ DEV void decout_z_body(const StepArgs& a) {
         // after the barrier starts from registers (they were dependent loads behind it)
         float b4p = 0.f, b5p = 0.f, epre = 0.f;
         int64_t stp = 0, grow0p = 0;
-        if constexpr (ZM == 2) {
+        if constexpr (ZM >= 2) {
             if ((int)threadIdx.x < per) {
                 const int ml = threadIdx.x / Z, j = threadIdx.x - ml * Z;
                 b4p = a.b4[j];
@@ -692,12 +729,21 @@ DEV void decout_z_body(const StepArgs& a) {
             __syncthreads();
             VAEB_STAMP(a, 6);   // (timeline build) slab sum done
         }
+        if constexpr (ZM == 3) {
+            if ((int)threadIdx.x < 16 * Z) {   // pair t: row t / Z, columns 2 (t % Z), + 1
+                const int r = (int)threadIdx.x / Z, c = 2 * ((int)threadIdx.x - r * Z);
+                msum[c][r] = fx_sum_get((uint64_t)fxp.x | ((uint64_t)fxp.y << 32));
+                msum[c + 1][r] = fx_sum_get((uint64_t)fxp.z | ((uint64_t)fxp.w << 32));
+            }
+            __syncthreads();
+            VAEB_STAMP(a, 6);
+        }
         if ((int)threadIdx.x < per) {
             const int ml = threadIdx.x / Z, j = threadIdx.x - ml * Z;
             const int i = i0 + ml;
             const bool rv = i < a.Mb;
             float mu, lv, e;
-            if constexpr (ZM == 2) {
+            if constexpr (ZM >= 2) {
                 mu = rv ? msum[j][ml] + b4p : 0.f;
                 lv = rv ? msum[Z + j][ml] + b5p : 0.f;
                 // eps as the encoder's reducer draws it (Philox keyed by the global row)

@@ -259,18 +259,32 @@ DEV void dhd_dz_body(const PDhdT<V>& p0, int bx, int by, f32x4* red, int sid) {
     VAEB_STAMP_AT(a, sid, 5);
 }
 
+// Side duties of the dhd launch.  pend (the deferred dW2: no dW2 tiles in this grid): set to 1
+// -- the next step's encoder launch, or the host's flush, runs this step's dW2 (| dW6)
+// (latent.hpp enc_latent16_w2_kernel).  zero[0 .. nzero): the encoder's fixed-point [mu | lv]
+// sums (latent.hpp fx_sum_add, HO 4), read by the decoder launch before this one; zeroed here
+// for the next step's encoder (plain stores, the kernel boundary publishes them).
+struct DhdAux {
+    int* pend;
+    uint64_t* zero;
+    int nzero;
+};
+
 // dhd (+ dZ slabs, latent backward) tiles and the dW2 (| dW6) weight-gradient tiles in one
 // grid.  The dhd tiles are dispatched first: with the latent backward behind them they are
 // the launch's critical path (tile_wgrad_kernel, without it, puts the dW2 blocks first).
 template <int NCT, int GCH, bool VEC, int TS, int HO>
-// pend (the deferred dW2: no dW2 tiles in this grid): set to 1 -- the next step's encoder
-// launch, or the host's flush, runs this step's dW2 (| dW6) (latent.hpp enc_latent16_w2_kernel)
-__global__ __launch_bounds__(512) void dhd_dz_wgrad_kernel(PDhdT<VEC> p, WGradArgs w, int ntile, int gx, int* pend) {
+// aux: side duties of the dhd launch (DhdAux)
+__global__ __launch_bounds__(512) void dhd_dz_wgrad_kernel(PDhdT<VEC> p, WGradArgs w, int ntile, int gx, DhdAux aux) {
     __shared__ float sa[kWKB][kWP];
     __shared__ float sb[kWKB][kWP];
     const int nwg = w.total_wgs - ntile;   // grid = w.total_wgs (no implicit-argument load)
     const int b0 = blockIdx.x;
-    if (pend && b0 == 0 && threadIdx.x == 0) *pend = 1;
+    if (aux.pend && b0 == 0 && threadIdx.x == 0) *aux.pend = 1;
+    if (aux.zero && b0 * 512 < aux.nzero) {
+        const int i = b0 * 512 + (int)threadIdx.x;
+        if (i < aux.nzero) aux.zero[i] = 0ull;
+    }
     const int bid = b0 < ntile ? xcd_remap(b0, ntile) : ntile + xcd_remap(b0 - ntile, nwg);
     if (bid < ntile) {
         dhd_dz_body<NCT, GCH, VEC, HO>(p, bid % gx, bid / gx, reinterpret_cast<f32x4*>(&sa[0][0]), bid);

@@ -623,6 +623,11 @@ struct BfState {
     bool thin_h = false, thin_z = false;   // heads / dz on the thin launches
     int nkl = 1;
     ShadowMap smap{};
+    // two-slice split-K of the forked weight gradients (gemm8_body, split2_combine): fp32
+    // partials [tiles][256 x 256] and tickets, dW2 (| dW6) at offset 0, dW3 after it
+    float* part = nullptr;
+    int* ticket = nullptr;
+    int t26 = 0, t3 = 0;              // their tile counts (0: that product is not split)
 };
 
 }  // namespace bf

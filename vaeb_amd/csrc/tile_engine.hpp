@@ -106,6 +106,7 @@ DEV int xcd_remap(int b, int n) {
 // loaded value, which keeps the load streams short and lets them all issue before the
 // first wait (the flat-pointer form of this code serialised behind vmcnt(0)).
 typedef __amdgpu_buffer_rsrc_t rsrc_t;
+typedef unsigned int v4u32 __attribute__((ext_vector_type(4)));
 constexpr uint32_t kOOB = 0x80000000u;  // every buffer here is < 2 GiB
 
 // The descriptor inputs go through readfirstlane so the compiler can PROVE them
@@ -125,6 +126,11 @@ template <int AUX>
 DEV float bldx(rsrc_t b, uint32_t off) { return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(b, off, 0, AUX)); }
 template <int AUX>
 DEV f32x4 bld4x(rsrc_t b, uint32_t off) { return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(b, off, 0, AUX)); }
+template <int AUX>
+DEV void bst4x(rsrc_t b, uint32_t off, f32x4 v) {
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u32, v), b, off, 0, AUX);
+}
+typedef __attribute__((address_space(1))) int gint;   // global int (agent-scope atomics)
 DEV void bst(rsrc_t b, uint32_t off, float v) { __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), b, off, 0, 0); }
 // Optimizer stores (theta', accumulator) are written through (sc1): the next launch reads
 // them from other XCDs anyway, and a launch that ends with megabytes of dirty L2 lines pays

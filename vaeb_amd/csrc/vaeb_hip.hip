@@ -92,7 +92,10 @@ const char* kKernelNames[] = {"p1_enc", "p2_heads", "p3_dechid", "p4_decout", "p
                               // folded latent backward (latent_bwd.hpp), ids 39..40
                               "p5_dhd_dz_w2", "p8_wgrad_w3w45w1",
                               // bf16 engine: dhd and dW2 (| dW6) in one grid, id 41
-                              "bf_dhd_dW26"};
+                              "bf_dhd_dW26",
+                              // deferred dW2 (round 4): the encoder launch carries the previous
+                              // step's dW2 tiles; the dhd launch has none, ids 42..43
+                              "p1_enc_latent_w2", "p5_dhd_dz"};
 
 }  // namespace
 
@@ -154,6 +157,7 @@ struct vaeb_ctx {
     hipEvent_t fk_ev[4] = {};     // fork after dhd, s3's work done, [dMu | dLv] ready, ELBO partials
     int bf_thin = 3;              // VAEB_BF_THIN mask: 1 heads, 2 dz on thin_bf16.hpp (0: split-K + latent kernels)
     bool bf_fork = true;          // VAEB_BF_FORK=0: dW2 in the dhd grid (bf_fuse) or after it
+    bool bf_split2 = false;       // VAEB_BF_SPLIT2: the forked dW2 / dW3 as two K slices (bf_wgrad256)
     hipStream_t s2 = nullptr;     // DP: the gradient buckets' all-reduces and their Adagrad
     hipEvent_t dp_ev[3] = {};     // fork after dW2, bucket A reduced, bucket A updated
     bool dp_overlap = false;      // bucket A on s2 (bf16 engine; VAEB_DP_OVERLAP=0/1 overrides)
@@ -163,6 +167,11 @@ struct vaeb_ctx {
     // reducer workgroups of the LAST launch (kernels_aux.hpp LatRed) instead of a ticket and
     // a last-arriver reducer in the dhd launch.  VAEB_BWD_DEFER=0: the ticketed form.
     bool bwd_defer = true;
+    // encoder -> decoder at fan-in > 16: the encoder adds its [mu | lv] partials as no-return
+    // fixed-point atomics (latent.hpp fx_sum_add, HO 4) and every decoder workgroup reads its
+    // row block's exact sums (5 KB) instead of summing 16 slabs (40 KB; ZM 3 instead of 2);
+    // the dhd launch zeroes the sums.  VAEB_ENC_FX=0: the slabs.
+    bool enc_fx = true;
     // the deferred dW2: dW2 (| dW6) + Adagrad of step t run in step t+1's encoder launch, on
     // the CUs the encoder leaves idle (latent.hpp enc_latent16_w2_kernel), so the dhd launch
     // holds the dhd tiles alone; host reads of the state flush a pending one first (w2_flush).
@@ -363,7 +372,7 @@ void launch_decout_z(hipStream_t s, dim3 grid, const StepArgs& a, int ct = 1) {
 // dhd_dz_wgrad_kernel at compile-time NCT (latent col tiles), GCH, load width, AT
 template <int TS, int HO>
 void launch_dhd_dz(hipStream_t s, dim3 grid, const PDhdT<true>& p5, const PDhdT<false>& p5s, const WGradArgs& w,
-                   int ntile, int gx, bool vec, bool deep, int* pend) {
+                   int ntile, int gx, bool vec, bool deep, DhdAux pend) {
     if (p5.a.Z <= 16) {
         if (deep) {
             if (vec) hipLaunchKernelGGL((dhd_dz_wgrad_kernel<1, 8, true, TS, HO>), grid, dim3(512), 0, s, p5, w, ntile, gx, pend);
@@ -422,19 +431,19 @@ void launch_enc16_w2(hipStream_t s, dim3 g1, const StepArgs& a, const W2Launch& 
 template <int HO>
 void launch_enc_latent(hipStream_t s, dim3 g1, const StepArgs& a, const FvFold& fvf, bool deep, int ct, bool e16,
                        bool c16, const W2Launch* w2 = nullptr) {
-    if constexpr (HO == 3) {   // slabs summed by the decoder launch: CT = 2 only, no FV stream
+    if constexpr (HO >= 3) {   // partials read by the decoder launch (3 slabs, 4 fixed-point sums): CT = 2, no FV
         if (e16) {   // 1024-thread workgroups, 16 waves splitting K (vaeb_ctx::enc16)
-            if (w2) { launch_enc16_w2<3, 2>(s, g1, a, *w2); return; }
-            if (a.Z <= 16) hipLaunchKernelGGL((enc_latent16_kernel<1, 4, 3, 2>), g1, dim3(1024), 0, s, a);
-            else hipLaunchKernelGGL((enc_latent16_kernel<2, 4, 3, 2>), g1, dim3(1024), 0, s, a);
+            if (w2) { launch_enc16_w2<HO, 2>(s, g1, a, *w2); return; }
+            if (a.Z <= 16) hipLaunchKernelGGL((enc_latent16_kernel<1, 4, HO, 2>), g1, dim3(1024), 0, s, a);
+            else hipLaunchKernelGGL((enc_latent16_kernel<2, 4, HO, 2>), g1, dim3(1024), 0, s, a);
             return;
         }
         if (a.Z <= 16) {
-            if (deep) hipLaunchKernelGGL((enc_latent_kernel<1, 8, 3, 2>), g1, dim3(512), 0, s, a);
-            else hipLaunchKernelGGL((enc_latent_kernel<1, 4, 3, 2>), g1, dim3(512), 0, s, a);
+            if (deep) hipLaunchKernelGGL((enc_latent_kernel<1, 8, HO, 2>), g1, dim3(512), 0, s, a);
+            else hipLaunchKernelGGL((enc_latent_kernel<1, 4, HO, 2>), g1, dim3(512), 0, s, a);
         } else {
-            if (deep) hipLaunchKernelGGL((enc_latent_kernel<2, 8, 3, 2>), g1, dim3(512), 0, s, a);
-            else hipLaunchKernelGGL((enc_latent_kernel<2, 4, 3, 2>), g1, dim3(512), 0, s, a);
+            if (deep) hipLaunchKernelGGL((enc_latent_kernel<2, 8, HO, 2>), g1, dim3(512), 0, s, a);
+            else hipLaunchKernelGGL((enc_latent_kernel<2, 4, HO, 2>), g1, dim3(512), 0, s, a);
         }
         return;
     }
@@ -461,11 +470,11 @@ bool folded_latent(const vaeb_ctx* c, const StepArgs& a) {
 bool enc_form(const vaeb_ctx* c, const StepArgs& a, const FvFold& fvf, int* ho_out, int* ct_out, bool* red_out) {
     const bool red = (c->enc_red < 0 ? ho_ml(c, 1) == 0 : c->enc_red == 1) && fvf.rows == 0 && cdiv(a.H, 32) <= 32;
     const int ct = (red || fvf.rows > 0) ? 2 : 1;
-    const int ho = red ? 3 : ho_ml(c, ct);
+    const int ho = red ? (c->enc_fx && c->fold_bwd ? 4 : 3) : ho_ml(c, ct);   // (the fold's dhd launch zeroes HO 4's sums)
     if (ho_out) *ho_out = ho;
     if (ct_out) *ct_out = ct;
     if (red_out) *red_out = red;
-    return (ho == 3 && c->enc16) || (ho == 1 && c->enc16 && c->enc16_at && fvf.rows == 0 && ct == 1);
+    return (ho >= 3 && c->enc16) || (ho == 1 && c->enc16 && c->enc16_at && fvf.rows == 0 && ct == 1);
 }
 
 int enqueue_forward(vaeb_ctx* c, const StepArgs& a0, Prof& pr, const FvFold& fvf = FvFold{},
@@ -487,10 +496,11 @@ int enqueue_forward(vaeb_ctx* c, const StepArgs& a0, Prof& pr, const FvFold& fvf
         enc_form(c, a, fvf, &ho, &ct, &red);
         const dim3 g1(a.Mbp / 16, cdiv(a.H, 16 * ct) + fvf.rows);
         const bool deep = cdiv(cdiv(a.D, 16), 8) > 4;
-        const int at = red ? 2 : (ho == 1 ? 1 : 0);
-        pr.mark(16);
+        const int at = red ? (ho == 4 ? 3 : 2) : (ho == 1 ? 1 : 0);
+        pr.mark(w2 ? 42 : 16);
         REP(pr) {
-            if (ho == 3) launch_enc_latent<3>(s, g1, a, fvf, deep, ct, c->enc16, c->enc16_at, w2);
+            if (ho == 4) launch_enc_latent<4>(s, g1, a, fvf, deep, ct, c->enc16, c->enc16_at, w2);
+            else if (ho == 3) launch_enc_latent<3>(s, g1, a, fvf, deep, ct, c->enc16, c->enc16_at, w2);
             else if (ho == 1) launch_enc_latent<1>(s, g1, a, fvf, deep, ct, c->enc16, c->enc16_at, w2);
             else launch_enc_latent<0>(s, g1, a, fvf, deep, ct, c->enc16, c->enc16_at);
         }
@@ -502,11 +512,13 @@ int enqueue_forward(vaeb_ctx* c, const StepArgs& a0, Prof& pr, const FvFold& fvf
         pr.mark(17);
         REP(pr) {
             if (gaussian(c)) {
-                if (at == 2) launch_decout_z<2, 2>(s, g4, a);
+                if (at == 3) launch_decout_z<2, 3>(s, g4, a);
+                else if (at == 2) launch_decout_z<2, 2>(s, g4, a);
                 else if (at == 1) launch_decout_z<2, 1>(s, g4, a);
                 else launch_decout_z<2, 0>(s, g4, a);
             } else {
-                if (at == 2) launch_decout_z<1, 2>(s, g4, a, dct);
+                if (at == 3) launch_decout_z<1, 3>(s, g4, a, dct);
+                else if (at == 2) launch_decout_z<1, 2>(s, g4, a, dct);
                 else if (at == 1) launch_decout_z<1, 1>(s, g4, a, dct);
                 else launch_decout_z<1, 0>(s, g4, a, dct);
             }
@@ -984,14 +996,20 @@ int enqueue_train_step(vaeb_ctx* c, int par, bool prof, bool fresh = true, int d
         if (int rc = prep_wgrad(c, &g4, 1, opt, nullptr, a, ntile, w, vec, kWTJ_P5)) return rc;
         // the dhd loaders' 16-byte form needs D % 4 == 0 and aligned dA2 / W2 too
         vec = vec && dhd_vec(a);
-        int* pend = nullptr;
+        DhdAux pend{nullptr, nullptr, 0};
         if (w2d) {   // no dW2 tiles here: the next step's encoder launch (or a flush) runs them
             w.total_wgs = ntile;
-            pend = c->w2pend;
+            pend.pend = c->w2pend;
+        }
+        int eho;
+        enc_form(c, a, FvFold{}, &eho, nullptr, nullptr);
+        if (eho == 4) {   // the encoder's fixed-point [mu | lv] sums, consumed by the decoder: zero them
+            pend.zero = c->acc_ml;
+            pend.nzero = a.Mbp * 2 * a.Z;
         }
         const dim3 grid(w.total_wgs);
         const bool deep = cdiv(cdiv(p5.K, 16), 8) > 4;
-        pr.mark(39);
+        pr.mark(w2d ? 43 : 39);
         REP(pr) {
             switch (ho_dz(c)) {
                 case 1: launch_dhd_dz<kWTJ_P5 / 16, 1>(s, grid, p5, p5s, w, ntile, gx, vec, deep, pend); break;
@@ -1261,8 +1279,10 @@ int vaeb_create(const vaeb_config* cfg, vaeb_ctx** out) {
     e = hipStreamCreateWithFlags(&c->s, hipStreamNonBlocking);
     if (const char* fb = getenv("VAEB_FOLD_BWD")) c->fold_bwd = atoi(fb) != 0;
     if (const char* bd = getenv("VAEB_BWD_DEFER")) c->bwd_defer = atoi(bd) != 0;
+    if (const char* ef = getenv("VAEB_ENC_FX")) c->enc_fx = atoi(ef) != 0;
     if (const char* wd = getenv("VAEB_DW2_DEFER")) c->dw2_defer = atoi(wd) != 0;
     if (const char* bk = getenv("VAEB_BF_FORK")) c->bf_fork = atoi(bk) != 0;
+    if (const char* b2 = getenv("VAEB_BF_SPLIT2")) c->bf_split2 = atoi(b2) != 0;
     if (const char* bt = getenv("VAEB_BF_THIN")) c->bf_thin = atoi(bt) & 3;
     if (const char* ah = getenv("VAEB_ATOMIC_HO")) c->atomic_ho = atoi(ah) != 0 ? 1 : 0;
     if (const char* er = getenv("VAEB_ENC_RED")) c->enc_red = atoi(er) != 0 ? 1 : 0;
@@ -2132,7 +2152,10 @@ int vaeb_debug_timeline(vaeb_ctx* c, int32_t batch_index, uint64_t* out, int64_t
 
 int vaeb_test_gemm_bf16(vaeb_ctx* c, int32_t ako, int32_t bko, int32_t M, int32_t N, int32_t K, const float* A,
                         const float* B, float* C, int32_t ksplit) {
-    // ksplit < 0: the 256 x 256 8-phase main loop (gemm8_kernel) with -ksplit slices
+    // ksplit < 0: the 256 x 256 8-phase main loop (gemm8_kernel) with -ksplit slices;
+    // -22: two slices combined in the launch (split2_combine), one output
+    const bool split2 = ksplit == -22;
+    if (split2) ksplit = -2;
     const bool force8 = ksplit < 0;
     if (force8) ksplit = -ksplit;
     if (!c || !A || !B || !C || M <= 0 || N <= 0 || K <= 0 || ksplit <= 0) return fail(VAEB_ERR_ARG, "bad arguments");
@@ -2148,6 +2171,13 @@ int vaeb_test_gemm_bf16(vaeb_ctx* c, int32_t ako, int32_t bko, int32_t M, int32_
     rc = rc ? rc : dalloc(&ba, na);
     rc = rc ? rc : dalloc(&bb, nb);
     rc = rc ? rc : dalloc(&fc, (size_t)nz * M * N);
+    float* part = nullptr;
+    int* ticket = nullptr;
+    const int tiles256 = cdiv(M, bf::BM) * cdiv(N, 256);
+    if (split2) {
+        rc = rc ? rc : dalloc(&part, (size_t)tiles256 * 65536);
+        rc = rc ? rc : dalloc(&ticket, (size_t)tiles256);
+    }
     if (!rc) {
         hipMemcpy(fa, A, na * 4, hipMemcpyHostToDevice);
         hipMemcpy(fb, B, nb * 4, hipMemcpyHostToDevice);
@@ -2158,6 +2188,11 @@ int vaeb_test_gemm_bf16(vaeb_ctx* c, int32_t ako, int32_t bko, int32_t M, int32_
         const int64_t ab = (int64_t)na * 2, bbytes = (int64_t)nb * 2;
         if (force8) {
             bf::GemmArgs g = bf_args256(ba, lda, ab, bb, ldb, bbytes, M, N, K, ksplit);
+            if (split2) {
+                g.part = part;
+                g.ticket = ticket;
+                g.kslice = ((cdiv(K, 2) + 63) / 64) * 64;
+            }
             if (!ako && !bko) rc = bf_launch8<bf::KC, bf::KC>(c->s, g, nz, e);
             else if (!ako && bko) rc = bf_launch8<bf::KC, bf::KO>(c->s, g, nz, e);
             else if (ako && !bko) rc = bf_launch8<bf::KO, bf::KC>(c->s, g, nz, e);
@@ -2178,7 +2213,13 @@ int vaeb_test_gemm_bf16(vaeb_ctx* c, int32_t ako, int32_t bko, int32_t M, int32_
             C[i] = v;
         }
     }
-    for (void* p : {(void*)fa, (void*)fb, (void*)fc, (void*)ba, (void*)bb}) if (p) hipFree(p);
+    if (!rc && split2) {   // every ticket back at zero
+        std::vector<int> tk(tiles256);
+        if (hipMemcpy(tk.data(), ticket, tk.size() * 4, hipMemcpyDeviceToHost) != hipSuccess)
+            rc = fail(VAEB_ERR_HIP, "test gemm: ticket copy");
+        for (int t : tk) if (!rc && t != 0) rc = fail(VAEB_ERR_HIP, "test gemm: split-K ticket left at %d", t);
+    }
+    for (void* p : {(void*)fa, (void*)fb, (void*)fc, (void*)ba, (void*)bb, (void*)part, (void*)ticket}) if (p) hipFree(p);
     return rc;
 }
 
@@ -2195,16 +2236,21 @@ __global__ __launch_bounds__(256) void fill_bf16_kernel(bf16_t* p, int64_t n, ui
 
 template <int LA, int LB>
 static int bench_gemm_launch(hipStream_t s, const bf16_t* A, const bf16_t* B, int M, int N, int K, int bn,
-                             const bf::EpiBiasAct& e) {
+                             const bf::EpiBiasAct& e, float* part, int* ticket) {
     bf::GemmArgs g{};
     g.A = A; g.lda = LA == bf::KO ? M : K; g.a_bytes = (int64_t)M * K * 2;
     g.B = B; g.ldb = LB == bf::KO ? N : K; g.b_bytes = (int64_t)N * K * 2;
     g.M = M; g.N = N; g.K = K;
     g.tiles_m = cdiv(M, bf::BM); g.tiles_n = cdiv(N, bn);
     g.kslice = ((K + bf::BK - 1) / bf::BK) * bf::BK;
-    if (bn == 8) {
+    if (bn == 8 || bn == 9) {
         g.tiles_n = cdiv(N, 256);
-        return bf_launch8<LA, LB>(s, g, 1, e);
+        if (bn == 9) {   // two K slices combined in the launch (split2_combine)
+            g.part = part;
+            g.ticket = ticket;
+            g.kslice = ((cdiv(K, 2) + 63) / 64) * 64;
+        }
+        return bf_launch8<LA, LB>(s, g, bn == 9 ? 2 : 1, e);
     }
     if (bn == 256) return bf_launch<LA, LB, 256>(s, g, 1, e);
     return bf_launch<LA, LB, 128>(s, g, 1, e);
@@ -2216,11 +2262,18 @@ int vaeb_bench_gemm_bf16(vaeb_ctx* c, int32_t ako, int32_t bko, int32_t M, int32
     if (!c || !out_ms || M <= 0 || N <= 0 || K <= 0 || reps <= 0) return fail(VAEB_ERR_ARG, "bad arguments");
     if (K % 8 || M % 8 || N % 8) return fail(VAEB_ERR_ARG, "bench gemm: M, N, K must be multiples of 8");
     if (bn == 0) bn = bf_bn(M, N);
-    if (bn != 128 && bn != 256 && bn != 8)
-        return fail(VAEB_ERR_ARG, "bench gemm: tile width 128 or 256 (8: 256 x 256 on the 8-phase loop)");
+    if (bn != 128 && bn != 256 && bn != 8 && bn != 9)
+        return fail(VAEB_ERR_ARG, "bench gemm: tile width 128 or 256 (8: 256 x 256 on the 8-phase loop, "
+                                  "9: the same as two K slices)");
     bf16_t *a = nullptr, *b = nullptr, *o = nullptr;
-    float* bias = nullptr;
+    float *bias = nullptr, *part = nullptr;
+    int* ticket = nullptr;
     int rc = 0;
+    if (bn == 9) {
+        const int tiles = cdiv(M, bf::BM) * cdiv(N, 256);
+        rc = rc ? rc : dalloc(&part, (size_t)tiles * 65536);
+        rc = rc ? rc : dalloc(&ticket, (size_t)tiles);
+    }
     rc = rc ? rc : dalloc(&a, (size_t)M * K);
     rc = rc ? rc : dalloc(&b, (size_t)N * K);
     rc = rc ? rc : dalloc(&o, (size_t)M * N);
@@ -2231,10 +2284,10 @@ int vaeb_bench_gemm_bf16(vaeb_ctx* c, int32_t ako, int32_t bko, int32_t M, int32
         hipLaunchKernelGGL(fill_bf16_kernel, dim3(1024), dim3(256), 0, c->s, b, (int64_t)N * K, 2u);
         const bf::EpiBiasAct e{bias, 0, M, N, o, N};
         auto one = [&]() {
-            if (!ako && !bko) return bench_gemm_launch<bf::KC, bf::KC>(c->s, a, b, M, N, K, bn, e);
-            if (!ako && bko) return bench_gemm_launch<bf::KC, bf::KO>(c->s, a, b, M, N, K, bn, e);
-            if (ako && !bko) return bench_gemm_launch<bf::KO, bf::KC>(c->s, a, b, M, N, K, bn, e);
-            return bench_gemm_launch<bf::KO, bf::KO>(c->s, a, b, M, N, K, bn, e);
+            if (!ako && !bko) return bench_gemm_launch<bf::KC, bf::KC>(c->s, a, b, M, N, K, bn, e, part, ticket);
+            if (!ako && bko) return bench_gemm_launch<bf::KC, bf::KO>(c->s, a, b, M, N, K, bn, e, part, ticket);
+            if (ako && !bko) return bench_gemm_launch<bf::KO, bf::KC>(c->s, a, b, M, N, K, bn, e, part, ticket);
+            return bench_gemm_launch<bf::KO, bf::KO>(c->s, a, b, M, N, K, bn, e, part, ticket);
         };
         rc = one();   // warm-up
         hipEventCreate(&e0);
@@ -2250,7 +2303,7 @@ int vaeb_bench_gemm_bf16(vaeb_ctx* c, int32_t ako, int32_t bko, int32_t M, int32
     }
     if (e0) hipEventDestroy(e0);
     if (e1) hipEventDestroy(e1);
-    for (void* p : {(void*)a, (void*)b, (void*)o, (void*)bias}) if (p) hipFree(p);
+    for (void* p : {(void*)a, (void*)b, (void*)o, (void*)bias, (void*)part, (void*)ticket}) if (p) hipFree(p);
     return rc;
 }
 
