@@ -166,3 +166,34 @@ def test_sharded_dp_optimizer_world1_is_bitwise_the_replicated_one(continuous, o
     for key, o in outs.items():
         assert o[0] == ref[0] and o[1] == ref[1], key
         assert np.array_equal(o[2], ref[2]) and np.array_equal(o[3], ref[3]), key
+
+
+@pytest.mark.parametrize("shard", ["0", "1"])
+def test_dp_eager_update_matches_graph_update_many(shard, monkeypatch):
+    """vaeb_update runs its step eagerly at any world size (and update_many's
+    first step is eager too), so the eager data-parallel step is a product path: with a
+    communicator (world 1; the sharded optimizer forced or not) one update(i) per batch
+    equals update_many(order) over graph replay bit for bit -- ELBO, theta, Adagrad state."""
+    from vaeb_amd import _lib
+    monkeypatch.setenv("VAEB_DP_SHARD", shard)
+    cfg = O.Config(D=784, H=500, Z=20)
+    x = O.synthetic_mnist(n=2000)
+    order = np.random.default_rng(3).permutation(20).astype(np.int32)
+    outs = []
+    for eager in (True, False):
+        ctx = _lib.Context(cfg.D, cfg.H, cfg.Z, 100, max_eval_rows=500)
+        ctx.comm_init(_lib.Context.comm_unique_id(), 0, 1)
+        ctx.set_data(x)
+        ctx.set_params(O.flatten(O.init_params(cfg)))
+        ctx.set_eps_mode(_lib.EPS_PHILOX, 10)
+        ctx.set_step(0)
+        if eager:
+            for i in order:
+                ctx.update(int(i))
+        else:
+            ctx.update_many(order)
+        s, n = ctx.epoch_elbo()
+        outs.append((s, n, ctx.get_params(), ctx.get_adagrad_state()))
+        ctx.close()
+    assert outs[0][:2] == outs[1][:2]
+    assert np.array_equal(outs[0][2], outs[1][2]) and np.array_equal(outs[0][3], outs[1][3])
