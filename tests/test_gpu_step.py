@@ -384,8 +384,7 @@ def test_atomic_and_slab_handoffs_agree(kw, monkeypatch):
     latent backward finished in the dhd launch (VAEB_BWD_DEFER=0) instead of the last launch,
     each step's dW2 in its own dhd launch (VAEB_DW2_DEFER=0) instead of the next encoder's, the
     encoder's [mu | lv] partials as exact fixed-point sums (VAEB_ENC_FX=1) instead of fp32 slabs
-    summed by every decoder workgroup, and the deferred latent backward recomputed by every
-    consumer from exact dZ sums (VAEB_BWD_FX=1) instead of by reducer workgroups.
+    summed by every decoder workgroup.
     They sum the same partials in different arithmetic (exact integer vs ordered fp32), so
     they agree to rounding, and each is bitwise deterministic (graph == eager)."""
     from vaeb_amd import _lib
@@ -403,14 +402,11 @@ def test_atomic_and_slab_handoffs_agree(kw, monkeypatch):
     # "dw2now": VAEB_DW2_DEFER=0, each step's dW2 (| dW6) in its own dhd launch (default 1: in the
     # next step's encoder launch, the last one flushed by get_params)
     # "encfx": VAEB_ENC_FX=1, the encoder's [mu | lv] as exact fixed-point sums read by the decoder
-    # "bwdfx": VAEB_BWD_FX=1, every dW3 / dW4 | dW5 workgroup recomputes [dMu | dLv] from the dhd
-    # launch's exact dZ sums (default: the deferred latent backward by reducer workgroups)
     modes = {"atomic": ("1", "0", "1", "2", "2", "1", "1"), "slab": ("0", "0", "1", "2", "2", "1", "1"),
              "decred": ("1", "1", "1", "2", "2", "1", "1"), "unfolded": ("1", "0", "0", "2", "2", "1", "1"),
              "dct1": ("1", "0", "1", "1", "2", "1", "1"), "enc8": ("1", "1", "1", "2", "0", "1", "1"),
              "enc16slab": ("1", "0", "1", "2", "1", "1", "1"), "ticket": ("0", "0", "1", "2", "2", "0", "1"),
-             "dw2now": ("1", "0", "1", "2", "2", "1", "0"), "encfx": ("1", "0", "1", "2", "2", "1", "1", "1"),
-             "bwdfx": ("1", "1", "1", "2", "2", "1", "1", "0", "1")}
+             "dw2now": ("1", "0", "1", "2", "2", "1", "0"), "encfx": ("1", "0", "1", "2", "2", "1", "1", "1")}
     for mode in modes:
         for use_graph in (True, False):
             monkeypatch.setenv("VAEB_ATOMIC_HO", modes[mode][0])
@@ -421,7 +417,6 @@ def test_atomic_and_slab_handoffs_agree(kw, monkeypatch):
             monkeypatch.setenv("VAEB_BWD_DEFER", modes[mode][5])
             monkeypatch.setenv("VAEB_DW2_DEFER", modes[mode][6])
             monkeypatch.setenv("VAEB_ENC_FX", modes[mode][7] if len(modes[mode]) > 7 else "0")
-            monkeypatch.setenv("VAEB_BWD_FX", modes[mode][8] if len(modes[mode]) > 8 else "0")
             ctx = _lib.Context(cfg.D, cfg.H, cfg.Z, B, L=cfg.L,
                                decoder=_lib.DEC_GAUSSIAN if cfg.continuous else _lib.DEC_BERNOULLI,
                                max_eval_rows=B, use_graph=use_graph)
@@ -438,7 +433,7 @@ def test_atomic_and_slab_handoffs_agree(kw, monkeypatch):
         assert np.array_equal(out[mode, True][1], out[mode, False][1])
     es = out["slab", True][0]
     frac = {}
-    for mode in ("atomic", "decred", "unfolded", "dct1", "enc8", "enc16slab", "ticket", "dw2now", "encfx", "bwdfx"):
+    for mode in ("atomic", "decred", "unfolded", "dct1", "enc8", "enc16slab", "ticket", "dw2now", "encfx"):
         ea = out[mode, True][0]
         assert abs(ea - es) <= 1e-5 * abs(es), (mode, ea, es)
         d = np.abs(out[mode, True][1] - out["slab", True][1])

@@ -262,25 +262,7 @@ struct WGroup {
 // latent.hpp arrive_last cites.  The counter is zeroed by the dhd launch (a plain store the
 // boundary publishes).  The poll is bounded: a timeout sets the guard word (reported as a
 // step status) instead of hanging the GPU.
-// Exact fixed-point sums (latent.hpp fx_sum_add): round(v 2^32) added in 64-bit two's
-// complement; a poisoned (out-of-range / NaN) contributor adds 2^58, which decodes to NaN.
-constexpr double kFxScale = 4294967296.0;   // 2^32
-constexpr int64_t kFxSumPoison = (int64_t)1 << 58;
-DEV float fx_sum_get(uint64_t w) {
-    const int64_t q = (int64_t)w;
-    return (q >= kFxSumPoison / 2 || q <= -kFxSumPoison / 2) ? __builtin_nanf("") : (float)((double)q * (1.0 / kFxScale));
-}
-// The same decode in fp32 arithmetic only (hi + lo 2^-32: two roundings instead of one, but a
-// fixed function of the integer sum, so every workgroup still gets the same bits)
-DEV float fx_sum_get32(uint32_t lo, uint32_t hi) {
-    const int h = (int)hi;
-    const float v = (float)h + (float)lo * 2.3283064365386963e-10f;   // 2^-32
-    return (h >= (1 << 25) || h <= -(1 << 25)) ? __builtin_nanf("") : v;
-}
-
 struct LatRed {
-    const uint64_t* fx;                // DEFER 2: [L][Mbp][Z] exact dZ sums (dhd launch, HO 3)
-    const float* aux;                  // DEFER 2: [L][Mbp][Z] float4 dZ-free terms (StepArgs::lat_aux)
     const float* slab;                 // [L][nrb][nctH][Z][16] partial dZ slabs
     const float *mu, *lv, *eps, *z;    // [Mbp][Z]; [L][Mbp][Z]
     float* dZ;                         // [L][Mbp][Z] (kept for inspection, as the ticketed form)
@@ -408,85 +390,6 @@ DEV void lat_wait(int* cnt, int nred, uint64_t* const* guard) {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // keeps the sc1 loads below the poll
 }
 
-// DEFER 2 -- the latent backward recomputed by every consumer workgroup instead of handed off:
-// the dhd launch adds each tile's dZ partials into exact fixed-point sums (latent_bwd.hpp HO 3),
-// the kernel boundary publishes them, and each dW3 / dW4 | dW5 workgroup forms the [dMu | dLv]
-// rows it needs itself -- no reducer workgroups, no counter, no poll.  The same integer sums
-// and the same code in every workgroup: every copy is the same bits (and the integer sum does
-// not depend on the order the dhd tiles added in).
-// Rows [kb, kb + kWKB) x columns [c0, c0 + nc) of [dMu | dLv] into tb[row - kb][col - c0]
-// (zero past Mb; nc <= kWP).  All loads of the (row, latent) pairs a thread owns go out before
-// the first use (one round trip; Z <= 32, so <= 16 pairs per thread).  dml: the workgroup
-// that also stores the rows to global memory (kept for inspection), or nullptr.
-DEV void dml_table(const LatRed& r, int kb, int c0, int nc, float (*tb)[kWP], float* dml) {
-    constexpr int NS = 8;   // pairs per thread per round trip (MNIST: 100 x 20 pairs, one round)
-    const int Z = r.Z;
-    const int rows = max(0, min(kWKB, r.Mb - kb));
-    const int np = rows * Z;
-    const rsrc_t bf = mkbuf(r.fx, (int64_t)r.L * r.Mbp * Z * 8);
-    const rsrc_t bx = mkbuf(r.aux, (int64_t)r.L * r.Mbp * Z * 16);
-    // pair e = (row ml, latent j), e = threadIdx.x + 256 u: stepped by 256 without divisions
-    const int qz = 256 / Z, rz = 256 - qz * Z;
-    int ml0 = (int)threadIdx.x / Z, jn0 = (int)threadIdx.x - ml0 * Z;
-    for (int base = 0; base < np; base += 256 * NS) {
-        uint32_t flo[NS], fhi[NS];
-        f32x4 axv[NS];
-        int ml = ml0, j = jn0;
-#pragma unroll
-        for (int u = 0; u < NS; ++u) {
-            const bool ok = base + (int)threadIdx.x + 256 * u < np;
-            const uint32_t o = (uint32_t)((kb + ml) * Z + j);
-#ifdef VAEB_DBG_NOFX   // (timing-only build: the sums not read)
-            flo[u] = fhi[u] = 0u;
-#else
-            const auto w = __builtin_amdgcn_raw_buffer_load_b64(bf, ok ? o * 8u : kOOB, 0, 0);
-            flo[u] = w[0];
-            fhi[u] = w[1];
-#endif
-            axv[u] = bld4(bx, ok ? o * 16u : kOOB);
-            j += rz;
-            ml += qz + (j >= Z ? 1 : 0);
-            j -= j >= Z ? Z : 0;
-        }
-        ml = ml0;
-        j = jn0;
-#pragma unroll
-        for (int u = 0; u < NS; ++u) {
-            if (base + (int)threadIdx.x + 256 * u < np) {
-                const int m = kb + ml;
-                // dMu = sum_l (dZ_l - c_mu,l), dLv = sum_l (dZ_l (eps_l sd / 2) + c_lv,l)
-                const float dz = fx_sum_get32(flo[u], fhi[u]);
-                float dmu = dz - axv[u][1];
-                float dlv = dz * axv[u][0] + axv[u][2];
-                for (int l = 1; l < r.L; ++l) {   // further sample planes (not prefetched)
-                    const int64_t ol = ((int64_t)l * r.Mbp + m) * Z + j;
-                    const uint64_t wl = r.fx[ol];
-                    const float dzl = fx_sum_get32((uint32_t)wl, (uint32_t)(wl >> 32));
-                    const f32x4 al = reinterpret_cast<const f32x4*>(r.aux)[ol];
-                    dmu += dzl - al[1];
-                    dlv += dzl * al[0] + al[2];
-                }
-                if (j - c0 >= 0 && j - c0 < nc) tb[ml][j - c0] = dmu;
-                if (Z + j - c0 >= 0 && Z + j - c0 < nc) tb[ml][Z + j - c0] = dlv;
-                if (dml) {
-                    dml[(int64_t)m * 2 * Z + j] = dmu;
-                    dml[(int64_t)m * 2 * Z + Z + j] = dlv;
-                }
-            }
-            j += rz;
-            ml += qz + (j >= Z ? 1 : 0);
-            j -= j >= Z ? Z : 0;
-        }
-        ml0 = ml;
-        jn0 = j;
-    }
-    // rows past the minibatch: zeros (the bias row of dW4 | dW5 sums the panel's padding rows)
-    for (int e = (int)threadIdx.x; e < (kWKB - rows) * nc; e += 256) tb[rows + e / nc][e % nc] = 0.f;
-    if (dml)
-        for (int e = (int)threadIdx.x; e < 2 * Z * max(0, min(kWKB, r.Mbp - kb) - rows); e += 256)
-            dml[(int64_t)(kb + rows) * 2 * Z + e] = 0.f;
-}
-
 // Kernel arguments of a weight-gradient launch: up to two groups (WGradArgs), or the three
 // groups + dA3 source of the folded latent backward's last launch (WGradArgs3).  Separate
 // types because the kernarg size shows in every launch that takes it (the 3-group form as
@@ -548,11 +451,8 @@ DEV f32x4 ld_w45(rsrc_t bw4, rsrc_t bw5, int Z, int H, int n, int k, bool vz) {
 // a per-block load -> MFMA loop cost the launch a second one), the [W4 | W5]^T slice once.
 // DEFER (the deferred latent backward, LatRed): [dMu | dLv] is produced in this launch, so its
 // loads wait for the reducers' counter and are sc1; the W4 / W5 and h loads go out first.
-// DEFER 2: [dMu | dLv] was recomputed by the caller (dml_table) into tbuf -- the A panel's
-// LDS, free until the caller stores the X panel there, after the barrier that ends this.
-template <int NWV, int TS, int DEFER = 0>
-DEV void da3_panel(const Da3Src& d, int kb, int j0, bool store, float (*sb)[kWP], int* cnt = nullptr, int nred = 0,
-                   float (*tbuf)[kWP] = nullptr) {
+template <int NWV, int TS, bool DEFER = false>
+DEV void da3_panel(const Da3Src& d, int kb, int j0, bool store, float (*sb)[kWP], int* cnt = nullptr, int nred = 0) {
     constexpr int NR = kWKB / 16 / NWV;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int li = lane & 15, q = lane >> 4;
@@ -572,7 +472,7 @@ DEV void da3_panel(const Da3Src& d, int kb, int j0, bool store, float (*sb)[kWP]
     for (int u = 0; u < NR; ++u) {
         const int r0 = kb + 16 * (wv + NWV * u);
         const int rl = r0 < d.Mbp ? d.Mbp : 0;   // blocks past the padded batch load nothing
-        if constexpr (DEFER == 0)
+        if constexpr (!DEFER)
 #pragma unroll
             for (int c = 0; c < 4; ++c) av[u][c] = kc4(bd, K2, r0 + li, c * 16 + 4 * q, c < nkc ? rl : 0, K2, vd);
 #pragma unroll
@@ -585,21 +485,7 @@ DEV void da3_panel(const Da3Src& d, int kb, int j0, bool store, float (*sb)[kWP]
             }
         }
     }
-    if constexpr (DEFER == 2) {   // (the table was built by wgrad_body before the X panel loads)
-#pragma unroll
-        for (int u = 0; u < NR; ++u) {
-            const int rr = 16 * (wv + NWV * u) + li;   // table row (kb-relative)
-#pragma unroll
-            for (int c = 0; c < 4; ++c) {
-                const int k = c * 16 + 4 * q;
-                f32x4 v;
-#pragma unroll
-                for (int s = 0; s < 4; ++s) v[s] = (c < nkc && k + s < K2) ? tbuf[rr][k + s] : 0.f;
-                av[u][c] = v;
-            }
-        }
-        __syncthreads();   // every wave's table reads are done before tbuf takes the X panel
-    } else if constexpr (DEFER == 1) {
+    if constexpr (DEFER) {
         lat_wait(cnt, nred, &d.red.guard);
 #pragma unroll
         for (int u = 0; u < NR; ++u) {
@@ -642,7 +528,7 @@ DEV void da3_panel(const Da3Src& d, int kb, int j0, bool store, float (*sb)[kWP]
 // gate (the deferred dW2 workers, latent.hpp enc_latent16_w2_kernel): a device flag read at
 // entry, whose 0 drops the tile before its stores -- the operand loads go out speculatively
 // instead of one scalar round trip after it.
-template <bool VEC, int NWV, int TS, bool DA3 = false, int DEFER = 0, class WA>
+template <bool VEC, int NWV, int TS, bool DA3 = false, bool DEFER = false, class WA>
 DEV void wgrad_body(const WA& p, const WGroup& g, int bid, float (*sa)[kWP], float (*sb)[kWP],
                     const int* gate = nullptr) {
     const int gv = gate ? ld_launch_const(gate) : 1;
@@ -731,19 +617,6 @@ DEV void wgrad_body(const WA& p, const WGroup& g, int bid, float (*sa)[kWP], flo
     for (int t = 0; t < kWTS; ++t) acc[t] = zero4();
     int kb = 0;
     do {  // K >= 1 always; a do-loop keeps the pre-loop loads off the exit path
-#ifdef VAEB_TABLE_FIRST
-        if constexpr (DEFER == 2) {
-            // [dMu | dLv] rows of this stage recomputed from the exact dZ sums (dml_table) BEFORE
-            // the panel loads go out: dA3's operand into sa (read by da3_panel, which then
-            // frees sa for the X panel), dW4 | dW5's B panel straight into sb
-            if constexpr (DA3) {
-                dml_table(p.da3.red, kb, 0, 2 * p.da3.Z, sa, (i0 == 0 && j0 == 0) ? p.da3.red.dml : nullptr);
-                __syncthreads();
-            } else {
-                dml_table(p.da3.red, kb, j0, kWTJ, sb, nullptr);
-            }
-        }
-#endif
         // stage the panels: element e = (row kr, float4 column c4).  All 16 loads of a
         // thread are issued before the first LDS store (one memory round trip).
         constexpr int NU = (kWKB * 16) / NTH;
@@ -779,24 +652,13 @@ DEV void wgrad_body(const WA& p, const WGroup& g, int bid, float (*sa)[kWP], flo
                 }
             }
         }
-#ifndef VAEB_TABLE_FIRST
-        if constexpr (DEFER == 2) {   // (the table while the panel loads are in flight; VAEB_TABLE_FIRST: before them)
-            if constexpr (DA3) {
-                dml_table(p.da3.red, kb, 0, 2 * p.da3.Z, sa, (i0 == 0 && j0 == 0) ? p.da3.red.dml : nullptr);
-                __syncthreads();
-            } else {
-                dml_table(p.da3.red, kb, j0, kWTJ, sb, nullptr);
-            }
-        }
-#endif
 #ifdef VAEB_TIMELINE
-        if (VAEB_DBG_ON(p.dbg) && kb == 0 && DEFER == 2 && tid == 0) p.dbg[bid * 8 + 7] = __builtin_amdgcn_s_memrealtime();
         if (VAEB_DBG_ON(p.dbg) && kb == 0) {   // the stage's panel loads landed
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             if (tid == 0) p.dbg[bid * 8 + 5] = __builtin_amdgcn_s_memrealtime();
         }
 #endif
-        if constexpr (DEFER == 1 && !DA3) {
+        if constexpr (DEFER && !DA3) {
             // B panel = [dMu | dLv] of this launch's reducers: poll, then sc1 loads only
             if (kb == 0) lat_wait(p.hd.red_cnt, p.hd.nred, &p.da3.red.guard);
 #pragma unroll
@@ -822,7 +684,7 @@ DEV void wgrad_body(const WA& p, const WGroup& g, int bid, float (*sa)[kWP], flo
                 }
             }
         }
-        if constexpr (DA3 && DEFER) da3_panel<NWV, TS, DEFER>(p.da3, kb, j0, i0 == 0, sb, p.hd.red_cnt, p.hd.nred, sa);
+        if constexpr (DA3 && DEFER) da3_panel<NWV, TS, true>(p.da3, kb, j0, i0 == 0, sb, p.hd.red_cnt, p.hd.nred);
         else if constexpr (DA3) da3_panel<NWV, TS>(p.da3, kb, j0, i0 == 0, sb);
 #ifdef VAEB_TIMELINE
         if (VAEB_DBG_ON(p.dbg) && kb == 0 && tid == 0) p.dbg[bid * 8 + 2] = __builtin_amdgcn_s_memrealtime();
@@ -837,7 +699,7 @@ DEV void wgrad_body(const WA& p, const WGroup& g, int bid, float (*sa)[kWP], flo
 #pragma unroll
             for (int s = 0; s < 4; ++s) v[s] = (i + s == g.rowsW) ? ((kb + kr < g.K) ? 1.f : 0.f) : v[s];
             *reinterpret_cast<f32x4*>(&sa[kr][4 * c4]) = v;
-            if constexpr (!DA3 && DEFER != 2) *reinterpret_cast<f32x4*>(&sb[kr][4 * c4]) = rb[u];
+            if constexpr (!DA3) *reinterpret_cast<f32x4*>(&sb[kr][4 * c4]) = rb[u];
         }
         __syncthreads();
 #ifdef VAEB_TIMELINE
@@ -961,10 +823,8 @@ __global__ __launch_bounds__(512) void w2_flush_kernel(WGradArgs p, const int* p
 // DEFER (LatRed, p.da3.red.nred reducers): blocks [ELBO][reducers][tiles], the reducers
 // dispatched ahead of every tile that waits for them (and 2 workgroups per CU hold the whole
 // grid at MNIST: 1 + 21 + 448 <= 512).  Stamps: reducers at logical ids total_wgs + 1 + r.
-// DEFER 2: no reducers; every dW3 / dW4 | dW5 workgroup recomputes its [dMu | dLv] rows
-// (dml_table) from the dhd launch's exact fixed-point dZ sums.
-template <int VM, int TS, int DEFER>
-__global__ __launch_bounds__(256, 2) void wgrad3_kernel(WGradArgs3 p) {   // (2 waves / SIMD: 2 workgroups / CU)
+template <int VM, int TS, bool DEFER>
+__global__ __launch_bounds__(256) void wgrad3_kernel(WGradArgs3 p) {
     __shared__ float sa[kWKB][kWP];
     __shared__ float sb[kWKB][kWP];
     const W3Head h = p.hd;   // one scalar load: the role and group boundaries
@@ -981,7 +841,7 @@ __global__ __launch_bounds__(256, 2) void wgrad3_kernel(WGradArgs3 p) {   // (2 
         }
         --b;
     }
-    if constexpr (DEFER == 1) {
+    if constexpr (DEFER) {
         if (b < h.nred) {
             const int sid = h.total_wgs + 1 + b;
             if (VAEB_DBG_ON(p.dbg) && threadIdx.x == 0) p.dbg[sid * 8 + 0] = __builtin_amdgcn_s_memrealtime();

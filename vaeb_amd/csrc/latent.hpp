@@ -118,6 +118,7 @@ DEV bool arrive_last(int* cnt, int target, int* sflag) {
 // explicitly by BOTH hand-offs: acc_dz[-1] is a padding word of acc_ml's range; read and
 // cleared by the step's ELBO reduction, which reports it as VAEB_ERR_NUMERIC to the host).
 typedef __attribute__((address_space(1))) unsigned long long gu64;
+constexpr double kFxScale = 4294967296.0;   // 2^32
 constexpr float kFxMax = 131072.f;          // 2^17
 constexpr int kFxCntShift = 59, kFxPoisonShift = 54;
 DEV uint64_t fx_inc(float v, uint64_t* guard) {
@@ -157,6 +158,7 @@ DEV uint64_t* fx_at(uint64_t* base, int64_t e) { return base + e * kFxStride; }
 // (fx_sum_get) and a later launch of the step zeroes them.  Range: |v| < 2^17, so <= 16 ... 32
 // contributors stay below 2^54; an out-of-range / NaN partial adds POISON = 2^58 instead (and
 // sets the guard word), which decodes to NaN: 32 of them still fit below 2^63.
+constexpr int64_t kFxSumPoison = (int64_t)1 << 58;
 DEV void fx_sum_add(uint64_t* p, uint64_t* guard, float v) {
     int64_t q;
     if (__builtin_expect(!(__builtin_fabsf(v) < kFxMax), 0)) {
@@ -167,7 +169,10 @@ DEV void fx_sum_add(uint64_t* p, uint64_t* guard, float v) {
     }
     __hip_atomic_fetch_add((gu64*)p, (unsigned long long)q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-// (fx_sum_get, the decode: kernels_aux.hpp)
+DEV float fx_sum_get(uint64_t w) {
+    const int64_t q = (int64_t)w;
+    return (q >= kFxSumPoison / 2 || q <= -kFxSumPoison / 2) ? __builtin_nanf("") : (float)((double)q * (1.0 / kFxScale));
+}
 
 // A tile's 16 rows x 2Z partials (Z <= 32) are handed off by all 512 threads of its
 // workgroup, repacked through LDS so that no lane adds for a padding column: thread t takes
@@ -759,30 +764,11 @@ DEV void decout_z_body(const StepArgs& a) {
                 lv = a.lv[(int64_t)i * Z + j];
                 e = a.eps[((int64_t)l * a.Mbp + i) * Z + j];
             }
-            const float sd = fexp(0.5f * lv);
-            const float z = rv ? mu + sd * e : 0.f;
+            const float z = rv ? mu + fexp(0.5f * lv) * e : 0.f;
             zs[ml][j] = z;
             if (col0) {
                 a.z[((int64_t)l * a.Mbp + i) * Z + j] = z;
                 const float elv = fexp(lv);
-                if (a.lat_aux) {
-                    // dMu = sum_l (dZ_l - c_mu,l), dLv = sum_l (dZ_l (eps_l sd / 2) + c_lv,l): LB /
-                    // FV c_mu = sc mu, c_lv = sc (1 - e^lv) / 2 on plane 0; LA c_mu = sl z_l,
-                    // c_lv = sl (1/2 - z_l sd eps_l / 2) (VAEB.py:315-346, latent_bwd_elem)
-                    const float sl = a.sc / (float)a.L;
-                    f32x4 r4 = zero4();
-                    if (rv) {
-                        r4[0] = e * 0.5f * sd;
-                        if (a.est == EST_LA) {
-                            r4[1] = sl * z;
-                            r4[2] = sl * (0.5f - 0.5f * z * sd * e);
-                        } else if (l == 0) {
-                            r4[1] = a.sc * mu;
-                            r4[2] = a.sc * 0.5f * (1.f - elv);
-                        }
-                    }
-                    reinterpret_cast<f32x4*>(a.lat_aux)[((int64_t)l * a.Mbp + i) * Z + j] = r4;
-                }
                 float g;
                 if (a.est == EST_LA) {
                     const float d = z - mu;

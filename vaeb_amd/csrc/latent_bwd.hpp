@@ -55,9 +55,6 @@ DEV void latent_bwd_elem(const StepArgs& a, bool valid, int m, int j, float mu, 
 // red: >= 512 f32x4 of LDS.
 // HO 2 (deferred, VAEB_BWD_DEFER): the tile stores its slab plainly and ends; the last
 // launch's reducer workgroups sum the slabs (kernels_aux.hpp LatRed).
-// HO 3 (deferred, VAEB_BWD_FX): the tile adds its partial into exact fixed-point sums of dZ_l
-// (a.acc_dz: this step's [L][Mbp][Z] words, no-return atomics) and ends; every consumer
-// workgroup of the last launch recomputes [dMu | dLv] from them (kernels_aux.hpp dml_table).
 // AT (atomic hand-off, latent.hpp fx_*): instead of a dZ slab, the tile adds its partial
 // dZ_l(m, j) into S(m, j) = sum_l dZ_l and dZ_l eps_l(m, j) into E(m, j) = sum_l dZ_l eps_l
 // (acc_dz; L * H/16 contributors each); the add completing S stores dMu(m, j), the one
@@ -149,26 +146,13 @@ DEV void dhd_dz_body(const PDhdT<V>& p0, int bx, int by, f32x4* red, int sid) {
                     pm[Z + j][4 * q + r] = sv[r] * ev[r];
                 }
         } else {
-            if constexpr (HO == 3) {
-                // exact fixed-point sums of dZ_l (no-return adds; the kernel boundary publishes
-                // them to the last launch, whose workgroups recompute [dMu | dLv] from them)
-                if (j < Z)
-#pragma unroll
-                    for (int r = 0; r < 4; ++r)
-#ifdef VAEB_DBG_FXPLAIN   // (timing-only build: plain stores instead of the adds)
-                        a.acc_dz[((int64_t)l * a.Mbp + rbl * 16 + 4 * q + r) * Z + j] = (uint64_t)(int64_t)sv[r];
-#else
-                        fx_sum_add(a.acc_dz + ((int64_t)l * a.Mbp + rbl * 16 + 4 * q + r) * Z + j, a.acc_ml - 1, sv[r]);
-#endif
-            } else {
-                const rsrc_t bs = mkbuf(a.slab_dz, (int64_t)a.L * a.Mbp * nctH * Z * 4);
-                const int64_t blk = ((int64_t)l * nrb + rbl) * nctH + by;
-                const uint32_t so = j < Z ? (uint32_t)(((blk * Z + j) * 16 + 4 * q) * 4) : kOOB;
-                // HO 2 (deferred): plain stores, published by the kernel boundary to the reducers
-                // of the last launch (kernels_aux.hpp LatRed); HO 0: write-through for the ticket
-                if constexpr (HO == 2) __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, sv), bs, so, 0, 0);
-                else st4_sc1(bs, so, sv);
-            }
+            const rsrc_t bs = mkbuf(a.slab_dz, (int64_t)a.L * a.Mbp * nctH * Z * 4);
+            const int64_t blk = ((int64_t)l * nrb + rbl) * nctH + by;
+            const uint32_t so = j < Z ? (uint32_t)(((blk * Z + j) * 16 + 4 * q) * 4) : kOOB;
+            // HO 2 (deferred): plain stores, published by the kernel boundary to the reducers
+            // of the last launch (kernels_aux.hpp LatRed); HO 0: write-through for the ticket
+            if constexpr (HO == 2) __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, sv), bs, so, 0, 0);
+            else st4_sc1(bs, so, sv);
         }
     }
     if constexpr (AT) {
@@ -205,7 +189,6 @@ DEV void dhd_dz_body(const PDhdT<V>& p0, int bx, int by, f32x4* red, int sid) {
         return;
     }
     VAEB_STAMP_AT(a, sid, 2);
-    if constexpr (HO == 3) return;
     if constexpr (HO == 2) {
         // the last launch's reducers count their arrivals on cnt_dz[0] (zeroed here, before it)
         if (sid == 0 && threadIdx.x == 0) *a.cnt_dz = 0;
@@ -285,8 +268,6 @@ struct DhdAux {
     int* pend;
     uint64_t* zero;
     int nzero;
-    uint64_t* zero2;   // HO 3: the other step parity's dZ sums (last read by the previous step)
-    int nzero2;
 };
 
 // dhd (+ dZ slabs, latent backward) tiles and the dW2 (| dW6) weight-gradient tiles in one
@@ -303,10 +284,6 @@ __global__ __launch_bounds__(512) void dhd_dz_wgrad_kernel(PDhdT<VEC> p, WGradAr
     if (aux.zero && b0 * 512 < aux.nzero) {
         const int i = b0 * 512 + (int)threadIdx.x;
         if (i < aux.nzero) aux.zero[i] = 0ull;
-    }
-    if (aux.zero2 && b0 * 512 < aux.nzero2) {
-        const int i = b0 * 512 + (int)threadIdx.x;
-        if (i < aux.nzero2) aux.zero2[i] = 0ull;
     }
     const int bid = b0 < ntile ? xcd_remap(b0, ntile) : ntile + xcd_remap(b0 - ntile, nwg);
     if (bid < ntile) {

@@ -60,10 +60,6 @@ struct StepArgs {
     // counted fixed-point accumulators of the atomic hand-off (latent.hpp: fx_*), zero
     // between launches: [Mbp][2Z] for [mu | lv], [Mbp][2Z] for [sum_l dZ | sum_l dZ eps]
     uint64_t *acc_ml, *acc_dz;
-    // HO 3 (the latent backward recomputed by the last launch's workgroups): the decoder's
-    // column-0 workgroups store, per (plane, row, latent), {eps sd / 2, c_mu, c_lv, 0} -- the dZ-free
-    // terms of [dMu | dLv] (kernels_aux.hpp dml_table); null otherwise
-    float* lat_aux;
     uint64_t* dbg;         // diagnostics: per-workgroup s_memrealtime stamps (null = off)
 };
 

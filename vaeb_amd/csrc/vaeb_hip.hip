@@ -173,13 +173,6 @@ struct vaeb_ctx {
     // the dhd launch zeroes the sums.  VAEB_ENC_FX=1 (not the default: MNIST 34.4-34.5 us with
     // the slabs against 34.8-35.1 with the sums -- the encoder launch +0.4 us, decout +0.2)
     bool enc_fx = false;
-    // the deferred latent backward without reducers (HO 3): the dhd tiles add their dZ partials
-    // into exact fixed-point sums (one [L][Mbp][Z] array per step parity, the dhd launch zeroing
-    // the other), and every dW3 / dW4 | dW5 workgroup of the last launch recomputes its
-    // [dMu | dLv] rows from them.  VAEB_BWD_FX=1 (default 0: the reducers, HO 2).
-    bool bwd_fx = false;
-    uint64_t* dzfx = nullptr;   // 2 x [L][Mbp][Z] (inside blk: the acc_dz range)
-    float* lat_aux = nullptr;   // [L][Mbp][Z] float4: the decoder's dZ-free [dMu | dLv] terms
     // the deferred dW2: dW2 (| dW6) + Adagrad of step t run in step t+1's encoder launch, on
     // the CUs the encoder leaves idle (latent.hpp enc_latent16_w2_kernel), so the dhd launch
     // holds the dhd tiles alone; host reads of the state flush a pending one first (w2_flush).
@@ -215,8 +208,6 @@ bool gaussian(const vaeb_ctx* c) { return c->c.decoder == VAEB_DEC_GAUSSIAN; }
 
 uint64_t* next_dbg(vaeb_ctx* c) { return c->dbg ? c->dbg + (size_t)(c->dbg_slot++) * kDbgWG * 8 : nullptr; }
 
-int ho_dz(const vaeb_ctx* c);
-bool fused_latent(const vaeb_ctx* c);
 StepArgs make_args(vaeb_ctx* c, int par, int Mb, int mode, const float* xbase, bool train) {
     StepArgs a{};
     const vaeb_config& g = c->c;
@@ -262,7 +253,6 @@ StepArgs make_args(vaeb_ctx* c, int par, int Mb, int mode, const float* xbase, b
     a.nctD = cdiv(g.D, 16);
     a.slab_ml = c->slab_ml; a.slab_dz = c->slab_dz; a.cnt_ml = c->cnt_ml; a.cnt_dz = c->cnt_dz;
     a.acc_ml = c->acc_ml; a.acc_dz = c->acc_dz;
-    a.lat_aux = (train && ho_dz(c) == 3 && fused_latent(c) && c->fold_bwd) ? c->lat_aux : nullptr;
     return a;
 }
 
@@ -318,19 +308,10 @@ int ho_mode(const vaeb_ctx* c, int fan_in) {
     return fan_in <= kFxMaxFanIn ? 1 : 0;   // the count field holds <= 16 contributors (latent.hpp)
 }
 int ho_ml(const vaeb_ctx* c, int ct) { return ho_mode(c, cdiv(c->c.H, 16 * ct)); }
-// backward: 1 atomic, else deferred to the last launch -- 3 (exact sums recomputed by every
-// consumer, VAEB_BWD_FX; needs the step parity flip) or 2 (reducers) -- or 0 (ticket)
-bool flips(const vaeb_ctx* c);
-// the training decoder forms z itself (decout_z_body ZM >= 1, enc_form's red or counted forms),
-// so its column-0 workgroups can store the dZ-free latent terms (StepArgs::lat_aux)
-bool dec_forms_z(const vaeb_ctx* c) {
-    const bool red = (c->enc_red < 0 ? ho_ml(c, 1) == 0 : c->enc_red == 1) && cdiv(c->c.H, 32) <= 32;
-    return red || ho_ml(c, 1) == 1;
-}
+// backward: 1 atomic, else 2 (deferred to the last launch's reducers, VAEB_BWD_DEFER) or 0 (ticket)
 int ho_dz(const vaeb_ctx* c) {
     const int m = ho_mode(c, cdiv(c->c.H, 16) * c->c.L);
-    if (m != 0 || !c->bwd_defer) return m;
-    return c->bwd_fx && flips(c) && c->c.L <= 32 && dec_forms_z(c) ? 3 : 2;
+    return m == 0 && c->bwd_defer ? 2 : m;
 }
 
 // Measurement brackets: mark(id) records an event before launch slot `id`.  With
@@ -668,7 +649,7 @@ int launch_wgrad(vaeb_ctx* c, hipStream_t s, const WGroup* groups, int n, const 
         w.hd.red_cnt = da3->red.cnt;
         const dim3 grid(w.hd.total_wgs + (e ? 1 : 0) + nred);
         auto go = [&](auto DF) {
-            constexpr int df = decltype(DF)::value;
+            constexpr bool df = decltype(DF)::value;
             switch (vm) {
                 case 7: hipLaunchKernelGGL((wgrad3_kernel<7, kW3TS, df>), grid, dim3(256), 0, s, w); break;
                 case 1: hipLaunchKernelGGL((wgrad3_kernel<1, kW3TS, df>), grid, dim3(256), 0, s, w); break;
@@ -677,10 +658,9 @@ int launch_wgrad(vaeb_ctx* c, hipStream_t s, const WGroup* groups, int n, const 
                 default: hipLaunchKernelGGL((wgrad3_kernel<0, kW3TS, df>), grid, dim3(256), 0, s, w); break;
             }
         };
-        // DEFER: 1 reducers in this launch, 2 [dMu | dLv] recomputed from exact sums, 0 handed in
-        if (nred > 0) go(std::integral_constant<int, 1>{});
-        else if (da3->red.fx) go(std::integral_constant<int, 2>{});
-        else go(std::integral_constant<int, 0>{});
+        // DEFER: reducers in this launch, or [dMu | dLv] handed in by the dhd launch
+        if (nred > 0) go(std::true_type{});
+        else go(std::false_type{});
     } else {
         WGradArgs w;
         if (int rc = prep_wgrad(c, groups, n, opt, e, a, 0, w, vec, kWTJ_W)) return rc;
@@ -1013,16 +993,7 @@ int enqueue_train_step(vaeb_ctx* c, int par, bool prof, bool fresh = true, int d
         if (int rc = prep_wgrad(c, &g4, 1, opt, nullptr, a, ntile, w, vec, kWTJ_P5)) return rc;
         // the dhd loaders' 16-byte form needs D % 4 == 0 and aligned dA2 / W2 too
         vec = vec && dhd_vec(a);
-        DhdAux pend{nullptr, nullptr, 0, nullptr, 0};
-        const int hz = ho_dz(c);
-        const int64_t nfx = (int64_t)a.L * a.Mbp * a.Z;
-        PDhdT<true> p5x = p5;
-        PDhdT<false> p5sx = p5s;
-        if (hz == 3) {   // this step's sums; zero the other parity's (read by the previous step)
-            p5x.a.acc_dz = p5sx.a.acc_dz = c->dzfx + par * nfx;
-            pend.zero2 = c->dzfx + (par ^ 1) * nfx;
-            pend.nzero2 = (int)nfx;
-        }
+        DhdAux pend{nullptr, nullptr, 0};
         if (w2d) {   // no dW2 tiles here: the next step's encoder launch (or a flush) runs them
             w.total_wgs = ntile;
             pend.pend = c->w2pend;
@@ -1037,10 +1008,9 @@ int enqueue_train_step(vaeb_ctx* c, int par, bool prof, bool fresh = true, int d
         const bool deep = cdiv(cdiv(p5.K, 16), 8) > 4;
         pr.mark(w2d ? 43 : 39);
         REP(pr) {
-            switch (hz) {
+            switch (ho_dz(c)) {
                 case 1: launch_dhd_dz<kWTJ_P5 / 16, 1>(s, grid, p5, p5s, w, ntile, gx, vec, deep, pend); break;
                 case 2: launch_dhd_dz<kWTJ_P5 / 16, 2>(s, grid, p5, p5s, w, ntile, gx, vec, deep, pend); break;
-                case 3: launch_dhd_dz<kWTJ_P5 / 16, 3>(s, grid, p5x, p5sx, w, ntile, gx, vec, deep, pend); break;
                 default: launch_dhd_dz<kWTJ_P5 / 16, 0>(s, grid, p5, p5s, w, ntile, gx, vec, deep, pend); break;
             }
         }
@@ -1114,15 +1084,7 @@ int enqueue_train_step(vaeb_ctx* c, int par, bool prof, bool fresh = true, int d
         a.dbg = next_dbg(c);
         if (fold) {
             Da3Src d3{c->dMuLv, a.W4, a.W5, c->h, c->dA3, a.Z, a.H, a.Mb, a.Mbp, LatRed{}};
-            if (ho_dz(c) == 3) {
-                // recomputed by every consumer workgroup from this step's exact dZ sums
-                LatRed& r = d3.red;
-                r.fx = c->dzfx + par * (int64_t)a.L * a.Mbp * a.Z;
-                r.aux = c->lat_aux;
-                r.mu = c->mu; r.lv = c->lv; r.eps = c->eps; r.z = c->z;
-                r.dZ = c->dZ; r.dml = c->dMuLv; r.cnt = nullptr; r.guard = c->blk + kBlkFxErr;
-                r.nred = 0; r.L = a.L; r.est = a.est; r.Mb = a.Mb; r.Mbp = a.Mbp; r.Z = a.Z; r.sc = a.sc;
-            } else if (ho_dz(c) == 2) {
+            if (ho_dz(c) == 2) {
                 // the deferred latent backward: ceil(Z / 8) column groups per 16-row block
                 LatRed& r = d3.red;
                 r.slab = c->slab_dz; r.mu = c->mu; r.lv = c->lv; r.eps = c->eps; r.z = c->z;
@@ -1318,7 +1280,6 @@ int vaeb_create(const vaeb_config* cfg, vaeb_ctx** out) {
     if (const char* fb = getenv("VAEB_FOLD_BWD")) c->fold_bwd = atoi(fb) != 0;
     if (const char* bd = getenv("VAEB_BWD_DEFER")) c->bwd_defer = atoi(bd) != 0;
     if (const char* ef = getenv("VAEB_ENC_FX")) c->enc_fx = atoi(ef) != 0;
-    if (const char* bx = getenv("VAEB_BWD_FX")) c->bwd_fx = atoi(bx) != 0;
     if (const char* wd = getenv("VAEB_DW2_DEFER")) c->dw2_defer = atoi(wd) != 0;
     if (const char* bk = getenv("VAEB_BF_FORK")) c->bf_fork = atoi(bk) != 0;
     if (const char* b2 = getenv("VAEB_BF_SPLIT2")) c->bf_split2 = atoi(b2) != 0;
@@ -1379,7 +1340,6 @@ int vaeb_create(const vaeb_config* cfg, vaeb_ctx** out) {
     rc = rc ? rc : dalloc(&c->dA1, (size_t)RL * H);
     rc = rc ? rc : dalloc(&c->dZ, (size_t)RL * Z);
     rc = rc ? rc : dalloc(&c->dMuLv, (size_t)R * 2 * Z);
-    rc = rc ? rc : dalloc(&c->lat_aux, (size_t)RL * Z * 4);
     rc = rc ? rc : dalloc(&c->dA3, (size_t)R * H);
     rc = rc ? rc : dalloc(&c->kl_part, (size_t)RL * cdiv(Z, 16));
     rc = rc ? rc : dalloc(&c->lp_part, (size_t)RL * cdiv(D, 16));
@@ -1398,9 +1358,6 @@ int vaeb_create(const vaeb_config* cfg, vaeb_ctx** out) {
             c->elbo_out = reinterpret_cast<float*>(c->blk + kBlkElbo);
             c->acc_ml = c->blk + kBlkAcc;
             c->acc_dz = c->acc_ml + nacc;
-            // HO 3's two [L][Mbp][Z] sum arrays use the counted form's accumulator range (only
-            // one of the two forms runs in a context; 2 L Bp Z <= 66 Bp Z words for L <= 32)
-            c->dzfx = c->acc_dz;
         }
     }
     if (!rc && is_bf16(c)) rc = bf_alloc(c);
@@ -1449,7 +1406,7 @@ int vaeb_destroy(vaeb_ctx* c) {
     if (c->comm) ncclCommDestroy(c->comm);
     float* fp[] = {c->theta2[0], c->theta2[1], c->acc, c->grad, c->fvmu, c->fvsg, c->fvam, c->fvas, c->fv_part, c->data, c->xeval, c->xval,
                    c->eps_in, c->h, c->mu, c->lv, c->eps, c->z, c->hd, c->y, c->dA2, c->dA1,   // dA6 lives in dA2's block
-                   c->dZ, c->dMuLv, c->dA3, c->kl_part, c->lp_part, c->slab_ml, c->slab_dz, c->yacc, c->lat_aux,
+                   c->dZ, c->dMuLv, c->dA3, c->kl_part, c->lp_part, c->slab_ml, c->slab_dz, c->yacc,
                    c->fvzeta};
     for (float* p : fp) if (p) hipFree(p);
     if (c->cnt_ml) hipFree(c->cnt_ml);
