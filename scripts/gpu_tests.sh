@@ -3,7 +3,7 @@ set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1; rc=$?
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1; rc=$?
 tail -5 gpurun_out/gpu_tests.log
 [ $rc -ne 0 ] && { grep -E "FAILED|Error|assert" gpurun_out/gpu_tests.log | head -30; exit 1; }
 timeout -k 10 200 python3 bench.py --no-cpu-baseline > gpurun_out/bench_plain.json 2> gpurun_out/bench_plain.err || { tail -20 gpurun_out/bench_plain.err; exit 1; }

@@ -176,7 +176,8 @@ struct vaeb_ctx {
     // the deferred dW2: dW2 (| dW6) + Adagrad of step t run in step t+1's encoder launch, on
     // the CUs the encoder leaves idle (latent.hpp enc_latent16_w2_kernel), so the dhd launch
     // holds the dhd tiles alone; host reads of the state flush a pending one first (w2_flush).
-    // fp32 LB / LA, no communicator, 16-wave encoder.  VAEB_DW2_DEFER=0: dW2 in the dhd launch.
+    // fp32 LB / LA, no communicator, 16-wave encoder, the latent backward deferred too (ho_dz 2:
+    // dw2_deferred).  VAEB_DW2_DEFER=0: dW2 in the dhd launch.
     bool dw2_defer = true;
     int* w2pend = nullptr;        // device: 1 = a step's dW2 is pending (set by its dhd launch)
     bool w2_dirty = false;        // host: a step was enqueued since the last flush
@@ -693,10 +694,15 @@ int w2_args(vaeb_ctx* c, const StepArgs& a, const OptArgs& opt, int base, WGradA
 }
 
 // Whether the step on `a` defers its dW2 into the next step's encoder launch (vaeb_ctx::dw2_defer).
+// Only where the dhd launch hands its latent backward to the last launch (ho_dz 2): there the
+// dW2 tiles bound the dhd launch.  With the counted atomic backward (small fan-in: Frey) the dhd
+// launch is bound by that hand-off and hides dW2, while the encoder would pay for it: Frey
+// 29.78 / 29.87 µs in-step vs 31.54 / 31.55 deferred.
 bool dw2_deferred(const vaeb_ctx* c, const StepArgs& a) {
     const int est = c->c.estimator;
     return c->dw2_defer && c->c.dtype == VAEB_DTYPE_F32 && c->comm == nullptr && est != VAEB_EST_FV && est != VAEB_EST_FVS &&
-           fused_latent(c) && c->fold_bwd && folded_latent(c, a) && enc_form(c, a, FvFold{}, nullptr, nullptr, nullptr);
+           fused_latent(c) && c->fold_bwd && ho_dz(c) == 2 && folded_latent(c, a) &&
+           enc_form(c, a, FvFold{}, nullptr, nullptr, nullptr);
 }
 
 // Run the pending step's dW2 (| dW6) + Adagrad now (their own launch; the device flag makes it
