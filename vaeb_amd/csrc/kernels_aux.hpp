@@ -266,12 +266,23 @@ struct LatRed {
     const float* slab;                 // [L][nrb][nctH][Z][16] partial dZ slabs
     const float *mu, *lv, *eps, *z;    // [Mbp][Z]; [L][Mbp][Z]
     float* dZ;                         // [L][Mbp][Z] (kept for inspection, as the ticketed form)
-    float* dml;                        // [Mbp][2Z] [dMu | dLv]: the handed-off bytes
-    int* cnt;                          // completion counter
+    float* dml;                        // [Mbp][2Z] [dMu | dLv]: the handed-off bytes, kLatRep copies
+    int* cnt;                          // completion counters, one per copy (kLatCntStride apart)
     uint64_t* guard;                   // blk[kBlkFxErr]: timeout bit
     int nred, ngrp, zg, nctH, L, est, Mb, Mbp, Z;
     float sc;
+    int rep;                           // floats between the copies of dml
 };
+// Optionally replicated per XCD (-DVAEB_LAT_REP=8 build): each reducer stores its block into
+// kLatRep copies and adds to kLatRep counters, and a consumer polls and reads the copy of its XCD
+// (blockIdx.x % 8, the dispatcher's round robin; any copy is correct, the choice only spreads the
+// memory-side traffic of 448 pollers / readers).  Measured: the poll returned ~0.5 us earlier but
+// the eight-fold stores and adds cost more -- last launch 10.86 vs 10.57 us -- so one copy.
+#ifndef VAEB_LAT_REP
+#define VAEB_LAT_REP 1
+#endif
+constexpr int kLatRep = VAEB_LAT_REP, kLatCntStride = 16;   // counters 64 B apart
+DEV int lat_copy() { return (int)(blockIdx.x & (kLatRep - 1)); }
 struct Da3Src {
     const float *dml, *W4, *W5, *h;
     float* dA3;           // the column slice is also stored (by the D-row tile 0 workgroups)
@@ -282,7 +293,9 @@ constexpr uint64_t kGuardHandoffTimeout = 4;
 
 // One reducer workgroup (256 threads): row block rb, latent columns [j0, j0 + nj).  Element
 // thread t < 16 nj owns (row rb * 16 + t / nj, column j0 + t % nj).
-DEV void lat_reduce_wg(const LatRed& r, int wi, f32x4* red, float (*dzs)[17]) {
+// dbg (timeline build): stamp slots of this reducer (5 slab loads landed, 2 [dMu | dLv] formed,
+// 6 stores drained)
+DEV void lat_reduce_wg(const LatRed& r, int wi, f32x4* red, float (*dzs)[17], uint64_t* dbg = nullptr) {
     const int Z = r.Z, nrb = r.Mbp >> 4;
     const int rb = wi / r.ngrp, cg = wi - rb * r.ngrp;
     const int j0 = cg * r.zg, nj = min(r.zg, Z - j0);
@@ -319,6 +332,10 @@ DEV void lat_reduce_wg(const LatRed& r, int wi, f32x4* red, float (*dzs)[17]) {
             }
 #pragma unroll
             for (int u = 0; u < SV; ++u) sum += v[u];
+        }
+        if (VAEB_DBG_ON(dbg) && l == 0 && t == 0) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            dbg[5] = __builtin_amdgcn_s_memrealtime();
         }
         red[t] = sum;
         __syncthreads();
@@ -357,17 +374,24 @@ DEV void lat_reduce_wg(const LatRed& r, int wi, f32x4* red, float (*dzs)[17]) {
             dlv = dzes * 0.5f * sd + r.sc * 0.5f * (1.f - fexp(lv));
         }
     }
-    // publish: sc1 stores by the storing waves (waves 0, 1 at 16 nj <= 128), each drained, the
-    // barrier, one counter add
+    if (VAEB_DBG_ON(dbg) && t == 0) dbg[2] = __builtin_amdgcn_s_memrealtime();
+    // publish: sc1 stores into every copy by the storing waves (waves 0, 1 at 16 nj <= 128), each
+    // drained, the barrier, one add per copy's counter
     if (el) {
-        const rsrc_t bd = mkbuf(r.dml, (int64_t)r.Mbp * 2 * Z * 4);
-        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, dmu), bd, (uint32_t)(m * 2 * Z + j) * 4u, 0, 16);
-        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, dlv), bd, (uint32_t)(m * 2 * Z + Z + j) * 4u, 0, 16);
+        const rsrc_t bd = mkbuf(r.dml, (int64_t)(kLatRep - 1) * r.rep * 4 + (int64_t)r.Mbp * 2 * Z * 4);
+#pragma unroll
+        for (int c = 0; c < kLatRep; ++c) {
+            const uint32_t o = (uint32_t)(c * r.rep + m * 2 * Z + j) * 4u;
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, dmu), bd, o, 0, 16);
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, dlv), bd, o + (uint32_t)Z * 4u, 0, 16);
+        }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (t == 0) __hip_atomic_fetch_add((__attribute__((address_space(1))) int*)r.cnt, 1, __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_AGENT);
+    if (VAEB_DBG_ON(dbg) && t == 0) dbg[6] = __builtin_amdgcn_s_memrealtime();
+    if (t < kLatRep)
+        __hip_atomic_fetch_add((__attribute__((address_space(1))) int*)(r.cnt + t * kLatCntStride), 1, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // Consumer side: one lane polls the counter (sc1 loads, s_sleep between polls, bounded), the
@@ -452,12 +476,14 @@ DEV f32x4 ld_w45(rsrc_t bw4, rsrc_t bw5, int Z, int H, int n, int k, bool vz) {
 // DEFER (the deferred latent backward, LatRed): [dMu | dLv] is produced in this launch, so its
 // loads wait for the reducers' counter and are sc1; the W4 / W5 and h loads go out first.
 template <int NWV, int TS, bool DEFER = false>
-DEV void da3_panel(const Da3Src& d, int kb, int j0, bool store, float (*sb)[kWP], int* cnt = nullptr, int nred = 0) {
+DEV void da3_panel(const Da3Src& d, int kb, int j0, bool store, float (*sb)[kWP], int* cnt = nullptr, int nred = 0,
+                   uint64_t* dbg = nullptr) {   // dbg (timeline build): slot 7 = the poll returned
     constexpr int NR = kWKB / 16 / NWV;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int li = lane & 15, q = lane >> 4;
     const int Z = d.Z, H = d.H, K2 = 2 * d.Z;
-    const rsrc_t bd = mkbuf(d.dml, (int64_t)d.Mbp * K2 * 4);
+    // (DEFER: the copy of this workgroup's XCD)
+    const rsrc_t bd = mkbuf(d.dml + (DEFER ? lat_copy() * d.red.rep : 0), (int64_t)d.Mbp * K2 * 4);
     const rsrc_t bw4 = mkbuf(d.W4, (int64_t)H * Z * 4), bw5 = mkbuf(d.W5, (int64_t)H * Z * 4);
     const rsrc_t bh = mkbuf(d.h, (int64_t)d.Mbp * H * 4);
     const bool vz = (Z & 3) == 0 && aligned16(d.W4) && aligned16(d.W5);
@@ -486,7 +512,8 @@ DEV void da3_panel(const Da3Src& d, int kb, int j0, bool store, float (*sb)[kWP]
         }
     }
     if constexpr (DEFER) {
-        lat_wait(cnt, nred, &d.red.guard);
+        lat_wait(cnt + lat_copy() * kLatCntStride, nred, &d.red.guard);
+        if (VAEB_DBG_ON(dbg) && kb == 0 && threadIdx.x == 0) dbg[7] = __builtin_amdgcn_s_memrealtime();
 #pragma unroll
         for (int u = 0; u < NR; ++u) {
             const int r0 = kb + 16 * (wv + NWV * u);
@@ -660,7 +687,11 @@ DEV void wgrad_body(const WA& p, const WGroup& g, int bid, float (*sa)[kWP], flo
 #endif
         if constexpr (DEFER && !DA3) {
             // B panel = [dMu | dLv] of this launch's reducers: poll, then sc1 loads only
-            if (kb == 0) lat_wait(p.hd.red_cnt, p.hd.nred, &p.da3.red.guard);
+            // (the copy of this workgroup's XCD: its counter and its [dMu | dLv])
+            if (kb == 0) lat_wait(p.hd.red_cnt + lat_copy() * kLatCntStride, p.hd.nred, &p.da3.red.guard);
+            const int co = lat_copy() * p.da3.red.rep;
+            const rsrc_t cb0 = mkbuf(g.b0 + co, (int64_t)g.K * g.ld0 * 4);
+            const rsrc_t cb1 = mkbuf((g.b1 ? g.b1 : g.b0) + co, (int64_t)g.K * (g.b1 ? g.ld1 : g.ld0) * 4);
 #pragma unroll
             for (int u = 0; u < NU; ++u) {
                 const int e = tid + NTH * u;
@@ -672,19 +703,21 @@ DEV void wgrad_body(const WA& p, const WGroup& g, int bid, float (*sa)[kWP], flo
                     const bool in0 = j < g.N0;
                     const uint32_t o0 = (jt && k < g.K && in0) ? (uint32_t)(k * g.ld0 + j) * 4u : kOOB;
                     const uint32_t o1 = (jt && k < g.K && !in0 && j - g.N0 < g.N1) ? (uint32_t)(k * g.ld1 + j - g.N0) * 4u : kOOB;
-                    rb[u] = in0 ? bld4x<16>(bb0, o0) : bld4x<16>(bb1, o1);
+                    rb[u] = in0 ? bld4x<16>(cb0, o0) : bld4x<16>(cb1, o1);
                 } else {
 #pragma unroll
                     for (int s = 0; s < 4; ++s) {
                         const int jj = j + s;
                         const bool in0 = jj < g.N0;
-                        rb[u][s] = in0 ? bldx<16>(bb0, (jt && k < g.K) ? (uint32_t)(k * g.ld0 + jj) * 4u : kOOB)
-                                       : bldx<16>(bb1, (jt && k < g.K && jj - g.N0 < g.N1) ? (uint32_t)(k * g.ld1 + jj - g.N0) * 4u : kOOB);
+                        rb[u][s] = in0 ? bldx<16>(cb0, (jt && k < g.K) ? (uint32_t)(k * g.ld0 + jj) * 4u : kOOB)
+                                       : bldx<16>(cb1, (jt && k < g.K && jj - g.N0 < g.N1) ? (uint32_t)(k * g.ld1 + jj - g.N0) * 4u : kOOB);
                     }
                 }
             }
         }
-        if constexpr (DA3 && DEFER) da3_panel<NWV, TS, true>(p.da3, kb, j0, i0 == 0, sb, p.hd.red_cnt, p.hd.nred);
+        if constexpr (DA3 && DEFER)
+            da3_panel<NWV, TS, true>(p.da3, kb, j0, i0 == 0, sb, p.hd.red_cnt, p.hd.nred,
+                                     VAEB_DBG_ON(p.dbg) ? p.dbg + bid * 8 : nullptr);
         else if constexpr (DA3) da3_panel<NWV, TS>(p.da3, kb, j0, i0 == 0, sb);
 #ifdef VAEB_TIMELINE
         if (VAEB_DBG_ON(p.dbg) && kb == 0 && tid == 0) p.dbg[bid * 8 + 2] = __builtin_amdgcn_s_memrealtime();
@@ -845,7 +878,8 @@ __global__ __launch_bounds__(256) void wgrad3_kernel(WGradArgs3 p) {
         if (b < h.nred) {
             const int sid = h.total_wgs + 1 + b;
             if (VAEB_DBG_ON(p.dbg) && threadIdx.x == 0) p.dbg[sid * 8 + 0] = __builtin_amdgcn_s_memrealtime();
-            lat_reduce_wg(p.da3.red, b, reinterpret_cast<f32x4*>(&sa[0][0]), reinterpret_cast<float(*)[17]>(&sb[0][0]));
+            lat_reduce_wg(p.da3.red, b, reinterpret_cast<f32x4*>(&sa[0][0]), reinterpret_cast<float(*)[17]>(&sb[0][0]),
+                          VAEB_DBG_ON(p.dbg) ? p.dbg + sid * 8 : nullptr);
             if (VAEB_DBG_ON(p.dbg) && threadIdx.x == 0) p.dbg[sid * 8 + 3] = __builtin_amdgcn_s_memrealtime();
             return;
         }
