@@ -266,23 +266,25 @@ struct LatRed {
     const float* slab;                 // [L][nrb][nctH][Z][16] partial dZ slabs
     const float *mu, *lv, *eps, *z;    // [Mbp][Z]; [L][Mbp][Z]
     float* dZ;                         // [L][Mbp][Z] (kept for inspection, as the ticketed form)
-    float* dml;                        // [Mbp][2Z] [dMu | dLv]: the handed-off bytes, kLatRep copies
-    int* cnt;                          // completion counters, one per copy (kLatCntStride apart)
+    float* dml;                        // [Mbp][2Z] [dMu | dLv]: the handed-off bytes
+    int* cnt;                          // completion counter, kLatCnt replicas kLatCntStride apart
     uint64_t* guard;                   // blk[kBlkFxErr]: timeout bit
     int nred, ngrp, zg, nctH, L, est, Mb, Mbp, Z;
     float sc;
-    int rep;                           // floats between the copies of dml
 };
-// Optionally replicated per XCD (-DVAEB_LAT_REP=8 build): each reducer stores its block into
-// kLatRep copies and adds to kLatRep counters, and a consumer polls and reads the copy of its XCD
-// (blockIdx.x % 8, the dispatcher's round robin; any copy is correct, the choice only spreads the
-// memory-side traffic of 448 pollers / readers).  Measured: the poll returned ~0.5 us earlier but
-// the eight-fold stores and adds cost more -- last launch 10.86 vs 10.57 us -- so one copy.
-#ifndef VAEB_LAT_REP
-#define VAEB_LAT_REP 1
+// The completion counter can be kept in kLatCnt replicas on lines of their own (MI355X_MICROARCH.md's
+// hand-off table, row 2; -DVAEB_LAT_CNT=8 build): each reducer adds to every replica with ONE
+// wave instruction of kLatCnt lanes, and a consumer polls the replica of its round-robin slot
+// (blockIdx.x % 8), so the launch's 448 pollers spread over 8 lines.  Round 4 A/B (alternating
+// 4000-step runs): with 16-byte publication stores (-DVAEB_LAT_ST4) 34.51 / 34.53 µs, the single
+// counter with those stores 35.06 / 35.17, the single counter with dword stores (the default)
+// 34.51 / 34.35; the timeline build saw the poll return ~2 µs earlier with replicas, the
+// production step did not.  Eight copies of [dMu | dLv] as well (one per XCD): 10.86 vs 10.57 µs.
+#ifndef VAEB_LAT_CNT
+#define VAEB_LAT_CNT 1
 #endif
-constexpr int kLatRep = VAEB_LAT_REP, kLatCntStride = 16;   // counters 64 B apart
-DEV int lat_copy() { return (int)(blockIdx.x & (kLatRep - 1)); }
+constexpr int kLatCnt = VAEB_LAT_CNT, kLatCntStride = 16;   // replicas 64 B apart
+DEV int lat_slot() { return (int)(blockIdx.x & (kLatCnt - 1)); }
 struct Da3Src {
     const float *dml, *W4, *W5, *h;
     float* dA3;           // the column slice is also stored (by the D-row tile 0 workgroups)
@@ -375,21 +377,40 @@ DEV void lat_reduce_wg(const LatRed& r, int wi, f32x4* red, float (*dzs)[17], ui
         }
     }
     if (VAEB_DBG_ON(dbg) && t == 0) dbg[2] = __builtin_amdgcn_s_memrealtime();
-    // publish: sc1 stores into every copy by the storing waves (waves 0, 1 at 16 nj <= 128), each
-    // drained, the barrier, one add per copy's counter
-    if (el) {
-        const rsrc_t bd = mkbuf(r.dml, (int64_t)(kLatRep - 1) * r.rep * 4 + (int64_t)r.Mbp * 2 * Z * 4);
-#pragma unroll
-        for (int c = 0; c < kLatRep; ++c) {
-            const uint32_t o = (uint32_t)(c * r.rep + m * 2 * Z + j) * 4u;
-            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, dmu), bd, o, 0, 16);
-            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, dlv), bd, o + (uint32_t)Z * 4u, 0, 16);
+    // publish, write-through (sc1): dword stores (VAEB_LAT_ST4: 16-byte runs staged through LDS);
+    // then every storing wave drains, the barrier, one add per counter replica (one instruction)
+    const rsrc_t bd = mkbuf(r.dml, (int64_t)r.Mbp * 2 * Z * 4);
+#ifdef VAEB_LAT_ST4   // (A/B build: 16-byte runs; measured no faster, see kLatCnt)
+    if ((nj & 3) == 0 && (Z & 3) == 0 && (j0 & 3) == 0) {
+#else
+    if (false) {
+#endif
+        float* stg = reinterpret_cast<float*>(red);   // [16 rows][2 nj + 1]
+        const int sp = 2 * nj + 1;
+        __syncthreads();   // (red held the partition sums)
+        if (el) {
+            stg[ml * sp + jj] = dmu;
+            stg[ml * sp + nj + jj] = dlv;
         }
+        __syncthreads();
+        const int nc4 = nj >> 1;   // 16-byte chunks per row: nj / 4 of dMu, nj / 4 of dLv
+        if (t < 16 * nc4) {
+            const int row = t / nc4, q = t - row * nc4;
+            const int half = q >= (nj >> 2) ? 1 : 0, c4 = q - half * (nj >> 2);
+            const int mm = rb * 16 + row;
+            f32x4 v;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) v[k] = stg[row * sp + half * nj + 4 * c4 + k];
+            bst4x<16>(bd, (mm < r.Mbp) ? (uint32_t)(mm * 2 * Z + half * Z + j0 + 4 * c4) * 4u : kOOB, v);
+        }
+    } else if (el) {
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, dmu), bd, (uint32_t)(m * 2 * Z + j) * 4u, 0, 16);
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, dlv), bd, (uint32_t)(m * 2 * Z + Z + j) * 4u, 0, 16);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (VAEB_DBG_ON(dbg) && t == 0) dbg[6] = __builtin_amdgcn_s_memrealtime();
-    if (t < kLatRep)
+    if (t < kLatCnt)
         __hip_atomic_fetch_add((__attribute__((address_space(1))) int*)(r.cnt + t * kLatCntStride), 1, __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -482,8 +503,7 @@ DEV void da3_panel(const Da3Src& d, int kb, int j0, bool store, float (*sb)[kWP]
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int li = lane & 15, q = lane >> 4;
     const int Z = d.Z, H = d.H, K2 = 2 * d.Z;
-    // (DEFER: the copy of this workgroup's XCD)
-    const rsrc_t bd = mkbuf(d.dml + (DEFER ? lat_copy() * d.red.rep : 0), (int64_t)d.Mbp * K2 * 4);
+    const rsrc_t bd = mkbuf(d.dml, (int64_t)d.Mbp * K2 * 4);
     const rsrc_t bw4 = mkbuf(d.W4, (int64_t)H * Z * 4), bw5 = mkbuf(d.W5, (int64_t)H * Z * 4);
     const rsrc_t bh = mkbuf(d.h, (int64_t)d.Mbp * H * 4);
     const bool vz = (Z & 3) == 0 && aligned16(d.W4) && aligned16(d.W5);
@@ -512,7 +532,7 @@ DEV void da3_panel(const Da3Src& d, int kb, int j0, bool store, float (*sb)[kWP]
         }
     }
     if constexpr (DEFER) {
-        lat_wait(cnt + lat_copy() * kLatCntStride, nred, &d.red.guard);
+        lat_wait(cnt + lat_slot() * kLatCntStride, nred, &d.red.guard);
         if (VAEB_DBG_ON(dbg) && kb == 0 && threadIdx.x == 0) dbg[7] = __builtin_amdgcn_s_memrealtime();
 #pragma unroll
         for (int u = 0; u < NR; ++u) {
@@ -687,11 +707,9 @@ DEV void wgrad_body(const WA& p, const WGroup& g, int bid, float (*sa)[kWP], flo
 #endif
         if constexpr (DEFER && !DA3) {
             // B panel = [dMu | dLv] of this launch's reducers: poll, then sc1 loads only
-            // (the copy of this workgroup's XCD: its counter and its [dMu | dLv])
-            if (kb == 0) lat_wait(p.hd.red_cnt + lat_copy() * kLatCntStride, p.hd.nred, &p.da3.red.guard);
-            const int co = lat_copy() * p.da3.red.rep;
-            const rsrc_t cb0 = mkbuf(g.b0 + co, (int64_t)g.K * g.ld0 * 4);
-            const rsrc_t cb1 = mkbuf((g.b1 ? g.b1 : g.b0) + co, (int64_t)g.K * (g.b1 ? g.ld1 : g.ld0) * 4);
+            // (the counter replica of this workgroup's round-robin slot)
+            if (kb == 0) lat_wait(p.hd.red_cnt + lat_slot() * kLatCntStride, p.hd.nred, &p.da3.red.guard);
+            const rsrc_t cb0 = bb0, cb1 = bb1;
 #pragma unroll
             for (int u = 0; u < NU; ++u) {
                 const int e = tid + NTH * u;

@@ -190,9 +190,9 @@ DEV void dhd_dz_body(const PDhdT<V>& p0, int bx, int by, f32x4* red, int sid) {
     }
     VAEB_STAMP_AT(a, sid, 2);
     if constexpr (HO == 2) {
-        // the last launch's reducers count their arrivals on the per-XCD counters cnt_dz[16 c]
-        // (kernels_aux.hpp kLatRep; zeroed here, before it)
-        if (sid == 0 && (int)threadIdx.x < kLatRep) a.cnt_dz[threadIdx.x * kLatCntStride] = 0;
+        // the last launch's reducers count their arrivals on the counter replicas cnt_dz[16 c]
+        // (kernels_aux.hpp kLatCnt; zeroed here, before it)
+        if (sid == 0 && (int)threadIdx.x < kLatCnt) a.cnt_dz[threadIdx.x * kLatCntStride] = 0;
         return;
     }
     if (!arrive_last<NCT>(a.cnt_dz + rbl, nctH * a.L, &sflag)) return;

@@ -1095,9 +1095,12 @@ int enqueue_train_step(vaeb_ctx* c, int par, bool prof, bool fresh = true, int d
                 LatRed& r = d3.red;
                 r.slab = c->slab_dz; r.mu = c->mu; r.lv = c->lv; r.eps = c->eps; r.z = c->z;
                 r.dZ = c->dZ; r.dml = c->dMuLv; r.cnt = c->cnt_dz; r.guard = c->blk + kBlkFxErr;
-                r.ngrp = cdiv(a.Z, 8); r.zg = cdiv(a.Z, r.ngrp); r.nred = (a.Mbp / 16) * r.ngrp;
+                // (Z % 4 == 0: groups of a multiple of 4 latents, so VAEB_LAT_ST4 reducers can
+                // publish whole 16-byte runs; MNIST-20: 8, 8, 4)
+                r.ngrp = cdiv(a.Z, 8); r.zg = cdiv(a.Z, r.ngrp);
+                if (a.Z % 4 == 0) { r.zg = (r.zg + 3) & ~3; r.ngrp = cdiv(a.Z, r.zg); }
+                r.nred = (a.Mbp / 16) * r.ngrp;
                 r.nctH = cdiv(a.H, 16); r.L = a.L; r.est = a.est; r.Mb = a.Mb; r.Mbp = a.Mbp; r.Z = a.Z; r.sc = a.sc;
-                r.rep = (int)(c->cap * 2 * a.Z);   // the copies of [dMu | dLv], one per XCD
             }
             pr.mark(40);
             REP(pr) if (int rc = launch_wgrad(c, s, g12, 3, opt, &e1, a, &d3)) return rc;
@@ -1346,8 +1349,7 @@ int vaeb_create(const vaeb_config* cfg, vaeb_ctx** out) {
     if (!rc && gaussian(c)) c->dA6 = c->dA2 + (size_t)RL * D;
     rc = rc ? rc : dalloc(&c->dA1, (size_t)RL * H);
     rc = rc ? rc : dalloc(&c->dZ, (size_t)RL * Z);
-    // (kLatRep copies: the deferred latent backward publishes one per XCD, kernels_aux.hpp)
-    rc = rc ? rc : dalloc(&c->dMuLv, (size_t)kLatRep * R * 2 * Z);
+    rc = rc ? rc : dalloc(&c->dMuLv, (size_t)R * 2 * Z);
     rc = rc ? rc : dalloc(&c->dA3, (size_t)R * H);
     rc = rc ? rc : dalloc(&c->kl_part, (size_t)RL * cdiv(Z, 16));
     rc = rc ? rc : dalloc(&c->lp_part, (size_t)RL * cdiv(D, 16));
@@ -1356,7 +1358,7 @@ int vaeb_create(const vaeb_config* cfg, vaeb_ctx** out) {
         rc = rc ? rc : dalloc(&c->slab_ml, (size_t)(Bp * nctH * 64));
         rc = rc ? rc : dalloc(&c->slab_dz, (size_t)(g.L * Bp * nctH * 32));
         rc = rc ? rc : dalloc(&c->cnt_ml, (size_t)(Bp / 16));
-        rc = rc ? rc : dalloc(&c->cnt_dz, (size_t)std::max<int64_t>(Bp / 16, kLatRep * kLatCntStride));
+        rc = rc ? rc : dalloc(&c->cnt_dz, (size_t)std::max<int64_t>(Bp / 16, kLatCnt * kLatCntStride));
         rc = rc ? rc : dalloc(&c->w2pend, 1);
         // one allocation: the guard word the contributors set sits at acc_ml[-1] (latent.hpp fx_inc)
         const size_t nacc = (size_t)(Bp * 2 * Z * kFxStride);
