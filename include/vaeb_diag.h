@@ -47,13 +47,15 @@ int vaeb_debug_timeline(vaeb_ctx* ctx, int32_t batch_index, uint64_t* out, int64
 
 /* Test hook for the bf16 GEMM engine: C[M x N] = sum_k A(m, k) B(k, n) with the operands
  * rounded to bf16 on device.  a_kouter = 0: A is stored [M x K], 1: [K x M]; b_kouter = 0:
- * B is stored [N x K], 1: [K x N].  ksplit K slices are summed in fixed order.  Uses the
- * context's device and stream. */
+ * B is stored [N x K], 1: [K x N].  ksplit K slices are summed in fixed order; ksplit < 0: the
+ * 256 x 256 8-phase main loop with -ksplit slices; -22: two slices combined inside the launch
+ * (split2_combine).  Uses the context's device and stream. */
 int vaeb_test_gemm_bf16(vaeb_ctx* ctx, int32_t a_kouter, int32_t b_kouter, int32_t M, int32_t N, int32_t K,
                         const float* A, const float* B, float* C, int32_t ksplit);
 /* Diagnostics: mean time (ms) of `reps` back-to-back launches of the bf16 GEMM on
  * device-generated uniform [-1, 1) operands of the given layouts, bias + bf16-store
- * epilogue; tile width 128 / 256 (0: the engine's choice). */
+ * epilogue; tile width 128 / 256 (0: the engine's choice; 8: 256 x 256 on the 8-phase loop;
+ * 9: the same as two K slices combined in the launch). */
 int vaeb_bench_gemm_bf16(vaeb_ctx* ctx, int32_t a_kouter, int32_t b_kouter, int32_t M, int32_t N, int32_t K,
                          int32_t tile_n, int32_t reps, float* out_ms);
 

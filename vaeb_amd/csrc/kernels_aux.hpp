@@ -417,12 +417,15 @@ DEV void lat_reduce_wg(const LatRed& r, int wi, f32x4* red, float (*dzs)[17], ui
 
 // Consumer side: one lane polls the counter (sc1 loads, s_sleep between polls, bounded), the
 // workgroup joins a barrier; every later load of [dMu | dLv] in the workgroup is an sc1 load.
+#ifndef VAEB_POLL_SLEEP
+#define VAEB_POLL_SLEEP 2   // s_sleep units (64 clocks) between polls (A/B builds: other values)
+#endif
 DEV void lat_wait(int* cnt, int nred, uint64_t* const* guard) {
     if (threadIdx.x == 0) {
         typedef __attribute__((address_space(1))) int gi32;
         uint32_t spins = 0;
         while (__hip_atomic_load((gi32*)cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < nred) {
-            __builtin_amdgcn_s_sleep(2);
+            __builtin_amdgcn_s_sleep(VAEB_POLL_SLEEP);
             if (++spins >= (1u << 20)) {   // ~1 s: never a hang; the step reports a status instead
                 __hip_atomic_fetch_or((__attribute__((address_space(1))) unsigned long long*)*guard,
                                       (unsigned long long)kGuardHandoffTimeout, __ATOMIC_RELAXED,
