@@ -39,6 +39,35 @@ def test_folded_launch_flops_sum_to_step():
     assert fl["bf_dhd_dW26"] == fl["bf_dhd"] + fl["bf_dW26"]
 
 
+def test_deferred_dw2_launch_flops_sum_to_step():
+    """Round 4's MNIST form: the previous step's dW2 rides the encoder launch, the dhd launch has
+    none; the four launches still cover the step (the roofline divides by these)."""
+    for gauss in (False, True):
+        fl = bench.phase_flops(784, 500, 20, 100, gaussian=gauss)
+        parts = ["p1_enc_latent_w2", "p4_decout_z", "p5_dhd_dz", "p8_wgrad_w3w45w1"]
+        assert sum(fl[k] for k in parts) == bench.step_flops(784, 500, 20, 100, gaussian=gauss)
+
+
+def test_library_launch_names_have_flops_and_symbols():
+    """Every profile id the library emits for the fp32 four-launch step has a FLOP count and a
+    kernel symbol for the committed PMC lookup (bench.KERNEL_SYMBOLS)."""
+    src = open(os.path.join(ROOT, "vaeb_amd", "csrc", "vaeb_hip.hip")).read()
+    fl = bench.phase_flops(784, 500, 20, 100)
+    for name in ("p1_enc_latent_w2", "p5_dhd_dz", "p8_wgrad_w3w45w1", "p4_decout_z"):
+        assert f'"{name}"' in src
+        assert name in fl and name in bench.KERNEL_SYMBOLS
+
+
+def test_round4_traffic_file_resolves_every_launch():
+    """bench.py reads roofline.traffic from the committed round-4 PMC passes: each of the four
+    MNIST launches resolves to a per-launch byte count there."""
+    path = bench.PMC_FILES["mnist"]
+    assert os.path.exists(path), path
+    for name in ("p1_enc_latent_w2", "p4_decout_z", "p5_dhd_dz", "p8_wgrad_w3w45w1"):
+        v = bench.committed_traffic(name, path)
+        assert v is not None and v > 1e6, (name, v)
+
+
 def test_bf16_launch_flops_sum_to_step():
     fl = bench.phase_flops(4096, 2048, 128, 8192)
     parts = ["bf_enc", "bf_heads", "bf_dechid", "bf_decout", "bf_dhd", "bf_dW26", "bf_dz", "bf_dW1", "bf_dh",
