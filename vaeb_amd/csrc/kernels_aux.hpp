@@ -418,7 +418,8 @@ DEV void lat_reduce_wg(const LatRed& r, int wi, f32x4* red, float (*dzs)[17], ui
 // Consumer side: one lane polls the counter (sc1 loads, s_sleep between polls, bounded), the
 // workgroup joins a barrier; every later load of [dMu | dLv] in the workgroup is an sc1 load.
 #ifndef VAEB_POLL_SLEEP
-#define VAEB_POLL_SLEEP 2   // s_sleep units (64 clocks) between polls (A/B builds: other values)
+#define VAEB_POLL_SLEEP 30   // s_sleep units (64 clocks) between polls: fewer polls of the one counter line
+                            // (A/B, 4000-step runs: 2 -> 34.66 / 34.72 us, 10 -> 34.48 / 34.51, 30 -> 34.34 / 34.35)
 #endif
 DEV void lat_wait(int* cnt, int nred, uint64_t* const* guard) {
     if (threadIdx.x == 0) {
