@@ -419,7 +419,8 @@ DEV void lat_reduce_wg(const LatRed& r, int wi, f32x4* red, float (*dzs)[17], ui
 // workgroup joins a barrier; every later load of [dMu | dLv] in the workgroup is an sc1 load.
 #ifndef VAEB_POLL_SLEEP
 #define VAEB_POLL_SLEEP 30   // s_sleep units (64 clocks) between polls: fewer polls of the one counter line
-                            // (A/B, 4000-step runs: 2 -> 34.66 / 34.72 us, 10 -> 34.48 / 34.51, 30 -> 34.34 / 34.35)
+                            // (A/B, 4000-step runs: 2 -> 34.66 / 34.72 us, 10 -> 34.48 / 34.51, 30 -> 34.34 / 34.35;
+                            // then 30 -> 34.26 / 34.29, 60 -> 34.38 / 34.33, 110 -> 35.61 / 35.55)
 #endif
 DEV void lat_wait(int* cnt, int nred, uint64_t* const* guard) {
     if (threadIdx.x == 0) {
