@@ -40,6 +40,18 @@ int vaeb_busy(vaeb_ctx* ctx, int32_t us);
  * all-reduce + Adagrad overlap the backward on a second stream (-1: no communicator), and
  * the communicator's world size (1 without one). */
 int vaeb_comm_info(vaeb_ctx* ctx, int32_t* rccl_version, int32_t* dp_overlap, int32_t* world);
+/* Host-only diagnostics (no device call, no context): the sharded data-parallel optimizer's
+ * index plan exactly as a rank's step computes it (vaeb_hip.hip dp_bucket_*_runs,
+ * dp_shard_len, dp_opt_range, dp_foreign_range; the reference's simultaneous Adagrad,
+ * VAEB.py:426-444, split over ranks).  bucket: 0 = A (W2 | W6), 1 = B (the rest and the SGVB
+ * slot), 2 = all.  sharded: 1 = reduce-scatter / own shard / all-gather, 0 = replicated.
+ * Outputs (each may be NULL): out_P the arena length; runs[3 * 3] per run (lo, n, shard
+ * length S), out_nrun runs; own[2 * 6] the (lo, n) index runs this rank's optimizer launch
+ * updates, out_nown of them, out_book whether it also books the SGVB slot; foreign[2 * 6]
+ * the runs other ranks own (the bf16 shadow fix), out_nforeign of them. */
+int vaeb_dp_plan(const vaeb_config* cfg, int32_t world, int32_t rank, int32_t sharded, int32_t bucket,
+                 int64_t* out_P, int64_t* runs, int32_t* out_nrun, int64_t* own, int32_t* out_nown,
+                 int32_t* out_book, int64_t* foreign, int32_t* out_nforeign);
 /* Diagnostics: one eager step with a 100 MHz s_memrealtime stamp per workgroup at the
  * stage boundaries of every launch; out = [launch][1024 workgroups][8 slots]. */
 int vaeb_debug_timeline(vaeb_ctx* ctx, int32_t batch_index, uint64_t* out, int64_t cap,

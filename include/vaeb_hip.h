@@ -156,7 +156,10 @@ int vaeb_get_step(vaeb_ctx* ctx, int64_t* step);
  * only, VAEB.py:189-203, so a resumed run restarts Adagrad): one file holding the model
  * shape, theta, the Adagrad accumulators, the Philox seed / step and (FV / FVS) the
  * variational state.  A context loaded from it continues bit-identically to the run that
- * wrote it.  Loading checks that the file's D, H, Z, L, decoder and estimator match. */
+ * wrote it.  Loading checks that the file's D, H, Z, L, decoder and estimator match.
+ * With a sharded data-parallel communicator (world > 1) saving is a collective: every rank
+ * calls it (the Adagrad shards are all-gathered first); a rank passing path == NULL joins the
+ * gather and writes nothing (rank 0 writes the file). */
 int vaeb_checkpoint_save(vaeb_ctx* ctx, const char* path);
 int vaeb_checkpoint_load(vaeb_ctx* ctx, const char* path);
 

@@ -90,6 +90,19 @@ class RecordingCtx:
         out, self.acc = tuple(self.acc), [0.0, 0]
         return out
 
+    def checkpoint_save(self, path):
+        """vaeb_checkpoint_save under the sharded optimizer is a collective (the Adagrad shards
+        are all-gathered before the write): modelled with a gloo all-gather every rank must
+        join; path None = join without writing."""
+        if self.world > 1 and self.uid is not None:
+            import torch
+            import torch.distributed as dist
+            parts = [torch.zeros(4, dtype=torch.float64) for _ in range(self.world)]
+            dist.all_gather(parts, torch.tensor(self.theta[:4]))
+        if path is not None:
+            with open(path, "w") as f:
+                f.write("state")
+
     def close(self):
         pass
 
@@ -142,7 +155,7 @@ def test_cli_world_size_two(tmp_path, monkeypatch, scaling):
     monkeypatch.chdir(tmp_path)
     trace = str(tmp_path / "t.csv")
     argv = ARGV + ['--trace_file', trace, '--world_size', '2', '--dp_scaling', scaling,
-                   '--save_file', str(tmp_path / 'm.mdl')]
+                   '--save_file', str(tmp_path / 'm.mdl'), '--state_file', str(tmp_path / 'm.state')]
     res = _two_ranks(argv)
     (c0, u0, th0, o0, out0), (c1, u1, th1, o1, out1) = res[0], res[1]
     if scaling == "strong":   # the reference's 100-row minibatch split 50 / 50
@@ -161,6 +174,13 @@ def test_cli_world_size_two(tmp_path, monkeypatch, scaling):
     rows = open(trace).read().splitlines()
     assert rows[0] == 'num_samples,L,Lvalid' and len(rows) == 5 and rows[1] == rows[2]
     assert os.path.exists(tmp_path / 'm.mdl')    # written once, by rank 0
+    # the native checkpoint: a collective every rank joined, written by rank 0
+    assert open(tmp_path / 'm.state').read() == "state"
+    # the .mdl header holds the reference-level batch size (the global minibatch), not this
+    # rank's share: strong 100, weak 200 rows per step
+    from vaeb_amd.pickle_static import read_mdl
+    hdr, _ = read_mdl(str(tmp_path / 'm.mdl'))
+    assert int(hdr["batch_size"]) == (100 if scaling == "strong" else 200)
     if scaling == "strong":
         # the same steps as one process on the whole minibatch
         monkeypatch.delenv("WORLD_SIZE", raising=False)

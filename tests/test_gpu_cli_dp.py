@@ -81,3 +81,31 @@ def test_cli_world1_communicator_fp32_equals_fused_step(tmp_path, monkeypatch):
         model.close()
         rows.append(_rows(t))
     np.testing.assert_allclose(rows[0], rows[1], rtol=1e-6)
+
+
+@pytest.mark.parametrize("dtype", ["float32", "bf16"])
+def test_cli_world1_sharded_optimizer_equals_replicated(tmp_path, monkeypatch, dtype):
+    """the sharded DP optimizer (reduce-scatter -> own-shard Adagrad ->
+    all-gather, VAEB_DP_SHARD=1) through cli.main at --world_size 1, against the replicated
+    all-reduce + Adagrad (VAEB_DP_SHARD=0): the same trace, parameters and native checkpoint
+    (--state_file: the Adagrad shards gathered before the write), bit for bit."""
+    from vaeb_amd import cli
+    _clean_env(monkeypatch)
+    monkeypatch.chdir(tmp_path)
+    x = O.synthetic_mnist(n=1500, seed=3)
+    monkeypatch.setattr(cli, "load_dataset", lambda continuous, synthetic=False, splits=2: (x[:1200], x[1200:]))
+    shape = ['--n_latent', '20'] if dtype == "float32" else ['--hidden_unit', '64', '--n_latent', '16',
+                                                              '--batch_size', '120']
+    out = {}
+    for shard in ("1", "0"):
+        monkeypatch.setenv("VAEB_DP_SHARD", shard)
+        t = str(tmp_path / f"t{shard}.csv")
+        st = str(tmp_path / f"s{shard}.ckpt")
+        model, _ = cli.main(['--n_epochs', '2', '--world_size', '1', '--dtype', dtype, '--trace_file', t,
+                             '--trace_dedup', '1', '--state_file', st] + shape)
+        assert model._ctx.comm_count() == 1
+        out[shard] = (_rows(t), model._ctx.get_params(), open(st, "rb").read())
+        model.close()
+    assert out["1"][0] == out["0"][0]
+    assert np.array_equal(out["1"][1], out["0"][1])
+    assert out["1"][2] == out["0"][2]

@@ -490,6 +490,47 @@ def test_deferred_dw2_is_bitwise_the_same_step(kw, monkeypatch):
     assert np.array_equal(ref[4], ref[5])   # resume: the same two steps from the checkpoint
 
 
+def test_deferred_dw2_pending_after_a_replayed_single_step():
+    """a one-step update_many / update_async after a flush is a graph REPLAY with
+    no eager first step; the replayed step leaves its dW2 pending, so the next host read
+    (get_params, the Adagrad state, a validation, a checkpoint) must flush it.  The sequence
+    the advisor named -- update_many(order), get_params, update_async(i), get_params /
+    validate -- and single-step epochs between evaluations, bit for bit against the in-step
+    dW2 (VAEB_DW2_DEFER=0)."""
+    import os
+    from vaeb_amd import _lib
+    cfg = O.Config(D=784, H=500, Z=20)
+    x = data_for(cfg, 800)
+    res = {}
+    for defer in ("1", "0"):
+        os.environ["VAEB_DW2_DEFER"] = defer
+        try:
+            ctx = _lib.Context(cfg.D, cfg.H, cfg.Z, 100, max_eval_rows=200, use_graph=True)
+        finally:
+            del os.environ["VAEB_DW2_DEFER"]
+        ctx.set_data(x)
+        ctx.set_params(O.flatten(O.init_params(cfg)))
+        ctx.set_eps_mode(_lib.EPS_PHILOX, 10)
+        out = []
+        ctx.update_many(np.array([3, 1, 4], np.int32))      # captures the graphs, replays
+        out.append(ctx.get_params())                        # flush
+        ctx.update_async(2)                                 # one replayed step, no eager step
+        out.append(ctx.get_params())                        # must include that step's dW2
+        out.append(ctx.get_adagrad_state())
+        ctx.update_many(np.array([6], np.int32))            # a one-minibatch epoch
+        out.append(ctx.validate(x[:200]))                   # the evaluation flushes first
+        ctx.update_many(np.array([5], np.int32))
+        out.append(ctx.validate(x[200:400]))
+        ctx.update_many(np.array([0, 7], np.int32))         # training after the evaluations
+        out.append(ctx.get_params())
+        out.append(ctx.get_adagrad_state())
+        out.append(ctx.epoch_elbo()[0])
+        ctx.close()
+        res[defer] = out
+    for i, (a, b) in enumerate(zip(res["1"], res["0"])):
+        assert np.array_equal(np.asarray(a), np.asarray(b)), i
+
+
 def test_fixed_point_handoff_overflow_is_reported_not_silent():
     """The counted fixed-point hand-off (latent.hpp fx_inc) at Frey 560-200-2 (fan-in 13, the
     atomic form): an encoder partial beyond its range -- here every W4 entry 1e3, so the mu

@@ -39,7 +39,8 @@ EXPORTS = [
     "vaeb_ae_train_many", "vaeb_ae_reconstruct", "vaeb_ae_encode", "vaeb_ae_decode",
 ]
 DIAG_EXPORTS = ["vaeb_profile_steps", "vaeb_kernel_name", "vaeb_debug_timeline", "vaeb_test_gemm_bf16",
-                "vaeb_bench_gemm_bf16", "vaeb_graph_status", "vaeb_comm_info", "vaeb_time_update_many", "vaeb_busy"]
+                "vaeb_bench_gemm_bf16", "vaeb_graph_status", "vaeb_comm_info", "vaeb_time_update_many", "vaeb_busy",
+                "vaeb_dp_plan"]
 GRAPH_MODES = {0: "off", 1: "not_captured", 2: "replay", 3: "eager_fallback"}
 AE_MAX_LAYERS = 8
 AE_BINARY, AE_CONT = 0, 1
@@ -132,6 +133,10 @@ def load():
         "vaeb_graph_status": ([_P, ctypes.POINTER(ctypes.c_int32), ctypes.c_char_p, ctypes.c_int32], ctypes.c_int),
         "vaeb_comm_info": ([_P] + [ctypes.POINTER(ctypes.c_int32)] * 3, ctypes.c_int),
         "vaeb_busy": ([_P, ctypes.c_int32], ctypes.c_int),
+        "vaeb_dp_plan": ([ctypes.POINTER(VaebConfig)] + [ctypes.c_int32] * 4 +
+                         [ctypes.POINTER(_I64), ctypes.POINTER(_I64), ctypes.POINTER(ctypes.c_int32),
+                          ctypes.POINTER(_I64), ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int32),
+                          ctypes.POINTER(_I64), ctypes.POINTER(ctypes.c_int32)], ctypes.c_int),
         "vaeb_time_update_many": ([_P, ctypes.POINTER(ctypes.c_int32), ctypes.c_int32, _F,
                                    ctypes.POINTER(ctypes.c_double)], ctypes.c_int),
         "vaeb_debug_timeline": ([_P, ctypes.c_int32, ctypes.POINTER(ctypes.c_uint64), _I64,
@@ -165,6 +170,29 @@ def check(rc):
     if rc != 0:
         msg = _lib.vaeb_last_error().decode(errors="replace") if _lib is not None else "?"
         raise VaebError(f"libvaeb_hip error {rc}: {msg}")
+
+
+def dp_plan(D, H, Z, world, rank, bucket=2, sharded=True, decoder=DEC_BERNOULLI):
+    """The sharded DP optimizer's index plan as the library computes it (vaeb_dp_plan; host
+    only, no GPU).  bucket 0 = A (W2 | W6), 1 = B, 2 = all.  Returns a dict: P, runs [(lo, n,
+    S)], own [(lo, n)], book (bool), foreign [(lo, n)]."""
+    lib = load()
+    cfg = VaebConfig()
+    cfg.D, cfg.H, cfg.Z, cfg.B, cfg.L = D, H, Z, 1, 1
+    cfg.decoder = decoder
+    P = _I64()
+    runs = (_I64 * 9)()
+    own = (_I64 * 12)()
+    foreign = (_I64 * 12)()
+    nrun, nown, book, nfor = (ctypes.c_int32() for _ in range(4))
+    check(lib.vaeb_dp_plan(ctypes.byref(cfg), world, rank, int(bool(sharded)), bucket, ctypes.byref(P), runs,
+                           ctypes.byref(nrun), own, ctypes.byref(nown), ctypes.byref(book), foreign,
+                           ctypes.byref(nfor)))
+    return {"P": P.value,
+            "runs": [(runs[3 * j], runs[3 * j + 1], runs[3 * j + 2]) for j in range(nrun.value)],
+            "own": [(own[2 * k], own[2 * k + 1]) for k in range(nown.value)],
+            "book": bool(book.value),
+            "foreign": [(foreign[2 * k], foreign[2 * k + 1]) for k in range(nfor.value)]}
 
 
 def fptr(a: np.ndarray):
@@ -272,7 +300,8 @@ class Context:
 
     # ---- native checkpoint (theta, Adagrad state, Philox seed / step, FV state)
     def checkpoint_save(self, path):
-        check(self.lib.vaeb_checkpoint_save(self.h, os.fsencode(path)))
+        """path None: join a sharded DP gather without writing (every rank calls it at world > 1)."""
+        check(self.lib.vaeb_checkpoint_save(self.h, None if path is None else os.fsencode(path)))
 
     def checkpoint_load(self, path):
         check(self.lib.vaeb_checkpoint_load(self.h, os.fsencode(path)))

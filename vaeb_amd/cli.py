@@ -246,8 +246,10 @@ def train_model(args):
                 f.write('{0},{1},{2}\n'.format(model.N * (epoch + 1), LB, LBvalidation))
     if len(save_file) > 0 and lead:
         model.save(save_file)
-    if args.get('state_file') and lead:
-        model.save_state(args['state_file'])
+    if args.get('state_file'):
+        # a collective with the sharded DP optimizer (the Adagrad shards are gathered): every
+        # rank joins, rank 0 writes (rank 0 alone blocked in the all-gather)
+        model.save_state(args['state_file'] if lead else None)
     return model, data
 
 

@@ -181,6 +181,7 @@ struct vaeb_ctx {
     bool dw2_defer = true;
     int* w2pend = nullptr;        // device: 1 = a step's dW2 is pending (set by its dhd launch)
     bool w2_dirty = false;        // host: a step was enqueued since the last flush
+    bool w2_graph = false;        // host: the captured graphs hold deferred-dW2 steps (run_steps sets w2_dirty)
     int atomic_ho = 1;            // folded latent hand-offs: 1 by fan-in (ho_mode), 0 slabs
     bool graph_upload = true;     // hipGraphUpload at capture (VAEB_GRAPH_UPLOAD=0: at first launch)
     // the slab-only encoder on 1024-thread workgroups (16 waves splitting K: twice the loads in
@@ -206,6 +207,20 @@ struct vaeb_ctx {
 namespace {
 
 bool gaussian(const vaeb_ctx* c) { return c->c.decoder == VAEB_DEC_GAUSSIAN; }
+
+// The parameter arena in reference order W3 W4 W5 W1 W2 [W6] b3 b4 b5 b1 b2 [b6]
+// (VAEB.py:74-104): c->off, c->nparams, c->P from the config alone (no device call).
+void set_arena_layout(vaeb_ctx* c) {
+    const int64_t D = c->c.D, H = c->c.H, Z = c->c.Z;
+    std::vector<int64_t> sz = {D * H, H * Z, H * Z, Z * H, H * D};
+    if (gaussian(c)) sz.push_back(H * D);
+    sz.insert(sz.end(), {H, Z, Z, H, D});
+    if (gaussian(c)) sz.push_back(D);
+    c->nparams = (int)sz.size();
+    int64_t o = 0;
+    for (int i = 0; i < c->nparams; ++i) { c->off[i] = o; o += sz[i]; }
+    c->P = o;
+}
 
 uint64_t* next_dbg(vaeb_ctx* c) { return c->dbg ? c->dbg + (size_t)(c->dbg_slot++) * kDbgWG * 8 : nullptr; }
 
@@ -1135,6 +1150,7 @@ void free_graphs(vaeb_ctx* c) {
     for (auto& gn : c->gN) if (gn) hipGraphExecDestroy(gn);
     c->g1[0] = c->g1[1] = nullptr;
     for (auto& gn : c->gN) gn = nullptr;
+    c->w2_graph = false;
 }
 
 // Capture nsteps consecutive steps starting from parameter arena `par`.
@@ -1142,10 +1158,16 @@ int capture(vaeb_ctx* c, int nsteps, int par, hipGraphExec_t* out) {
     hipGraph_t gr = nullptr;
     HIP_TRY(hipStreamBeginCapture(c->s, hipStreamCaptureModeThreadLocal));
     int rc = 0;
+    // a captured deferred-dW2 step sets w2_dirty as it is recorded; what the host must know is
+    // that every REPLAY leaves a dW2 pending: w2_graph, applied by run_steps
+    const bool dirty0 = c->w2_dirty;
+    c->w2_dirty = false;
     for (int i = 0; i < nsteps && rc == 0; ++i) {
         rc = enqueue_train_step(c, par, false, i == 0);
         if (flips(c)) par ^= 1;
     }
+    if (c->w2_dirty) c->w2_graph = true;
+    c->w2_dirty = dirty0;
     hipError_t e = hipStreamEndCapture(c->s, &gr);
     if (rc) { if (gr) hipGraphDestroy(gr); return rc; }
     if (e != hipSuccess) return fail(VAEB_ERR_HIP, "hipStreamEndCapture: %s", hipGetErrorString(e));
@@ -1206,6 +1228,7 @@ int run_steps(vaeb_ctx* c, int n) {
                 if (flips(c)) c->par = m & 1;
                 i += m;
             }
+            if (n > 0 && c->w2_graph) c->w2_dirty = true;   // the last replayed step left its dW2 pending
             return 0;
         }
     }
@@ -1311,14 +1334,7 @@ int vaeb_create(const vaeb_config* cfg, vaeb_ctx** out) {
     }
     if (e != hipSuccess) { delete c; return fail(VAEB_ERR_HIP, "stream/event create: %s", hipGetErrorString(e)); }
     const int64_t D = g.D, H = g.H, Z = g.Z;
-    std::vector<int64_t> sz = {D * H, H * Z, H * Z, Z * H, H * D};
-    if (gaussian(c)) sz.push_back(H * D);
-    sz.insert(sz.end(), {H, Z, Z, H, D});
-    if (gaussian(c)) sz.push_back(D);
-    c->nparams = (int)sz.size();
-    int64_t o = 0;
-    for (int i = 0; i < c->nparams; ++i) { c->off[i] = o; o += sz[i]; }
-    c->P = o;
+    set_arena_layout(c);
     c->cap = std::max(r16(g.B), r16(c->c.max_eval_rows));
     const int64_t R = c->cap, RL = (int64_t)c->cap * g.L;
     int rc = 0;
@@ -1852,9 +1868,10 @@ struct FileCloser { FILE* f; ~FileCloser() { if (f) fclose(f); } };
 }  // namespace
 
 int vaeb_checkpoint_save(vaeb_ctx* c, const char* path) {
-    if (!c || !path) return fail(VAEB_ERR_ARG, "null argument");
+    if (!c) return fail(VAEB_ERR_ARG, "null argument");
     if (int rc = w2_flush(c)) return rc;   // a pending deferred dW2 (vaeb_ctx::dw2_defer)
     if (int rc = dp_gather_acc(c)) return rc;   // sharded DP: the whole Adagrad state (every rank calls)
+    if (!path) return 0;   // a non-writing rank: it joined the gather
     const vaeb_config& g = c->c;
     CkptHeader h{};
     memcpy(h.magic, kCkptMagic, 8);
@@ -2364,6 +2381,44 @@ int vaeb_comm_info(vaeb_ctx* c, int32_t* rccl_version, int32_t* dp_overlap, int3
     }
     if (dp_overlap) *dp_overlap = c->comm ? (c->dp_overlap ? 1 : 0) : -1;
     if (world) *world = c->comm ? c->world : 1;
+    return 0;
+}
+
+int vaeb_dp_plan(const vaeb_config* cfg, int32_t world, int32_t rank, int32_t sharded, int32_t bucket,
+                 int64_t* out_P, int64_t* runs, int32_t* out_nrun, int64_t* own, int32_t* out_nown, int32_t* out_book,
+                 int64_t* foreign, int32_t* out_nforeign) {
+    if (!cfg || world <= 0 || rank < 0 || rank >= world || bucket < 0 || bucket > 2)
+        return fail(VAEB_ERR_ARG, "bad plan arguments");
+    if (cfg->D <= 0 || cfg->H <= 0 || cfg->Z <= 0) return fail(VAEB_ERR_ARG, "dimensions must be positive");
+    // a host-only context holding exactly the fields the plan functions read (no stream, no
+    // allocation): the same code dp_reduce_update runs on a rank
+    vaeb_ctx c;
+    c.c = *cfg;
+    set_arena_layout(&c);
+    c.world = world;
+    c.rank = rank;
+    c.dp_shard = sharded != 0;
+    const DpBucket bk = bucket == 0 ? dp_bucket_a_runs(&c) : bucket == 1 ? dp_bucket_b_runs(&c) : dp_bucket_all_runs(&c);
+    if (out_P) *out_P = c.P;
+    if (runs)
+        for (int j = 0; j < bk.nrun; ++j) {
+            runs[3 * j] = bk.lo[j];
+            runs[3 * j + 1] = bk.n[j];
+            runs[3 * j + 2] = dp_shard_len(&c, bk.n[j]);
+        }
+    if (out_nrun) *out_nrun = bk.nrun;
+    auto put = [](const DpRange& r, int64_t* dst, int32_t* cnt) {
+        int k = 0;
+        while (k < kDpRuns && r.n[k]) {
+            if (dst) { dst[2 * k] = r.lo[k]; dst[2 * k + 1] = r.n[k]; }
+            ++k;
+        }
+        if (cnt) *cnt = k;
+    };
+    const DpRange o = dp_opt_range(&c, bk);
+    put(o, own, out_nown);
+    if (out_book) *out_book = o.book;
+    put(dp_foreign_range(&c, bk), foreign, out_nforeign);
     return 0;
 }
 

@@ -47,11 +47,19 @@ def free_port():
         return so.getsockname()[1]
 
 
-def spawn_ranks(n, cmd, poll_s=0.2, env_extra=None):
+RANK_HUNG = 124   # spawn_ranks: a rank still running after its peers finished (timeout(1)'s code)
+
+
+def spawn_ranks(n, cmd, poll_s=0.2, env_extra=None, straggler_s=None):
     """Start n rank processes of `cmd` (an argv list; one per GPU, RANK = LOCAL_RANK = r,
     WORLD_SIZE = n, rendezvous on 127.0.0.1) and wait.  The parent makes no GPU call.  If
     one rank fails the others are stopped (they would wait in a collective forever);
-    returns the first non-zero exit code, else 0."""
+    returns the first non-zero exit code, else 0.  Once any rank has exited 0 the others get
+    `straggler_s` seconds (VAEB_RANK_DEADLINE_S, default 600) to follow: a rank left alone in a
+    collective would otherwise hold the launcher forever.  Past it they are killed, the
+    still-running ranks are named on stderr, and the code is RANK_HUNG."""
+    if straggler_s is None:
+        straggler_s = float(os.environ.get("VAEB_RANK_DEADLINE_S", "600"))
     port = free_port()
     procs = []
     for r in range(n):
@@ -59,18 +67,31 @@ def spawn_ranks(n, cmd, poll_s=0.2, env_extra=None):
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), **(env_extra or {}))
         env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
         procs.append(subprocess.Popen(list(cmd), env=env))
+
+    def stop_all():
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+        for p in procs:
+            p.wait()
+
+    first_done = None
     while True:
         codes = [p.poll() for p in procs]
         bad = [c for c in codes if c not in (None, 0)]
         if bad:
-            for p in procs:
-                if p.poll() is None:
-                    p.kill()
-            for p in procs:
-                p.wait()
+            stop_all()
             return bad[0]
         if all(c == 0 for c in codes):
             return 0
+        if first_done is None and any(c == 0 for c in codes):
+            first_done = time.monotonic()
+        if first_done is not None and time.monotonic() - first_done > straggler_s:
+            hung = [r for r, c in enumerate(codes) if c is None]
+            print(f"spawn_ranks: rank(s) {hung} still running {straggler_s:g} s after a peer finished; "
+                  f"stopping them", file=sys.stderr, flush=True)
+            stop_all()
+            return RANK_HUNG
         time.sleep(poll_s)
 
 

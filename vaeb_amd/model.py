@@ -321,7 +321,9 @@ class VAEB:
         float32 ndarrays (no Theano wrapper)."""
         print('Saving model to: {0}'.format(file_name))
         with open(file_name, "wb") as f:
-            for v in (self.n_hidden_units, self.n_latent, self.continuous, self.learning_rate, self.batch_size,
+            # the reference-level batch size: under data parallelism self.batch_size is this
+            # rank's share, B_global the minibatch a step covers (ADVICE r4)
+            for v in (self.n_hidden_units, self.n_latent, self.continuous, self.learning_rate, self.B_global,
                       np.random.RandomState(10), self.sigmaInit, self.L, self.genericEstimator):
                 pickle.dump(v, f, protocol=2)
             for a in self._param_arrays():
@@ -330,7 +332,9 @@ class VAEB:
     def save_state(self, file_name):
         """Native checkpoint (vaeb_checkpoint_save): theta, the Adagrad accumulators, the
         Philox seed / step and the variational state -- everything a bit-identical resume
-        needs, unlike the reference's .mdl (VAEB.py:189-203 keeps theta only)."""
+        needs, unlike the reference's .mdl (VAEB.py:189-203 keeps theta only).  With a
+        data-parallel communicator every rank calls it (the sharded Adagrad state is gathered
+        first); file_name None joins that gather without writing."""
         self._ctx.checkpoint_save(file_name)
 
     def load_state(self, file_name):
