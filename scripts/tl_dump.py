@@ -22,5 +22,5 @@ for i in range(30):
     ctx.update(i % 20)
 reps = np.stack([ctx.debug_timeline(r) for r in range(5)])
 os.makedirs("gpurun_out", exist_ok=True)
-np.savez_compressed(f"gpurun_out/tl_{tag}.npz", tl=reps)
+np.savez_compressed(f"gpurun_out/tl_{tag}{os.environ.get('TL_SUFFIX', '')}.npz", tl=reps)
 print("saved", reps.shape)

@@ -402,11 +402,15 @@ def test_atomic_and_slab_handoffs_agree(kw, monkeypatch):
     # "dw2now": VAEB_DW2_DEFER=0, each step's dW2 (| dW6) in its own dhd launch (default 1: in the
     # next step's encoder launch, the last one flushed by get_params)
     # "encfx": VAEB_ENC_FX=1, the encoder's [mu | lv] as exact fixed-point sums read by the decoder
+    # "dhd2": VAEB_DHD2=1, two dA1 column tiles per 1024-thread dhd workgroup where one-tile
+    # workgroups exceed the atomics' fan-in (MNIST: 16 instead of 32 contributors), the counted
+    # atomics completing [dMu | dLv] in the dhd launch (default 0: the last launch's reducers)
     modes = {"atomic": ("1", "0", "1", "2", "2", "1", "1"), "slab": ("0", "0", "1", "2", "2", "1", "1"),
              "decred": ("1", "1", "1", "2", "2", "1", "1"), "unfolded": ("1", "0", "0", "2", "2", "1", "1"),
              "dct1": ("1", "0", "1", "1", "2", "1", "1"), "enc8": ("1", "1", "1", "2", "0", "1", "1"),
-             "enc16slab": ("1", "0", "1", "2", "1", "1", "1"), "ticket": ("0", "0", "1", "2", "2", "0", "1"),
-             "dw2now": ("1", "0", "1", "2", "2", "1", "0"), "encfx": ("1", "0", "1", "2", "2", "1", "1", "1")}
+             "enc16slab": ("1", "0", "1", "2", "1", "1", "1"), "ticket": ("0", "0", "1", "2", "2", "0", "1", "0", "0"),
+             "dw2now": ("1", "0", "1", "2", "2", "1", "0"), "encfx": ("1", "0", "1", "2", "2", "1", "1", "1"),
+             "dhd2": ("1", "0", "1", "2", "2", "1", "1", "0", "1")}
     for mode in modes:
         for use_graph in (True, False):
             monkeypatch.setenv("VAEB_ATOMIC_HO", modes[mode][0])
@@ -417,6 +421,7 @@ def test_atomic_and_slab_handoffs_agree(kw, monkeypatch):
             monkeypatch.setenv("VAEB_BWD_DEFER", modes[mode][5])
             monkeypatch.setenv("VAEB_DW2_DEFER", modes[mode][6])
             monkeypatch.setenv("VAEB_ENC_FX", modes[mode][7] if len(modes[mode]) > 7 else "0")
+            monkeypatch.setenv("VAEB_DHD2", modes[mode][8] if len(modes[mode]) > 8 else "0")
             ctx = _lib.Context(cfg.D, cfg.H, cfg.Z, B, L=cfg.L,
                                decoder=_lib.DEC_GAUSSIAN if cfg.continuous else _lib.DEC_BERNOULLI,
                                max_eval_rows=B, use_graph=use_graph)
@@ -433,7 +438,7 @@ def test_atomic_and_slab_handoffs_agree(kw, monkeypatch):
         assert np.array_equal(out[mode, True][1], out[mode, False][1])
     es = out["slab", True][0]
     frac = {}
-    for mode in ("atomic", "decred", "unfolded", "dct1", "enc8", "enc16slab", "ticket", "dw2now", "encfx"):
+    for mode in ("atomic", "decred", "unfolded", "dct1", "enc8", "enc16slab", "ticket", "dw2now", "encfx", "dhd2"):
         ea = out[mode, True][0]
         assert abs(ea - es) <= 1e-5 * abs(es), (mode, ea, es)
         d = np.abs(out[mode, True][1] - out["slab", True][1])
@@ -457,9 +462,13 @@ def test_deferred_dw2_is_bitwise_the_same_step(kw, monkeypatch):
     cfg = O.Config(**kw)
     x = data_for(cfg, 800)
     res = {}
-    for defer in ("1", "0"):
+    # VAEB_DHD2=0: the latent backward's form held fixed (the deferred reducers), so the deferral
+    # alone differs; "dhd2" runs the two-tile dhd launch (VAEB_DHD2=1; only with the deferral), whose
+    # graph and eager runs must agree bitwise along the same sequence
+    for defer, dhd2 in (("1", "0"), ("0", "0"), ("1", "1")):
         for use_graph in (True, False):
             monkeypatch.setenv("VAEB_DW2_DEFER", defer)
+            monkeypatch.setenv("VAEB_DHD2", dhd2)
             ctx = _lib.Context(cfg.D, cfg.H, cfg.Z, 100, decoder=int(cfg.continuous), max_eval_rows=200,
                                use_graph=use_graph)
             ctx.set_data(x)
@@ -482,12 +491,14 @@ def test_deferred_dw2_is_bitwise_the_same_step(kw, monkeypatch):
             out.append(ctx.get_adagrad_state())
             out.append(ctx.epoch_elbo()[0])
             ctx.close()
-            res[defer, use_graph] = out
-    ref = res["0", True]
-    for key, out in res.items():
-        for a, b in zip(out, ref):
-            assert np.array_equal(np.asarray(a), np.asarray(b)), key
-    assert np.array_equal(ref[4], ref[5])   # resume: the same two steps from the checkpoint
+            res[defer, dhd2, use_graph] = out
+    for group in (("1", "0"), ("0", "0")), (("1", "1"),):
+        ref = res[group[-1] + (True,)]
+        for key, out in res.items():
+            if key[:2] in group:
+                for a, b in zip(out, ref):
+                    assert np.array_equal(np.asarray(a), np.asarray(b)), key
+        assert np.array_equal(ref[4], ref[5])   # resume: the same two steps from the checkpoint
 
 
 def test_deferred_dw2_pending_after_a_replayed_single_step():
@@ -502,12 +513,14 @@ def test_deferred_dw2_pending_after_a_replayed_single_step():
     cfg = O.Config(D=784, H=500, Z=20)
     x = data_for(cfg, 800)
     res = {}
-    for defer in ("1", "0"):
-        os.environ["VAEB_DW2_DEFER"] = defer
+    # (defer, dhd2, graph): the deferral against the in-step dW2 with the latent backward's form
+    # held fixed (VAEB_DHD2=0), and the two-tile dhd form (VAEB_DHD2=1) replayed against eager steps
+    for key in (("1", "0", True), ("0", "0", True), ("1", "1", True), ("1", "1", False)):
+        os.environ["VAEB_DW2_DEFER"], os.environ["VAEB_DHD2"] = key[0], key[1]
         try:
-            ctx = _lib.Context(cfg.D, cfg.H, cfg.Z, 100, max_eval_rows=200, use_graph=True)
+            ctx = _lib.Context(cfg.D, cfg.H, cfg.Z, 100, max_eval_rows=200, use_graph=key[2])
         finally:
-            del os.environ["VAEB_DW2_DEFER"]
+            del os.environ["VAEB_DW2_DEFER"], os.environ["VAEB_DHD2"]
         ctx.set_data(x)
         ctx.set_params(O.flatten(O.init_params(cfg)))
         ctx.set_eps_mode(_lib.EPS_PHILOX, 10)
@@ -526,9 +539,10 @@ def test_deferred_dw2_pending_after_a_replayed_single_step():
         out.append(ctx.get_adagrad_state())
         out.append(ctx.epoch_elbo()[0])
         ctx.close()
-        res[defer] = out
-    for i, (a, b) in enumerate(zip(res["1"], res["0"])):
-        assert np.array_equal(np.asarray(a), np.asarray(b)), i
+        res[key] = out
+    for k1, k2 in ((("1", "0", True), ("0", "0", True)), (("1", "1", True), ("1", "1", False))):
+        for i, (a, b) in enumerate(zip(res[k1], res[k2])):
+            assert np.array_equal(np.asarray(a), np.asarray(b)), (k1, i)
 
 
 def test_fixed_point_handoff_overflow_is_reported_not_silent():

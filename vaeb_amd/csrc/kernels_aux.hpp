@@ -518,7 +518,13 @@ DEV void da3_panel(const Da3Src& d, int kb, int j0, bool store, float (*sb)[kWP]
 #pragma unroll
     for (int ts = 0; ts < TS; ++ts)
 #pragma unroll
-        for (int c = 0; c < 4; ++c) bw[ts][c] = ld_w45(bw4, bw5, Z, c < nkc ? H : 0, j0 + 16 * ts + li, c * 16 + 4 * q, vz);
+        for (int c = 0; c < 4; ++c) {
+#ifdef VAEB_KO_DA3_NOW45   // timing-only knock-out builds of the dA3 panel (wrong results)
+            bw[ts][c] = f32x4{1e-3f * c, 2e-3f, 3e-3f, 4e-3f};
+#else
+            bw[ts][c] = ld_w45(bw4, bw5, Z, c < nkc ? H : 0, j0 + 16 * ts + li, c * 16 + 4 * q, vz);
+#endif
+        }
 #pragma unroll
     for (int u = 0; u < NR; ++u) {
         const int r0 = kb + 16 * (wv + NWV * u);
@@ -532,7 +538,11 @@ DEV void da3_panel(const Da3Src& d, int kb, int j0, bool store, float (*sb)[kWP]
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int mm = r0 + 4 * q + r;
+#ifdef VAEB_KO_DA3_NOH
+                hv[u][ts][r] = 0.5f + 1e-3f * r + (float)mm * 1e-6f; (void)n;
+#else
                 hv[u][ts][r] = bld(bh, (n < H && mm < d.Mb) ? (uint32_t)(mm * H + n) * 4u : kOOB);
+#endif
             }
         }
     }
@@ -544,7 +554,13 @@ DEV void da3_panel(const Da3Src& d, int kb, int j0, bool store, float (*sb)[kWP]
             const int r0 = kb + 16 * (wv + NWV * u);
             const int rl = r0 < d.Mbp ? d.Mbp : 0;
 #pragma unroll
-            for (int c = 0; c < 4; ++c) av[u][c] = kc4x<16>(bd, K2, r0 + li, c * 16 + 4 * q, c < nkc ? rl : 0, K2, vd);
+            for (int c = 0; c < 4; ++c) {
+#ifdef VAEB_KO_DA3_NODML
+                av[u][c] = f32x4{1e-3f * c, 2e-3f * u, 3e-3f, 4e-3f};
+#else
+                av[u][c] = kc4x<16>(bd, K2, r0 + li, c * 16 + 4 * q, c < nkc ? rl : 0, K2, vd);
+#endif
+            }
         }
     }
 #pragma unroll
@@ -555,9 +571,14 @@ DEV void da3_panel(const Da3Src& d, int kb, int j0, bool store, float (*sb)[kWP]
 #pragma unroll
         for (int ts = 0; ts < TS; ++ts) {
             f32x4 acc = zero4();
+#ifdef VAEB_KO_DA3_NOMFMA   // the loaded operands summed instead of multiplied (no MFMA chain)
+#pragma unroll
+            for (int c = 0; c < 4; ++c) acc += av[u][c] + bw[ts][c];
+#else
 #pragma unroll
             for (int c = 0; c < 4; ++c)
                 if (c < nkc) acc = mfma4(av[u][c], bw[ts][c], acc);
+#endif
             const int n = j0 + 16 * ts + li;
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
@@ -653,7 +674,10 @@ DEV void wgrad_body(const WA& p, const WGroup& g, int bid, float (*sa)[kWP], flo
             off[t][r] = ok ? (uint32_t)idx * 4u : kOOB;
             // unconditional loads (no branch): the waitcnt pass then sees them retired
             // by the first panel wait instead of re-waiting after every epilogue store
-            const uint32_t lo = (upd && kh == 0) ? off[t][r] : kOOB;
+            uint32_t lo = (upd && kh == 0) ? off[t][r] : kOOB;
+#ifdef VAEB_KO_W3_NOPREF   // timing-only knock-out build (wrong results): no theta / acc prefetch
+            if constexpr (DA3) lo = kOOB;
+#endif
             th[t][r] = bld(bth, lo);
             ac[t][r] = bld(bac, lo);
         }
@@ -680,6 +704,9 @@ DEV void wgrad_body(const WA& p, const WGroup& g, int bid, float (*sa)[kWP], flo
             const int k = kb + kr;
             const int i = i0 + 4 * c4, j = j0 + 4 * c4;
             const bool jt = 4 * c4 < kWTJ;   // B columns beyond a narrow tile: no fetch
+#ifdef VAEB_KO_W3_NOX   // timing-only knock-out build: no X panel loads in the dW3 tiles
+            if constexpr (DA3) { ra[u] = zero4(); rb[u] = zero4(); continue; }
+#endif
             if (va) {
                 ra[u] = bld4(ba, (k < g.klim_at && i < g.rowsW) ? (uint32_t)(k * g.ld_at + i) * 4u : kOOB);
             } else {
@@ -738,10 +765,16 @@ DEV void wgrad_body(const WA& p, const WGroup& g, int bid, float (*sa)[kWP], flo
                 }
             }
         }
+#ifdef VAEB_KO_W3_NODA3   // timing-only knock-out build: the dA3 panel not formed (and no poll)
+        if constexpr (DA3) {
+            for (int e = tid; e < kWKB * 16; e += NTH) sb[e >> 4][e & 15] = 0.f;
+        }
+#else
         if constexpr (DA3 && DEFER)
             da3_panel<NWV, TS, true>(p.da3, kb, j0, i0 == 0, sb, p.hd.red_cnt, p.hd.nred,
                                      VAEB_DBG_ON(p.dbg) ? p.dbg + bid * 8 : nullptr);
         else if constexpr (DA3) da3_panel<NWV, TS>(p.da3, kb, j0, i0 == 0, sb);
+#endif
 #ifdef VAEB_TIMELINE
         if (VAEB_DBG_ON(p.dbg) && kb == 0 && tid == 0) p.dbg[bid * 8 + 2] = __builtin_amdgcn_s_memrealtime();
 #endif
@@ -824,6 +857,15 @@ DEV void wgrad_body(const WA& p, const WGroup& g, int bid, float (*sa)[kWP], flo
         if (VAEB_DBG_ON(p.dbg) && tid == 0) p.dbg[bid * 8 + 3] = __builtin_amdgcn_s_memrealtime();
         return;
     }
+#ifdef VAEB_KO_W3_NOSTORE   // timing-only knock-out build: the dW3 tiles store nothing
+    if constexpr (DA3) {
+        float sink = 0.f;
+        for (int t = 0; t < kWTS; ++t)
+            for (int r = 0; r < 4; ++r) { float a2 = ac[t][r]; sink += opt_rule(p.opt, th[t][r], a2, acc[t][r]) + a2; }
+        if (sink == 12345.678f) bst(bgr, 0, sink);
+        return;
+    }
+#endif
 #pragma unroll
     for (int t = 0; t < kWTS; ++t)
 #pragma unroll
@@ -907,6 +949,9 @@ __global__ __launch_bounds__(256) void wgrad3_kernel(WGradArgs3 p) {
             return;
         }
         b -= h.nred;
+#ifdef VAEB_TILE_DELAY   // A/B build: the tiles hold their bulk loads back so the reducers' slab loads go first
+        __builtin_amdgcn_s_sleep(VAEB_TILE_DELAY);
+#endif
     }
     const int bid = xcd_remap(b, h.total_wgs);
     if (VAEB_DBG_ON(p.dbg) && threadIdx.x == 0) p.dbg[bid * 8 + 0] = __builtin_amdgcn_s_memrealtime();

@@ -638,7 +638,11 @@ DEV void decout_z_body(const StepArgs& a) {
 #pragma unroll
                 for (int w = 0; w < NT; ++w) {
                     const int k = kb + 16 * q + 4 * r + u;
+#ifdef VAEB_KO_DEC_NOW2   // timing-only knock-out build: no W2 loads
+                    w2b[u][r][w] = (float)k * 1e-9f;
+#else
                     w2b[u][r][w] = p.b1(n0 + 16 * (w / NB) + li, k, w % NB);
+#endif
                 }
     };
     // ZM 2: the first kSlabPer slab loads of each thread are issued BEFORE the weight block:
@@ -663,7 +667,11 @@ DEV void decout_z_body(const StepArgs& a) {
 #pragma unroll
         for (int u = 0; u < kSlabPer; ++u) {
             const int ct = partS + u * npS;
+#ifdef VAEB_KO_DEC_NOSLAB   // timing-only knock-out build: no slab loads (mu, lv = biases)
+            sv0[u] = zero4(); (void)ct;
+#else
             sv0[u] = bld4(bsl, (partS < npS && ct < nctS) ? (uint32_t)((firstS + (int64_t)ct * nf4S) * 16) : kOOB);
+#endif
         }
     }
     load_block(64 * wave);
@@ -707,7 +715,11 @@ DEV void decout_z_body(const StepArgs& a) {
             f32x4 sum = zero4();
 #pragma unroll
             for (int u = 0; u < kSlabPer; ++u) sum += sv0[u];
+#ifdef VAEB_KO_DEC_NOSLAB
+            for (int c0 = nct; c0 < nct; c0 += kSlabPer * np) {
+#else
             for (int c0 = part + kSlabPer * np; c0 < nct; c0 += kSlabPer * np) {
+#endif
                 f32x4 v[kSlabPer];
 #pragma unroll
                 for (int u = 0; u < kSlabPer; ++u) {
@@ -857,6 +869,10 @@ DEV void decout_z_body(const StepArgs& a) {
         c[w] = t;
     }
     VAEB_STAMP_SYNC(a, 4);   // (timeline build) the epilogue's operands landed
+#ifdef VAEB_KO_DEC_NOEPI   // timing-only knock-out build: no likelihood epilogue, no stores
+    if (c[0] == 12345.678f) a.y[0] = c[NB - 1];
+    return;
+#endif
     p.epilogue_row(m0, n0 + 16 * et, er, c[0], c[NB - 1], pre);
     VAEB_STAMP(a, 3);
     VAEB_STAMP_SYNC(a, 5);   // (timeline build) the epilogue's stores drained

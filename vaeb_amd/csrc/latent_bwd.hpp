@@ -52,47 +52,60 @@ DEV void latent_bwd_elem(const StepArgs& a, bool valid, int m, int j, float mu, 
 
 // One dhd tile (bx = row block of the L * Mbp decoder rows, by = H column tile) + its dZ
 // slab; the last arriver of latent row block bx % (Mbp / 16) finishes the latent backward.
-// red: >= 512 f32x4 of LDS.
+// red: >= 512 f32x4 of LDS (CT = 2, NWV = 16: 2048).
 // HO 2 (deferred, VAEB_BWD_DEFER): the tile stores its slab plainly and ends; the last
 // launch's reducer workgroups sum the slabs (kernels_aux.hpp LatRed).
 // AT (atomic hand-off, latent.hpp fx_*): instead of a dZ slab, the tile adds its partial
 // dZ_l(m, j) into S(m, j) = sum_l dZ_l and dZ_l eps_l(m, j) into E(m, j) = sum_l dZ_l eps_l
-// (acc_dz; L * H/16 contributors each); the add completing S stores dMu(m, j), the one
-// completing E stores dLv(m, j).  dZ itself is not stored on this path.
-template <int NCT, int GCH, bool V, int HO>
+// (acc_dz; L * ceil(H / 16 CT) contributors each); the add completing S stores dMu(m, j), the
+// one completing E stores dLv(m, j).  dZ itself is not stored on this path.
+// CT column tiles per workgroup over NWV waves splitting K (CT = 2, NWV = 16: 1024-thread
+// workgroups, the encoder's enc_latent16 geometry): half the contributors per latent element,
+// so MNIST 784-500-20 (32 H column tiles) comes under the counted atomics' fan-in limit of 16
+// and the latent backward completes inside this launch -- the last launch then starts from a
+// finished [dMu | dLv] instead of reducing slabs and handing them to its tiles in-launch.
+template <bool V>
+struct PDhdCT : PDhdT<V> {
+    DEV f32x4 b4(int n, int k, int w) const { return this->ld(this->bw, this->wplane, n + 16 * w, this->a.H, k); }
+};
+template <int NCT, int GCH, bool V, int HO, int CT = 1, int NWV = 8>
 DEV void dhd_dz_body(const PDhdT<V>& p0, int bx, int by, f32x4* red, int sid) {
+    static_assert(CT == 1 || (HO == 1 && NWV == 16), "two column tiles: the atomic hand-off on 16 waves");
     constexpr bool AT = HO == 1;
-    __shared__ float ts[16][20];
+    constexpr int NTH = 64 * NWV;
+    constexpr int NS = NWV == 16 ? 1 : NCT;   // atomic-add slots per thread: 32 Z <= 1024
+    __shared__ float ts[16][16 * CT + 4];
     __shared__ int sflag;
     __shared__ float pm[AT ? 64 : 1][17];   // AT: [dZ | dZ eps] partials, [column][row]
-    PDhdT<V> p = p0;
+    PDhdCT<V> p{p0};
     p.prepare();
     const StepArgs& a = p.a;
     VAEB_STAMP_AT(a, sid, 0);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int li = lane & 15, q = lane >> 4;
     const int Z = a.Z, H = a.H;
-    const int m0 = bx * 16, n0 = by * 16;
-    const int nrb = a.Mbp >> 4, nctH = (H + 15) >> 4;
+    const int m0 = bx * 16, n0 = by * 16 * CT;
+    const int nrb = a.Mbp >> 4, nctH = (H + 16 * CT - 1) / (16 * CT);
     const int l = bx / nrb, rbl = bx % nrb;
 
-    // Row-parallel epilogue: phase A -- wave r < 4 finishes row group r of the dA1 tile (sum
-    // of the 8 K-slice partials, dtanh, dA1); phase B -- wave ct < NCT forms the tile's partial
-    // dZ for latent tile ct from all of dA1 through LDS (one wave running both phases serially
-    // took ~1.3 us of the launch's critical path).
-    const int er = wave & 3;
+    // Row-parallel epilogue: phase A -- wave w < 4 CT finishes row group r = w & 3 of column
+    // tile w >> 2 (sum of the NWV K-slice partials, dtanh, dA1); phase B -- wave ct < NCT forms
+    // the tile's partial dZ for latent tile ct from all of dA1 through LDS (one wave running
+    // both phases serially took ~1.3 us of the launch's critical path).
+    const int er = wave & 3, ca = wave >> 2;
     float hdv = 0.f;
-    f32x4 w1v{};
+    f32x4 w1v[CT];
     float ev[4];   // HO: eps_l at (row 4q + r, latent j = 16 wave + li)
-    if (wave < 4) {
-        const int n = n0 + li, m = m0 + 4 * q + er;
+    if (wave < 4 * CT) {
+        const int n = n0 + 16 * ca + li, m = m0 + 4 * q + er;
         hdv = bld(mkbuf(a.hd, (int64_t)a.Me * H * 4), (n < H && m < a.Me) ? (uint32_t)(m * H + n) * 4u : kOOB);
     }
     if (wave < NCT) {
-        // W1^T rows n0 .. n0 + 15 at latent j = 16 wave + li: 4 consecutive n per lane
+        // W1^T rows n0 + 16 c .. + 15 at latent j = 16 wave + li: 4 consecutive n per lane
         const rsrc_t bw1 = mkbuf(a.W1, (int64_t)Z * H * 4);
         const bool vh = (H & 3) == 0 && aligned16(a.W1);
-        w1v = kc4(bw1, H, wave * 16 + li, n0 + 4 * q, Z, H, vh);
+#pragma unroll
+        for (int c = 0; c < CT; ++c) w1v[c] = kc4(bw1, H, wave * 16 + li, n0 + 16 * c + 4 * q, Z, H, vh);
         if constexpr (AT) {
             const rsrc_t be = mkbuf(a.eps, (int64_t)a.Me * Z * 4);
 #pragma unroll
@@ -103,40 +116,48 @@ DEV void dhd_dz_body(const PDhdT<V>& p0, int bx, int by, f32x4* red, int sid) {
         }
     }
     // AT: mu, lv of each element this thread may complete (column c: dMu | dLv of latent c % Z)
-    float muv[NCT], lvv[NCT];
+    float muv[NS], lvv[NS];
     if constexpr (AT) {
         const rsrc_t bm = mkbuf(a.mu, (int64_t)a.Mbp * Z * 4), bl = mkbuf(a.lv, (int64_t)a.Mbp * Z * 4);
 #pragma unroll
-        for (int u = 0; u < NCT; ++u) {
-            const int e = (int)threadIdx.x + 512 * u, c = e >> 4, m = rbl * 16 + (e & 15);
+        for (int u = 0; u < NS; ++u) {
+            const int e = (int)threadIdx.x + NTH * u, c = e >> 4, m = rbl * 16 + (e & 15);
             const uint32_t o = e < 32 * Z ? (uint32_t)(m * Z + (c < Z ? c : c - Z)) * 4u : kOOB;
             muv[u] = bld(bm, o);
             lvv[u] = bld(bl, o);
         }
     }
-    f32x4 acc[1] = {zero4()};
-    wave_mainloop<1, 8, GCH>(p, m0 + li, n0 + li, p.K, wave, acc);
+    f32x4 acc[CT];
+#pragma unroll
+    for (int c = 0; c < CT; ++c) acc[c] = zero4();
+    wave_mainloop<CT, NWV, GCH>(p, m0 + li, n0 + li, p.K, wave, acc);
     VAEB_STAMP_AT(a, sid, 1);
-    float* redf = reinterpret_cast<float*>(red);   // [r][slice][lane]
+    float* redf = reinterpret_cast<float*>(red);   // [c][r][slice][lane]
 #pragma unroll
-    for (int r = 0; r < 4; ++r) redf[(r * 8 + wave) * 64 + lane] = acc[0][r];
+    for (int c = 0; c < CT; ++c)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) redf[((c * 4 + r) * NWV + wave) * 64 + lane] = acc[c][r];
     __syncthreads();
-    if (wave < 4) {
-        float t = redf[(er * 8) * 64 + lane];
+    if (wave < 4 * CT) {
+        float t = redf[((ca * 4 + er) * NWV) * 64 + lane];
 #pragma unroll
-        for (int sl = 1; sl < 8; ++sl) t += redf[(er * 8 + sl) * 64 + lane];
-        const int n = n0 + li, m = m0 + 4 * q + er;
+        for (int sl = 1; sl < NWV; ++sl) t += redf[((ca * 4 + er) * NWV + sl) * 64 + lane];
+        const int n = n0 + 16 * ca + li, m = m0 + 4 * q + er;
         const float v = (n < H && (m % a.Mbp) < a.Mb) ? t * (1.f - hdv * hdv) : 0.f;
         if (n < H) a.dA1[(int64_t)m * H + n] = v;
-        ts[4 * q + er][li] = v;
+        ts[4 * q + er][16 * ca + li] = v;
     }
     __syncthreads();
     if (wave < NCT) {
-        // partial dZ of this tile, latent tile ct = wave: (16 x 16 dA1) . (16 rows of W1^T)
-        f32x4 av;
+        // partial dZ of this tile, latent tile ct = wave: (16 x 16 CT dA1) . (16 CT rows of W1^T)
+        f32x4 sv = zero4();
 #pragma unroll
-        for (int s = 0; s < 4; ++s) av[s] = ts[li][4 * q + s];
-        const f32x4 sv = mfma4(av, w1v, zero4());
+        for (int c = 0; c < CT; ++c) {
+            f32x4 av;
+#pragma unroll
+            for (int s = 0; s < 4; ++s) av[s] = ts[li][16 * c + 4 * q + s];
+            sv = mfma4(av, w1v[c], sv);
+        }
         const int j = wave * 16 + li;
         if constexpr (AT) {
             if (j < Z)
@@ -158,11 +179,14 @@ DEV void dhd_dz_body(const PDhdT<V>& p0, int bx, int by, f32x4* red, int sid) {
     if constexpr (AT) {
         // column c < Z: S = sum_l dZ_l of latent c; c >= Z: E = sum_l dZ_l eps_l of latent c - Z
         __syncthreads();
-        FxSlots<NCT> fx;
+        VAEB_STAMP_AT(a, sid, 4);   // (timeline build: the partials are in LDS)
+        FxSlots<NS, NTH> fx;
         fx.add(a.acc_dz, a.acc_ml - 1, rbl * 16, 2 * Z, pm, 32 * Z);   // guard: blk[kBlkFxErr]
+        if (VAEB_DBG_ON(a.dbg)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        VAEB_STAMP_AT(a, sid, 3);   // (timeline build: this thread's adds returned)
         const float sl = a.sc / (float)a.L;
 #pragma unroll
-        for (int u = 0; u < NCT; ++u) {
+        for (int u = 0; u < NS; ++u) {
             float v;
             if (!(fx.ok[u] && fx_done(fx.t[u], nctH * a.L, v))) continue;
             const int c = fx.col[u], m = rbl * 16 + fx.row[u];
@@ -293,6 +317,23 @@ __global__ __launch_bounds__(512) void dhd_dz_wgrad_kernel(PDhdT<VEC> p, WGradAr
     }
     if (VAEB_DBG_ON(w.dbg) && threadIdx.x == 0) w.dbg[bid * 8 + 0] = __builtin_amdgcn_s_memrealtime();
     wgrad_body<VEC, 8, TS>(w, w.g[0], bid, sa, sb);
+}
+
+// The latent backward completed in the dhd launch at MNIST's width (vaeb_hip.hip ho_dz 3):
+// 1024-thread workgroups of two 16-column dA1 tiles each (16 waves splitting K), the counted
+// atomic hand-off at fan-in ceil(H / 32) L <= 16.  No weight-gradient tiles: dW2 (| dW6) is
+// deferred to the next step's encoder launch.  aux: as dhd_dz_wgrad_kernel's.
+template <int NCT, int GCH, bool VEC>
+__global__ __launch_bounds__(1024) void dhd2_dz_kernel(PDhdT<VEC> p, int ntile, int gx, DhdAux aux) {
+    __shared__ f32x4 red[2048];
+    const int b0 = blockIdx.x;
+    if (aux.pend && b0 == 0 && threadIdx.x == 0) *aux.pend = 1;
+    if (aux.zero && b0 * 1024 < aux.nzero) {
+        const int i = b0 * 1024 + (int)threadIdx.x;
+        if (i < aux.nzero) aux.zero[i] = 0ull;
+    }
+    const int bid = xcd_remap(b0, ntile);
+    dhd_dz_body<NCT, GCH, VEC, 1, 2, 16>(p, bid % gx, bid / gx, red, bid);
 }
 
 }  // namespace vaeb

@@ -179,6 +179,14 @@ struct vaeb_ctx {
     // fp32 LB / LA, no communicator, 16-wave encoder, the latent backward deferred too (ho_dz 2:
     // dw2_deferred).  VAEB_DW2_DEFER=0: dW2 in the dhd launch.
     bool dw2_defer = true;
+    // the latent backward completed inside the dhd launch at MNIST's width (ho_dz 3,
+    // latent_bwd.hpp dhd2_dz_kernel): two dA1 column tiles per 1024-thread workgroup halve the
+    // contributors per latent element to ceil(H / 32) L <= 16, so the counted atomics apply and
+    // the last launch needs no reducers, counter or poll.  Measured and not the default
+    // (VAEB_DHD2=1 selects it; round 5, alternating 2000-step runs): 39.41 / 39.35 us per step
+    // against 34.44 / 34.42 -- the dhd launch 5.61 -> 10.87 us (two tiles per CU on 112 CUs,
+    // 72 k returning 64-bit adds), the last launch only 10.62 -> 10.2 us.
+    bool dhd2 = false;
     int* w2pend = nullptr;        // device: 1 = a step's dW2 is pending (set by its dhd launch)
     bool w2_dirty = false;        // host: a step was enqueued since the last flush
     bool w2_graph = false;        // host: the captured graphs hold deferred-dW2 steps (run_steps sets w2_dirty)
@@ -324,9 +332,13 @@ int ho_mode(const vaeb_ctx* c, int fan_in) {
     return fan_in <= kFxMaxFanIn ? 1 : 0;   // the count field holds <= 16 contributors (latent.hpp)
 }
 int ho_ml(const vaeb_ctx* c, int ct) { return ho_mode(c, cdiv(c->c.H, 16 * ct)); }
-// backward: 1 atomic, else 2 (deferred to the last launch's reducers, VAEB_BWD_DEFER) or 0 (ticket)
+bool dw2_deferrable(const vaeb_ctx* c);
+// backward: 1 atomic, 3 atomic on two-column-tile workgroups (where one-tile workgroups would
+// exceed the fan-in limit; vaeb_ctx::dhd2), else 2 (deferred to the last launch's reducers,
+// VAEB_BWD_DEFER) or 0 (ticket)
 int ho_dz(const vaeb_ctx* c) {
     const int m = ho_mode(c, cdiv(c->c.H, 16) * c->c.L);
+    if (m == 0 && c->dhd2 && c->atomic_ho && cdiv(c->c.H, 32) * c->c.L <= kFxMaxFanIn && dw2_deferrable(c)) return 3;
     return m == 0 && c->bwd_defer ? 2 : m;
 }
 
@@ -713,11 +725,17 @@ int w2_args(vaeb_ctx* c, const StepArgs& a, const OptArgs& opt, int base, WGradA
 // dW2 tiles bound the dhd launch.  With the counted atomic backward (small fan-in: Frey) the dhd
 // launch is bound by that hand-off and hides dW2, while the encoder would pay for it: Frey
 // 29.78 / 29.87 µs in-step vs 31.54 / 31.55 deferred.
-bool dw2_deferred(const vaeb_ctx* c, const StepArgs& a) {
+// (ho_dz 3 carries no dW2 tiles of its own: it is chosen only where the deferral applies)
+bool dw2_deferrable(const vaeb_ctx* c) {
     const int est = c->c.estimator;
+    StepArgs a{};
+    a.H = c->c.H;   // (all enc_form reads of the training step's arguments)
     return c->dw2_defer && c->c.dtype == VAEB_DTYPE_F32 && c->comm == nullptr && est != VAEB_EST_FV && est != VAEB_EST_FVS &&
-           fused_latent(c) && c->fold_bwd && ho_dz(c) == 2 && folded_latent(c, a) &&
-           enc_form(c, a, FvFold{}, nullptr, nullptr, nullptr);
+           fused_latent(c) && c->fold_bwd && enc_form(c, a, FvFold{}, nullptr, nullptr, nullptr);
+}
+bool dw2_deferred(const vaeb_ctx* c, const StepArgs& a) {
+    const int hd = ho_dz(c);
+    return dw2_deferrable(c) && (hd == 2 || hd == 3) && folded_latent(c, a);
 }
 
 // Run the pending step's dW2 (| dW6) + Adagrad now (their own launch; the device flag makes it
@@ -1028,7 +1046,20 @@ int enqueue_train_step(vaeb_ctx* c, int par, bool prof, bool fresh = true, int d
         const dim3 grid(w.total_wgs);
         const bool deep = cdiv(cdiv(p5.K, 16), 8) > 4;
         pr.mark(w2d ? 43 : 39);
-        REP(pr) {
+        if (ho_dz(c) == 3) {
+            // two column tiles per 1024-thread workgroup, the counted atomic latent backward
+            if (!w2d) return fail(VAEB_ERR_ARG, "internal: the two-tile dhd launch needs the deferred dW2");
+            const int nt2 = gx * cdiv(p5.N, 32);
+            REP(pr) {
+                if (a.Z <= 16) {
+                    if (vec) hipLaunchKernelGGL((dhd2_dz_kernel<1, 4, true>), dim3(nt2), dim3(1024), 0, s, p5, nt2, gx, pend);
+                    else hipLaunchKernelGGL((dhd2_dz_kernel<1, 4, false>), dim3(nt2), dim3(1024), 0, s, p5s, nt2, gx, pend);
+                } else {
+                    if (vec) hipLaunchKernelGGL((dhd2_dz_kernel<2, 4, true>), dim3(nt2), dim3(1024), 0, s, p5, nt2, gx, pend);
+                    else hipLaunchKernelGGL((dhd2_dz_kernel<2, 4, false>), dim3(nt2), dim3(1024), 0, s, p5s, nt2, gx, pend);
+                }
+            }
+        } else REP(pr) {
             switch (ho_dz(c)) {
                 case 1: launch_dhd_dz<kWTJ_P5 / 16, 1>(s, grid, p5, p5s, w, ntile, gx, vec, deep, pend); break;
                 case 2: launch_dhd_dz<kWTJ_P5 / 16, 2>(s, grid, p5, p5s, w, ntile, gx, vec, deep, pend); break;
@@ -1314,6 +1345,7 @@ int vaeb_create(const vaeb_config* cfg, vaeb_ctx** out) {
     if (const char* bd = getenv("VAEB_BWD_DEFER")) c->bwd_defer = atoi(bd) != 0;
     if (const char* ef = getenv("VAEB_ENC_FX")) c->enc_fx = atoi(ef) != 0;
     if (const char* wd = getenv("VAEB_DW2_DEFER")) c->dw2_defer = atoi(wd) != 0;
+    if (const char* d2 = getenv("VAEB_DHD2")) c->dhd2 = atoi(d2) != 0;
     if (const char* bk = getenv("VAEB_BF_FORK")) c->bf_fork = atoi(bk) != 0;
     if (const char* b2 = getenv("VAEB_BF_SPLIT2")) c->bf_split2 = atoi(b2) != 0;
     if (const char* bt = getenv("VAEB_BF_THIN")) c->bf_thin = atoi(bt) & 3;
@@ -2097,7 +2129,7 @@ int vaeb_get_activation(vaeb_ctx* c, const char* name, float* out, int64_t n) {
     if (!c || !name || !out) return fail(VAEB_ERR_ARG, "null argument");
     float* ptrs[] = {c->h, c->mu, c->lv, c->eps, c->z, c->hd, c->dA2, c->dA6, c->dA1, c->dZ, c->dMuLv, c->dA3, c->y,
                      c->kl_part, c->lp_part};
-    if (strcmp(name, "dZ") == 0 && fused_latent(c) && c->fold_bwd && !is_bf16(c) && ho_dz(c) == 1)
+    if (strcmp(name, "dZ") == 0 && fused_latent(c) && c->fold_bwd && !is_bf16(c) && (ho_dz(c) == 1 || ho_dz(c) == 3))
         return fail(VAEB_ERR_STATE, "dZ is not stored by the atomic latent hand-off (fan-in <= 16, latent_bwd.hpp): "
                                     "create the context with VAEB_ATOMIC_HO=0 to read it");
     const int64_t R = c->cap, RL = (int64_t)c->cap * c->c.L, D = c->c.D, H = c->c.H, Z = c->c.Z;
