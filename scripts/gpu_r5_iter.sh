@@ -10,7 +10,7 @@ timeout -k 10 600 python -u -m pytest ${TESTS:-tests/test_gpu_step.py} -m gpu -x
 tail -2 $O/tests.log
 [ $rc -ne 0 ] && { grep -E "FAILED|Error|assert" $O/tests.log | head -30; exit 1; }
 for rep in 1 2; do
-  for v in 1 0; do
+  for v in ${AB_VALS:-1 0}; do
     env $AB=$v timeout -k 10 200 python3 bench.py --steps 2000 --warmup 200 --no-cpu-baseline > $O/b_${v}_$rep.json 2> $O/err.txt || { tail $O/err.txt; exit 1; }
     env $AB=$v timeout -k 10 200 python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline > $O/d_${v}_$rep.json 2> $O/err.txt || { tail $O/err.txt; exit 1; }
   done

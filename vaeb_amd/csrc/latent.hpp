@@ -602,7 +602,11 @@ DEV void decout_z_body(const StepArgs& a) {
     const int li = lane & 15, q = lane >> 4;
     const int gx = a.Me >> 4, gy = (a.D + CW - 1) / CW;   // the grid (no implicit-argument load)
     const int lin = xcd_remap(blockIdx.x + blockIdx.y * gx, gx * gy);
+#ifdef VAEB_DEC_ROWMAJOR   // A/B build: an XCD's workgroups share row blocks (slabs, x rows) instead of W2 columns
+    const int bxr = lin / gy, byr = lin % gy;
+#else
     const int bxr = lin % gx, byr = lin / gx;
+#endif
     const int m0 = bxr * 16, n0 = byr * CW;
     const int Z = a.Z, H = a.H;
     const bool col0 = byr == 0;
