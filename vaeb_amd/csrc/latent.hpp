@@ -558,12 +558,18 @@ __global__ __launch_bounds__(1024) void enc_latent16_w2_kernel(StepArgs a, WGrad
     __shared__ __attribute__((aligned(16))) float lds[4 * kWKB * kWP];
     static_assert(sizeof(float) * 4 * kWKB * kWP >= sizeof(f32x4) * 64 * 16 * CT, "LDS union");
     if ((int)blockIdx.y >= rows_enc) {
+#ifdef VAEB_KO_ENC_NOW2   // timing-only knock-out build (wrong results): no deferred dW2 workers
+        return;
+#endif
         const int half = (int)threadIdx.x >> 9;
         const int bid = 2 * (((int)blockIdx.y - rows_enc) * (a.Mbp >> 4) + (int)blockIdx.x) + half;
         float (*sa)[kWP] = reinterpret_cast<float(*)[kWP]>(lds + half * 2 * kWKB * kWP);
         wgrad_body<VEC, 8, TS>(w, w.g[0], bid, sa, sa + kWKB, pend);
         return;
     }
+#ifdef VAEB_KO_ENC_NOENC   // timing-only knock-out build: the dW2 workers alone in the launch
+    return;
+#endif
     enc_latent_body<NCT, GCH, false, HO, CT, 16, true>(a, FvFold{}, reinterpret_cast<f32x4*>(lds));
 }
 
@@ -602,11 +608,18 @@ DEV void decout_z_body(const StepArgs& a) {
     const int li = lane & 15, q = lane >> 4;
     const int gx = a.Me >> 4, gy = (a.D + CW - 1) / CW;   // the grid (no implicit-argument load)
     const int lin = xcd_remap(blockIdx.x + blockIdx.y * gx, gx * gy);
-#ifdef VAEB_DEC_ROWMAJOR   // A/B build: an XCD's workgroups share row blocks (slabs, x rows) instead of W2 columns
-    const int bxr = lin / gy, byr = lin % gy;
+    // CT = 2 (the Bernoulli two-tile decoder): consecutive logical ids (one XCD's run under
+    // xcd_remap) share a row block, so each XCD's L2 fetches the encoder slabs and x rows of ~1 row
+    // block instead of all 7 (the W2 column panels then spread over the XCDs): round 5, alternating
+    // 2000-step runs, MNIST 34.30 / 34.32 / 34.34 us against 34.46 / 34.46 column-major
+    // (-DVAEB_DEC_COLMAJOR).  CT = 1 (Gaussian, Frey) keeps the column-major order: 30.15 / 30.23
+    // row-major against 29.77 / 29.83 us.
+#ifdef VAEB_DEC_COLMAJOR
+    constexpr bool kRowMajor = false;
 #else
-    const int bxr = lin % gx, byr = lin / gx;
+    constexpr bool kRowMajor = CT == 2;
 #endif
+    const int bxr = kRowMajor ? lin / gy : lin % gx, byr = kRowMajor ? lin % gy : lin / gx;
     const int m0 = bxr * 16, n0 = byr * CW;
     const int Z = a.Z, H = a.H;
     const bool col0 = byr == 0;
