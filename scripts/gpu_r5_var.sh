@@ -7,7 +7,7 @@ O=gpurun_out/r5var
 mkdir -p $O
 i=0
 for r in $RUNS; do
-  v=${r%%:*}; e=${r#*:}; [ "$e" = "$r" ] && e=""
+  v=${r%%:*}; e=${r#*:}; [ "$e" = "$r" ] && e=""; e=${e//,/ }
   if [ $v = default ]; then L=""; else L=$v; fi
   i=$((i+1))
   env VAEB_LIB_VARIANT=$L $e timeout -k 10 200 python3 bench.py --steps ${STEPS:-2000} --warmup ${WARM:-200} --no-cpu-baseline $BARGS > $O/b_$i.json 2> $O/err.txt || { tail $O/err.txt; exit 1; }

@@ -321,15 +321,22 @@ def test_bf16_dp_path_world1_matches_fused_optimizer(overlap, fork, shard, monke
     assert rel(outs[1][2], outs[0][2]) <= 1e-4
 
 
-def test_bf16_forked_and_single_stream_steps_agree(monkeypatch):
+@pytest.mark.parametrize("forkpt,w2a,gauss", [("1", "0", False), ("2", "0", False), ("3", "0", False), ("1", "1", False),
+                                              ("2", "1", False), ("1", "1", True)])
+def test_bf16_forked_and_single_stream_steps_agree(monkeypatch, forkpt, w2a, gauss):
     """the forked bf16 step (dW1, dW2 | dW6 and dW4 | dW5 on a second stream
     beside the dz -> [dMu | dLv] -> dh -> dW3 chain, joined by events inside the graph) and
     the single-stream step (VAEB_BF_FORK=0: dhd and dW2 in one grid) compute the same
     products with the same K order, so 10 Philox steps agree to 1e-6 in every parameter and
     the ELBO -- this pins the cross-stream ordering independently of the golden tolerances;
-    graph replay and eager launches agree bitwise for each form."""
+    graph replay and eager launches agree bitwise for each form.  For every fork point
+    (VAEB_BF_FORKPT: after dhd, after dz + [dMu | dLv], after dh), and with dW2's second
+    column tile in dW3's grid (VAEB_BF_W2A=1 of D / 256 = 2; Gaussian: of 2D / 256 = 4, the
+    [W2 | W6] interleave)."""
+    monkeypatch.setenv("VAEB_BF_FORKPT", forkpt)
+    monkeypatch.setenv("VAEB_BF_W2A", w2a)
     from vaeb_amd import _lib
-    cfg = O.Config(D=512, H=256, Z=32)
+    cfg = O.Config(D=512, H=256, Z=32, continuous=gauss)
     B = 512
     x = (np.random.default_rng(4).random((6 * B, cfg.D)) < 0.4).astype(np.float32)
     order = np.array([3, 1, 4, 1, 5, 0, 2, 5, 3, 4], np.int32)
@@ -337,7 +344,8 @@ def test_bf16_forked_and_single_stream_steps_agree(monkeypatch):
     for fork in ("1", "0"):
         for use_graph in (True, False):
             monkeypatch.setenv("VAEB_BF_FORK", fork)
-            ctx = _lib.Context(cfg.D, cfg.H, cfg.Z, B, max_eval_rows=B, dtype=_lib.DTYPE_BF16, use_graph=use_graph)
+            ctx = _lib.Context(cfg.D, cfg.H, cfg.Z, B, decoder=int(gauss), max_eval_rows=B, dtype=_lib.DTYPE_BF16,
+                               use_graph=use_graph)
             ctx.set_data(x)
             ctx.set_params(O.flatten(O.init_params(cfg)))
             ctx.set_eps_mode(_lib.EPS_PHILOX, 10)
@@ -354,6 +362,47 @@ def test_bf16_forked_and_single_stream_steps_agree(monkeypatch):
         f = out[fork, True]
         assert abs(f[0] - u[0]) <= 1e-6 * abs(u[0])
         assert np.abs(f[1] - u[1]).max() <= 1e-6 and np.abs(f[2] - u[2]).max() <= 1e-6 * max(1.0, np.abs(u[2]).max())
+
+
+@pytest.mark.parametrize("var,alt,base,tol", [("VAEB_BF_SMALLK", "3", "0", 1e-6), ("VAEB_BF_DECT", "0", "1", 1e-5)])
+def test_bf16_tile_form_switches_agree(monkeypatch, var, alt, base, tol):
+    """Two tile forms of the same products, 6 Philox steps each, graph replay and eager
+    launches bitwise equal for each form:
+      * VAEB_BF_SMALLK=3: dechid (K = Z) and dh (K = 2Z) on 256 x 128 tiles with two blocks
+        per CU against the 256 x 256 8-phase tiles -- each output element sees the same MFMA
+        sequence over k: parameters and ELBO to 1e-6;
+      * VAEB_BF_DECT=0: the Bernoulli decoder on hd W2 (EpiDecOut) against the transposed
+        product W2^T hd^T (EpiDecOutT, the default) -- the same dot products, but the per-row
+        log p and the bias column sums are added in another order: ELBO to 1e-5 relative,
+        parameters to a few Adagrad steps."""
+    from vaeb_amd import _lib
+    cfg = O.Config(D=512, H=264, Z=40)
+    B = 520
+    x = (np.random.default_rng(6).random((4 * B, cfg.D)) < 0.4).astype(np.float32)
+    order = np.array([1, 3, 0, 2, 3, 1], np.int32)
+    out = {}
+    for v in (alt, base):
+        for use_graph in (True, False):
+            monkeypatch.setenv(var, v)
+            ctx = _lib.Context(cfg.D, cfg.H, cfg.Z, B, max_eval_rows=B, dtype=_lib.DTYPE_BF16, use_graph=use_graph)
+            ctx.set_data(x)
+            ctx.set_params(O.flatten(O.init_params(cfg)))
+            ctx.set_eps_mode(_lib.EPS_PHILOX, 10)
+            ctx.set_step(0)
+            ctx.update_many(order)
+            s_, n_ = ctx.epoch_elbo()
+            out[v, use_graph] = (s_ / n_, ctx.get_params(), ctx.get_adagrad_state())
+            ctx.close()
+    monkeypatch.setenv(var, base)
+    for v in (alt, base):
+        a, b = out[v, True], out[v, False]
+        assert a[0] == b[0] and np.array_equal(a[1], b[1]) and np.array_equal(a[2], b[2])
+    f, u = out[alt, True], out[base, True]
+    assert abs(f[0] - u[0]) <= tol * abs(u[0]), (f[0], u[0])
+    if tol <= 1e-6:
+        assert np.abs(f[1] - u[1]).max() <= 1e-6 and np.abs(f[2] - u[2]).max() <= 1e-6 * max(1.0, np.abs(u[2]).max())
+    else:
+        assert np.abs(f[1] - u[1]).max() <= 2 * len(order) * cfg.lr
 
 
 def test_bf16_thin_and_split_k_latent_agree(monkeypatch):

@@ -71,11 +71,13 @@ struct Shape {
     static constexpr int kBlocksPerCU = ST == 3 ? 2 : 1;
 };
 
-// f32 -> bf16, round to nearest even (inputs here are finite)
-DEV uint32_t f2bf(float f) {
-    const uint32_t u = __builtin_bit_cast(uint32_t, f);
-    return (u + 0x7FFFu + ((u >> 16) & 1u)) >> 16;
-}
+// f32 -> bf16, round to nearest even: gfx950's v_cvt_pk_bf16_f32 (one instruction; the
+// integer form (u + 0x7FFF + ((u >> 16) & 1)) >> 16 gives the same bits for finite inputs in
+// four).  f2bf2: two values in one instruction, a in the low half.
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
+DEV uint32_t f2bf(float f) { return __builtin_bit_cast(uint16_t, (__bf16)f); }
+DEV uint32_t f2bf2(float a, float b) { return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2_t){a, b}, bf16x2_t)); }
 DEV float bf2f(uint32_t b) { return __builtin_bit_cast(float, b << 16); }
 
 // KC images have 64-B rows (BK = 32): chunk c (0..3) of row r lives at c ^ g[(r >> 2) & 3],
@@ -342,6 +344,14 @@ DEV void gemm_body(const GemmArgs& g, const Epi& e, int bid, int kz, char* smem)
 template <int LA, int LB, int BNT, class Epi, int ST = 4>
 __global__ __launch_bounds__(NTHR, (2 * Shape<BNT, ST>::kBlocksPerCU)) void gemm_kernel(GemmArgs g, Epi e) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
+#ifdef VAEB_DECO_STAGGER   // (A/B build: the second block slot of every CU starts later)
+    if constexpr (ST == 3) {
+        if (blockIdx.x >= 256 && blockIdx.x < 512) {
+            const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+            while (__builtin_amdgcn_s_memrealtime() - t0 < (uint64_t)(VAEB_DECO_STAGGER * 100)) __builtin_amdgcn_s_sleep(8);
+        }
+    }
+#endif
     gemm_body<LA, LB, BNT, Epi, ST>(g, e, blockIdx.x, blockIdx.y, smem);
 }
 
@@ -498,6 +508,9 @@ struct EpiBiasAct {
 #ifndef VAEB_DBG_NO_TANH   // (timing-only build: the epilogue without its activation)
                     if (tanh_act) v = ftanh_bf(v);
 #endif
+#ifdef VAEB_KO_BA_NOLDS   // (timing-only build: no per-element LDS writes)
+                    if (v == 12345.f)
+#endif
                     lds_st_bf<W>(smem, erow(lr0, i, r, lane), ecol<CM>(lc0, j, lane), v);
                 }
         }
@@ -532,9 +545,15 @@ struct EpiDTanh {
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     const int lr = erow(lr0, i, r, lane), lc = ecol<CM>(lc0, j, lane);
+#ifdef VAEB_KO_DT_NOLDS   // (timing-only build: no per-element LDS reads / writes)
+                    const float tv = 0.5f * (float)(lr & 1);
+                    const float v = acc[i][j][r] * (1.f - tv * tv);
+                    if (v == 12345.f) lds_st_bf<W>(smem, lr, lc, v);
+#else
                     const float tv = lds_bf<W>(smem, lr, lc);
                     const float v = acc[i][j][r] * (1.f - tv * tv);
                     lds_st_bf<W>(smem, lr, lc, v);
+#endif
                     cs += (erow(mw, i, r, lane) < M) ? v : 0.f;
                 }
             cs = colsum_lanes(cs);
@@ -570,6 +589,9 @@ struct EpiDecOut {
     float* yout;
     template <int W>
     DEV void load_in(int m0, int n0, char* smem) const {
+#ifdef VAEB_KO_DECO_NOX   // (timing-only build: the x tile is not fetched)
+        return;
+#endif
         const rsrc_t src = mkbuf(x + xb.offset(), (int64_t)Mx * ldx * 2);
         if constexpr (GAUSS) tile_load<W / 2, W, true>(smem, src, ldx, m0, n0 / 2, M, D, Mx);
         else tile_load<W, W>(smem, src, ldx, m0, n0, M, D, Mx);
@@ -605,9 +627,18 @@ struct EpiDecOut {
                 for (int r = 0; r < 4; ++r) {
                     const int row = erow(mw, i, r, lane), lr = erow(lr0, i, r, lane);
                     const bool ok = cok[j] && row < M;
+#ifdef VAEB_KO_DECO_NOLDS   // (timing-only build: no per-element LDS x reads / dA writes)
+                    const float xv = (float)(lr & 1);
+#else
                     const float xv = lds_bf<W>(smem, lr, ecol<CM>(lc0, j, lane));
+#endif
                     const float a2 = acc[i][j][r] + bb2[j];
                     float y, lpv, g2, g6 = 0.f;
+#ifdef VAEB_KO_DECO_NOMATH   // (timing-only build: the likelihood arithmetic replaced by copies)
+                    if constexpr (true) {
+                        y = a2; lpv = xv; g2 = a2 + xv;
+                    } else
+#endif
                     if constexpr (!GAUSS) {
                         // log p = x a - softplus(a) = x a - max(a, 0) - log(1 + e^-|a|): the
                         // logs of a row's JN elements are taken once, of their product (<= 2^JN)
@@ -628,7 +659,9 @@ struct EpiDecOut {
                     rs[r] += ok ? lpv : 0.f;
                     if (yout && ok) yout[(int64_t)row * D + d[j]] = y;
                     if (train) {
+#ifndef VAEB_KO_DECO_NOLDS
                         lds_st_bf<W>(smem, lr, ecol<CM>(lc0, j, lane), g2);
+#endif
                         cs2[j] += ok ? g2 : 0.f;
                         if constexpr (GAUSS) {
                             lds_st_bf<W>(smem, lr, ecol<CM>(lc0, j, lane) + 32, g6);
@@ -660,7 +693,122 @@ struct EpiDecOut {
     }
     template <int W>
     DEV void store_out(int m0, int n0, char* smem) const {
+#ifndef VAEB_KO_DECO_NOST   // (timing-only build: dA not stored)
         if (train) tile_store<W>(smem, dA, ldd, m0, n0, M, N);
+#endif
+    }
+};
+
+// Bernoulli decoder output (VAEB.py:257-263, 302-313) on the TRANSPOSED product
+// a2^T = W2^T hd^T (gemm_body with A' = W2 K-outer, B' = hd K-contiguous; a block tile is 256
+// output columns x W output rows).  A lane's accumulator registers r = 0..3 of fragment (i, j)
+// are then four CONSECUTIVE output columns mw + 16 i + 4 q + r of ONE output row nw + 16 j +
+// (l & 15), so the x reads and dA writes through the LDS tile are one 8-byte access per four
+// elements (EpiDecOut: a 2-byte access per element -- 15 us of config 5's decoder in a
+// timing-only build without them), the bias is one 16-byte load, y one 16-byte store, and a
+// row's log p terms stay in the lane (16 elements per wave block, one log of their product).
+// Same outputs: lp[row * nlp + col / 64], colpart[row / 64][col], dA (bf16), y.
+struct EpiDecOutT {
+    static constexpr bool kIn = true, kOut = true;
+    const float* b2;
+    const bf16_t* x; int ldx; int Mx;   // data row of output row m is m % Mx
+    int M, D;                           // output rows, output columns (D % 8 == 0)
+    int train;
+    float sl;                           // sc / L
+    BatchRef xb;
+    bf16_t* dA; int ldd;
+    float* lp; int nlp;
+    float* colpart;
+    float* yout;                        // 16-byte aligned or null
+    // LDS tile [W rows][256 columns] bf16, pitch 528 B = 132 dwords = 4 (mod 64): the 8-byte
+    // accesses of a 32-lane group (16 rows x 2 column quads) hit 64 distinct banks
+    static constexpr int kPitch = 528;
+    template <int W>
+    DEV void load_in(int m0, int n0, char* smem) const {
+        const rsrc_t src = mkbuf(x + xb.offset(), (int64_t)Mx * ldx * 2);
+        constexpr int CPR = BM / 8, N = W * CPR / NTHR;
+#pragma unroll
+        for (int i = 0; i < N; ++i) {
+            const int id = threadIdx.x + NTHR * i;
+            const int row = id / CPR, ch = id % CPR;
+            const int gr = n0 + row, gc = m0 + ch * 8;
+            const uint32_t off = (gr < M && gc < D) ? ((uint32_t)(gr % Mx) * (uint32_t)ldx + (uint32_t)gc) * 2u : kOOB;
+            *reinterpret_cast<v4u*>(smem + row * kPitch + ch * 16) =
+                __builtin_bit_cast(v4u, __builtin_amdgcn_raw_buffer_load_b128(src, off, 0, 0));
+        }
+    }
+    template <int W, class CM = ColStd>
+    DEV void apply(int mw, int nw, f32x4 (&acc)[4][4], int, char* smem) const {
+        const int lane = threadIdx.x & 63, q = lane >> 4, li = lane & 15;
+        const int lc0 = mw & (BM - 1), lr0 = nw & (W - 1);
+        const rsrc_t bb = mkbuf(b2, (int64_t)D * 4);
+        const rsrc_t yb = mkbuf(yout, yout ? (int64_t)M * D * 4 : 0);
+        // output row tiles j outermost: the row's log p terms are two running values, the
+        // column sums 16 (4 column quads x 4) carried over the row tiles
+        f32x4 cs[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) cs[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int row = nw + 16 * j + li;
+            const bool rok = row < M;
+            float rs = 0.f, pd = 1.f;   // pd: prod (1 + e^-|a|) of the row's <= 16 elements (< 2^16)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int col = mw + 16 * i + 4 * q;
+                const bool ok = rok && col < D;
+                const f32x4 bias = bld4(bb, col < D ? (uint32_t)col * 4u : kOOB);
+                char* px = smem + (lr0 + 16 * j + li) * kPitch + (lc0 + 16 * i + 4 * q) * 2;
+                const uint2 xr = *reinterpret_cast<const uint2*>(px);
+                float gv[4];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const uint32_t xw = r < 2 ? xr.x : xr.y;
+                    const float xv = bf2f((r & 1) ? xw >> 16 : xw & 0xFFFFu);
+                    const float a = acc[i][j][r] + bias[r];
+                    const float t = fexp(-fabsf(a));
+                    const float dd = 1.f + t, rc = frcp(dd);
+                    const float y = a >= 0.f ? rc : t * rc;
+                    rs += ok ? xv * a - fmaxf(a, 0.f) : 0.f;
+                    pd *= ok ? dd : 1.f;
+                    const float g = sl * (xv - y);
+                    cs[i][r] += ok ? g : 0.f;
+                    if (yout && ok) bst(yb, (uint32_t)(row * D + col + r) * 4u, y);
+                    gv[r] = g;
+                }
+                if (train) *reinterpret_cast<uint2*>(px) = make_uint2(f2bf2(gv[0], gv[1]), f2bf2(gv[2], gv[3]));
+            }
+            float v = rs - flog(pd);
+            v += __shfl_xor(v, 16, 64);
+            v += __shfl_xor(v, 32, 64);
+            if (q == 0 && rok && mw < D) lp[(int64_t)row * nlp + (mw >> 6)] = v;
+        }
+        if (train) {
+            // the column sums of this wave block's 64 rows: 4 row tiles in the lane, then the 16
+            // lanes of the column quad
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int col = mw + 16 * i + 4 * q;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const float v = sum16(cs[i][r]);
+                    if (li == 0 && col < D) colpart[(int64_t)(nw >> 6) * D + col + r] = v;
+                }
+            }
+        }
+    }
+    template <int W>
+    DEV void store_out(int m0, int n0, char* smem) const {
+        if (!train) return;
+        constexpr int CPR = BM / 8, N = W * CPR / NTHR;
+#pragma unroll
+        for (int i = 0; i < N; ++i) {
+            const int id = threadIdx.x + NTHR * i;
+            const int row = id / CPR, ch = id % CPR;
+            const int gr = n0 + row, gc = m0 + ch * 8;
+            if (gr < M && gc < D)
+                *reinterpret_cast<v4u*>(dA + (int64_t)gr * ldd + gc) = *reinterpret_cast<const v4u*>(smem + row * kPitch + ch * 16);
+        }
     }
 };
 
@@ -704,6 +852,7 @@ struct Opt {
 struct EpiAdagrad {
     static constexpr bool kIn = false, kOut = false;
     ColMap map; Opt opt; int M, N;
+    int sld;   // row stride of the bf16 shadow (0: N; a column range of a wider weight: its width)
     // The optimizer rule of Opt::apply on the wave's 64 x 64 block, one 16-row fragment
     // row (16 elements per lane) per memory round trip: all theta / accumulator loads of
     // the fragment row are issued before its stores (buffer loads, masked elements read
@@ -741,7 +890,7 @@ struct EpiAdagrad {
                                          opt.decay * th[j][r] * th[j][r];
                         bst(bac, off[j][r], a);
                         bst(bto, off[j][r], tn);
-                        if (off[j][r] != kOOB) opt.shadow_out[(int64_t)row * N + col] = (bf16_t)f2bf(tn);
+                        if (off[j][r] != kOOB) opt.shadow_out[(int64_t)row * (sld ? sld : N) + col] = (bf16_t)f2bf(tn);
                     }
                 }
         }

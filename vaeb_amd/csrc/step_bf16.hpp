@@ -251,7 +251,7 @@ __global__ __launch_bounds__(256) void latent_bwd_kernel(LatentArgs a) {
 // latent_bwd_v4 owns BOTH outputs of a latent index (dMu at column j, dLv at Z + j), so
 // each dZ slab element is read once instead of twice.  Same arithmetic, same slab order.
 DEV void st_bf16x4(bf16_t* p, f32x4 v) {
-    const uint32_t lo = f2bf(v[0]) | (f2bf(v[1]) << 16), hi = f2bf(v[2]) | (f2bf(v[3]) << 16);
+    const uint32_t lo = f2bf2(v[0], v[1]), hi = f2bf2(v[2], v[3]);
     *reinterpret_cast<uint2*>(p) = make_uint2(lo, hi);
 }
 

@@ -158,6 +158,10 @@ struct vaeb_ctx {
     int bf_thin = 3;              // VAEB_BF_THIN mask: 1 heads, 2 dz on thin_bf16.hpp (0: split-K + latent kernels)
     bool bf_fork = true;          // VAEB_BF_FORK=0: dW2 in the dhd grid (bf_fuse) or after it
     bool bf_split2 = false;       // VAEB_BF_SPLIT2: the forked dW2 / dW3 as two K slices (bf_wgrad256)
+    int bf_smallk = 0;            // VAEB_BF_SMALLK mask: 1 dechid, 2 dh on 256 x 128 tiles, two blocks per CU
+    int bf_forkpt = 1;            // VAEB_BF_FORKPT: where the bf16 step forks its second stream (1, 2, 3)
+    int bf_dect = 1;              // VAEB_BF_DECT=0: the Bernoulli decoder on hd W2 (EpiDecOut) instead of its transpose
+    int bf_w2a = 0;               // VAEB_BF_W2A: 256-column tiles of dW2 forked after dhd (0: all), the rest in dW3's grid
     hipStream_t s2 = nullptr;     // DP: the gradient buckets' all-reduces and their Adagrad
     hipEvent_t dp_ev[3] = {};     // fork after dW2, bucket A reduced, bucket A updated
     bool dp_overlap = false;      // bucket A on s2 (bf16 engine; VAEB_DP_OVERLAP=0/1 overrides)
@@ -1348,6 +1352,10 @@ int vaeb_create(const vaeb_config* cfg, vaeb_ctx** out) {
     if (const char* d2 = getenv("VAEB_DHD2")) c->dhd2 = atoi(d2) != 0;
     if (const char* bk = getenv("VAEB_BF_FORK")) c->bf_fork = atoi(bk) != 0;
     if (const char* b2 = getenv("VAEB_BF_SPLIT2")) c->bf_split2 = atoi(b2) != 0;
+    if (const char* sk = getenv("VAEB_BF_SMALLK")) c->bf_smallk = atoi(sk) & 3;
+    if (const char* dt = getenv("VAEB_BF_DECT")) c->bf_dect = atoi(dt) != 0;
+    if (const char* wa = getenv("VAEB_BF_W2A")) c->bf_w2a = std::max(0, atoi(wa));
+    if (const char* fp = getenv("VAEB_BF_FORKPT")) c->bf_forkpt = std::min(3, std::max(1, atoi(fp)));
     if (const char* bt = getenv("VAEB_BF_THIN")) c->bf_thin = atoi(bt) & 3;
     if (const char* ah = getenv("VAEB_ATOMIC_HO")) c->atomic_ho = atoi(ah) != 0 ? 1 : 0;
     if (const char* er = getenv("VAEB_ENC_RED")) c->enc_red = atoi(er) != 0 ? 1 : 0;
