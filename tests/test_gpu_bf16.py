@@ -335,6 +335,10 @@ def test_bf16_forked_and_single_stream_steps_agree(monkeypatch, forkpt, w2a, gau
     [W2 | W6] interleave)."""
     monkeypatch.setenv("VAEB_BF_FORKPT", forkpt)
     monkeypatch.setenv("VAEB_BF_W2A", w2a)
+    # the forked dhd on the transposed product (VAEB_BF_DTT=1, the default) adds its bias column
+    # sums in another order than the single-stream grid: compared with DTT=0 here, and DTT=1
+    # against DTT=0 in test_bf16_tile_form_switches_agree
+    monkeypatch.setenv("VAEB_BF_DTT", "0")
     from vaeb_amd import _lib
     cfg = O.Config(D=512, H=256, Z=32, continuous=gauss)
     B = 512
@@ -364,7 +368,8 @@ def test_bf16_forked_and_single_stream_steps_agree(monkeypatch, forkpt, w2a, gau
         assert np.abs(f[1] - u[1]).max() <= 1e-6 and np.abs(f[2] - u[2]).max() <= 1e-6 * max(1.0, np.abs(u[2]).max())
 
 
-@pytest.mark.parametrize("var,alt,base,tol", [("VAEB_BF_SMALLK", "3", "0", 1e-6), ("VAEB_BF_DECT", "0", "1", 1e-5)])
+@pytest.mark.parametrize("var,alt,base,tol", [("VAEB_BF_SMALLK", "3", "0", 1e-6), ("VAEB_BF_DECT", "0", "1", 1e-5),
+                                              ("VAEB_BF_DTT", "0", "1", 1e-5)])
 def test_bf16_tile_form_switches_agree(monkeypatch, var, alt, base, tol):
     """Two tile forms of the same products, 6 Philox steps each, graph replay and eager
     launches bitwise equal for each form:
@@ -374,7 +379,9 @@ def test_bf16_tile_form_switches_agree(monkeypatch, var, alt, base, tol):
       * VAEB_BF_DECT=0: the Bernoulli decoder on hd W2 (EpiDecOut) against the transposed
         product W2^T hd^T (EpiDecOutT, the default) -- the same dot products, but the per-row
         log p and the bias column sums are added in another order: ELBO to 1e-5 relative,
-        parameters to a few Adagrad steps."""
+        parameters to a few Adagrad steps;
+      * VAEB_BF_DTT=0: dhd and dh on A W (EpiDTanh) against the transposed products
+        (EpiDTanhT, the default) -- their bias column sums in another order: the same bounds."""
     from vaeb_amd import _lib
     cfg = O.Config(D=512, H=264, Z=40)
     B = 520

@@ -564,6 +564,83 @@ struct EpiDTanh {
     DEV void store_out(int m0, int n0, char* smem) const { tile_store<W>(smem, out, ldo, m0, n0, M, N); }
 };
 
+// EpiDTanh on the TRANSPOSED product out^T (A' = the weight, B' = the data gradient; the
+// block tile is 256 output columns x W output rows): a lane's registers r = 0..3 of fragment
+// (i, j) are four consecutive output columns mw + 16 i + 4 q + r of output row nw + CM::off(j)
+// + (l & 15), so t is read and out written through the LDS tile with one 8-byte access per
+// four elements instead of a 2-byte access per element.  Column sums of out (fp32, before
+// rounding) per wave block -> colpart[CM::slot(nw)][col] (the 64 output rows of the wave:
+// contiguous with ColStd, two 32-row pieces with Col8; CM::slot numbers them 0.. per 256 rows).
+struct EpiDTanhT {
+    static constexpr bool kIn = true, kOut = true;
+    const bf16_t* t; int ldt; int M, N;   // output rows, output columns (N % 8 == 0)
+    bf16_t* out; int ldo;
+    float* colpart;
+    static constexpr int kPitch = 528;    // 256 bf16 + 16 B: 132 dwords = 4 (mod 64)
+    template <int W>
+    DEV void load_in(int m0, int n0, char* smem) const {
+        const rsrc_t src = mkbuf(t, (int64_t)M * ldt * 2);
+        constexpr int CPR = BM / 8, NL = W * CPR / NTHR;
+#pragma unroll
+        for (int i = 0; i < NL; ++i) {
+            const int id = threadIdx.x + NTHR * i;
+            const int row = id / CPR, ch = id % CPR;
+            const int gr = n0 + row, gc = m0 + ch * 8;
+            const uint32_t off = (gr < M && gc < N) ? ((uint32_t)gr * (uint32_t)ldt + (uint32_t)gc) * 2u : kOOB;
+            *reinterpret_cast<v4u*>(smem + row * kPitch + ch * 16) =
+                __builtin_bit_cast(v4u, __builtin_amdgcn_raw_buffer_load_b128(src, off, 0, 0));
+        }
+    }
+    template <int W, class CM = ColStd>
+    DEV void apply(int mw, int nw, f32x4 (&acc)[4][4], int, char* smem) const {
+        const int lane = threadIdx.x & 63, q = lane >> 4, li = lane & 15;
+        const int lc0 = mw & (BM - 1), lr0 = nw & (W - 1);
+        f32x4 cs[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) cs[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int row = nw + CM::off(j) + li;
+            const bool rok = row < M;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const bool ok = rok && mw + 16 * i + 4 * q < N;
+                char* px = smem + (lr0 + CM::off(j) + li) * kPitch + (lc0 + 16 * i + 4 * q) * 2;
+                const uint2 tr = *reinterpret_cast<const uint2*>(px);
+                const float tv[4] = {bf2f(tr.x & 0xFFFFu), bf2f(tr.x >> 16), bf2f(tr.y & 0xFFFFu), bf2f(tr.y >> 16)};
+                float v[4];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    v[r] = acc[i][j][r] * (1.f - tv[r] * tv[r]);
+                    cs[i][r] += ok ? v[r] : 0.f;
+                }
+                *reinterpret_cast<uint2*>(px) = make_uint2(f2bf2(v[0], v[1]), f2bf2(v[2], v[3]));
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int col = mw + 16 * i + 4 * q;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const float v = sum16(cs[i][r]);
+                if (li == 0 && col < N) colpart[(int64_t)CM::slot(nw) * N + col + r] = v;
+            }
+        }
+    }
+    template <int W>
+    DEV void store_out(int m0, int n0, char* smem) const {
+        constexpr int CPR = BM / 8, NL = W * CPR / NTHR;
+#pragma unroll
+        for (int i = 0; i < NL; ++i) {
+            const int id = threadIdx.x + NTHR * i;
+            const int row = id / CPR, ch = id % CPR;
+            const int gr = n0 + row, gc = m0 + ch * 8;
+            if (gr < M && gc < N)
+                *reinterpret_cast<v4u*>(out + (int64_t)gr * ldo + gc) = *reinterpret_cast<const v4u*>(smem + row * kPitch + ch * 16);
+        }
+    }
+};
+
 // Decoder output (VAEB.py:257-263, 302-313) on the [M_e x Dn] block of a2 (| a6):
 //  Bernoulli: a = acc + b2; log p += x a - softplus(a); dA2 = sl (x - sigmoid(a)).
 //  Gaussian : columns interleave in 32-wide groups ([W2 cols | W6 cols] per 64), so a
