@@ -321,7 +321,8 @@ def test_bf16_dp_path_world1_matches_fused_optimizer(overlap, fork, shard, monke
     assert rel(outs[1][2], outs[0][2]) <= 1e-4
 
 
-@pytest.mark.parametrize("forkpt,w2a,gauss", [("1", "0", False), ("2", "0", False), ("3", "0", False), ("1", "1", False),
+@pytest.mark.parametrize("forkpt,w2a,gauss", [("1", "0", False), ("0", "0", False), ("2", "0", False), ("3", "0", False),
+                                              ("1", "1", False),
                                               ("2", "1", False), ("1", "1", True)])
 def test_bf16_forked_and_single_stream_steps_agree(monkeypatch, forkpt, w2a, gauss):
     """the forked bf16 step (dW1, dW2 | dW6 and dW4 | dW5 on a second stream
@@ -330,7 +331,8 @@ def test_bf16_forked_and_single_stream_steps_agree(monkeypatch, forkpt, w2a, gau
     products with the same K order, so 10 Philox steps agree to 1e-6 in every parameter and
     the ELBO -- this pins the cross-stream ordering independently of the golden tolerances;
     graph replay and eager launches agree bitwise for each form.  For every fork point
-    (VAEB_BF_FORKPT: after dhd, after dz + [dMu | dLv], after dh), and with dW2's second
+    (VAEB_BF_FORKPT: after dhd, the same with the main chain captured first, after dz +
+    [dMu | dLv], after dh), and with dW2's second
     column tile in dW3's grid (VAEB_BF_W2A=1 of D / 256 = 2; Gaussian: of 2D / 256 = 4, the
     [W2 | W6] interleave)."""
     monkeypatch.setenv("VAEB_BF_FORKPT", forkpt)

@@ -1357,7 +1357,7 @@ int vaeb_create(const vaeb_config* cfg, vaeb_ctx** out) {
     if (const char* dt = getenv("VAEB_BF_DECT")) c->bf_dect = atoi(dt) != 0;
     if (const char* tt = getenv("VAEB_BF_DTT")) c->bf_dtt = atoi(tt) != 0;
     if (const char* wa = getenv("VAEB_BF_W2A")) c->bf_w2a = std::max(0, atoi(wa));
-    if (const char* fp = getenv("VAEB_BF_FORKPT")) c->bf_forkpt = std::min(3, std::max(1, atoi(fp)));
+    if (const char* fp = getenv("VAEB_BF_FORKPT")) c->bf_forkpt = std::min(3, std::max(0, atoi(fp)));
     if (const char* bt = getenv("VAEB_BF_THIN")) c->bf_thin = atoi(bt) & 3;
     if (const char* ah = getenv("VAEB_ATOMIC_HO")) c->atomic_ho = atoi(ah) != 0 ? 1 : 0;
     if (const char* er = getenv("VAEB_ENC_RED")) c->enc_red = atoi(er) != 0 ? 1 : 0;
