@@ -370,9 +370,10 @@ def test_bf16_forked_and_single_stream_steps_agree(monkeypatch, forkpt, w2a, gau
         assert np.abs(f[1] - u[1]).max() <= 1e-6 and np.abs(f[2] - u[2]).max() <= 1e-6 * max(1.0, np.abs(u[2]).max())
 
 
-@pytest.mark.parametrize("var,alt,base,tol", [("VAEB_BF_SMALLK", "3", "0", 1e-6), ("VAEB_BF_DECT", "0", "1", 1e-5),
-                                              ("VAEB_BF_DTT", "0", "1", 1e-5)])
-def test_bf16_tile_form_switches_agree(monkeypatch, var, alt, base, tol):
+@pytest.mark.parametrize("var,alt,base,tol,Z", [("VAEB_BF_SMALLK", "3", "0", 1e-6, 40), ("VAEB_BF_DECT", "0", "1", 1e-5, 40),
+                                                ("VAEB_BF_DTT", "0", "1", 1e-5, 40), ("VAEB_BF_DZFUSE", "0", "1", 1e-5, 32),
+                                                ("VAEB_BF_DZFUSE", "0", "1", 1e-5, 128)])
+def test_bf16_tile_form_switches_agree(monkeypatch, var, alt, base, tol, Z):
     """Two tile forms of the same products, 6 Philox steps each, graph replay and eager
     launches bitwise equal for each form:
       * VAEB_BF_SMALLK=3: dechid (K = Z) and dh (K = 2Z) on 256 x 128 tiles with two blocks
@@ -383,9 +384,12 @@ def test_bf16_tile_form_switches_agree(monkeypatch, var, alt, base, tol):
         log p and the bias column sums are added in another order: ELBO to 1e-5 relative,
         parameters to a few Adagrad steps;
       * VAEB_BF_DTT=0: dhd and dh on A W (EpiDTanh) against the transposed products
-        (EpiDTanhT, the default) -- their bias column sums in another order: the same bounds."""
+        (EpiDTanhT, the default) -- their bias column sums in another order: the same bounds;
+      * VAEB_BF_DZFUSE=0: dz + latent backward on the thin launch against dZ as split-K slabs
+        from the forked dhd blocks (EpiDTanhTDz, the default; Z % 16 == 0) -- dZ from the
+        bf16-stored dA1 in 256-deep slices: the same bounds (Z = 32; Z = 128: the thin path)."""
     from vaeb_amd import _lib
-    cfg = O.Config(D=512, H=264, Z=40)
+    cfg = O.Config(D=512, H=264, Z=Z)
     B = 520
     x = (np.random.default_rng(6).random((4 * B, cfg.D)) < 0.4).astype(np.float32)
     order = np.array([1, 3, 0, 2, 3, 1], np.int32)

@@ -79,6 +79,9 @@ typedef float f32x2_t __attribute__((ext_vector_type(2)));
 DEV uint32_t f2bf(float f) { return __builtin_bit_cast(uint16_t, (__bf16)f); }
 DEV uint32_t f2bf2(float a, float b) { return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2_t){a, b}, bf16x2_t)); }
 DEV float bf2f(uint32_t b) { return __builtin_bit_cast(float, b << 16); }
+// Epilogue functors with a post(m0, n0, smem) step after store_out (kPost; gemm8_body only)
+template <class E, class = void> struct HasPost : std::false_type {};
+template <class E> struct HasPost<E, std::void_t<decltype(E::kPost)>> : std::bool_constant<E::kPost> {};
 
 // KC images have 64-B rows (BK = 32): chunk c (0..3) of row r lives at c ^ g[(r >> 2) & 3],
 // g = {0, 2, 3, 1}, which makes the four ds_read_b128 lane groups of a 16-row fragment read
@@ -641,6 +644,48 @@ struct EpiDTanhT {
     }
 };
 
+// EpiDTanhT for dhd with dz fused into the block (VAEB_BF_DZFUSE): after the tanh backward the
+// LDS tile holds dA1 for the block's 256 rows x 256 hidden units (bf16, as stored), so the block
+// also forms the split-K partial dZ[rows][Z] = dA1[rows][h-tile] W1[:, h-tile]^T over its 256 h:
+// wave w takes latents 16 w .. + 15 for all 16 row tiles (A fragments from the LDS tile, B from
+// the K-contiguous W1 shadow in L2), 128 MFMAs, and stores the fp32 partial as slab m0 / 256 of
+// dz_slab (the layout of the split-K dz GEMM that latent_bwd_v4_kernel sums in slab order).  The
+// thin dz launch (its ~0.77 MB of LDS-DMA per CU) is then not needed.
+struct EpiDTanhTDz : EpiDTanhT {
+    static constexpr bool kPost = true;
+    const bf16_t* w1; int Z, H;          // W1 shadow [Z][H]
+    float* dz_slab; int64_t slab;        // slab stride (rows x Z floats)
+    DEV void post(int m0, int n0, char* smem) const {
+        const int lane = threadIdx.x & 63, q = lane >> 4, li = lane & 15;
+        const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+        if (16 * w >= Z) return;
+        const rsrc_t bw = mkbuf(w1, (int64_t)Z * H * 2);
+        const int z = 16 * w + li;
+        f32x4 acc[16];
+#pragma unroll
+        for (int rt = 0; rt < 16; ++rt) acc[rt] = zero4();
+#pragma unroll 2
+        for (int ks = 0; ks < 8; ++ks) {
+            const int h = m0 + 32 * ks + 8 * q;
+            const bf16x8 bfr = __builtin_bit_cast(
+                bf16x8, __builtin_amdgcn_raw_buffer_load_b128(bw, (z < Z && h < H) ? ((uint32_t)z * (uint32_t)H + (uint32_t)h) * 2u : kOOB, 0, 0));
+#pragma unroll
+            for (int rt = 0; rt < 16; ++rt) {
+                const bf16x8 af = *reinterpret_cast<const bf16x8*>(smem + (16 * rt + li) * kPitch + (32 * ks + 8 * q) * 2);
+                acc[rt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfr, acc[rt], 0, 0, 0);
+            }
+        }
+        float* out = dz_slab + (int64_t)(m0 >> 8) * slab;
+#pragma unroll
+        for (int rt = 0; rt < 16; ++rt)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int row = n0 + 16 * rt + 4 * q + r;
+                if (row < M && z < Z) out[(int64_t)row * Z + z] = acc[rt][r];
+            }
+    }
+};
+
 // Decoder output (VAEB.py:257-263, 302-313) on the [M_e x Dn] block of a2 (| a6):
 //  Bernoulli: a = acc + b2; log p += x a - softplus(a); dA2 = sl (x - sigmoid(a)).
 //  Gaussian : columns interleave in 32-wide groups ([W2 cols | W6 cols] per 64), so a
@@ -1185,6 +1230,7 @@ DEV void gemm8_body(const GemmArgs& g, const Epi& e, int bid, int kz, char* smem
         __syncthreads();
         e.template store_out<256>(m0, n0, smem);
     }
+    if constexpr (HasPost<Epi>::value) e.post(m0, n0, smem);
 }
 
 template <int LA, int LB, class Epi>
