@@ -372,7 +372,7 @@ def test_bf16_forked_and_single_stream_steps_agree(monkeypatch, forkpt, w2a, gau
 
 @pytest.mark.parametrize("var,alt,base,tol,Z", [("VAEB_BF_SMALLK", "3", "0", 1e-6, 40), ("VAEB_BF_DECT", "0", "1", 1e-5, 40),
                                                 ("VAEB_BF_DTT", "0", "1", 1e-5, 40), ("VAEB_BF_DZFUSE", "0", "1", 1e-5, 32),
-                                                ("VAEB_BF_DZFUSE", "0", "1", 1e-5, 128)])
+                                                ("VAEB_BF_DZFUSE", "0", "1", 1e-5, 128), ("VAEB_BF_ELBOMAIN", "0", "1", 1e-6, 32)])
 def test_bf16_tile_form_switches_agree(monkeypatch, var, alt, base, tol, Z):
     """Two tile forms of the same products, 6 Philox steps each, graph replay and eager
     launches bitwise equal for each form:
@@ -387,7 +387,9 @@ def test_bf16_tile_form_switches_agree(monkeypatch, var, alt, base, tol, Z):
         (EpiDTanhT, the default) -- their bias column sums in another order: the same bounds;
       * VAEB_BF_DZFUSE=0: dz + latent backward on the thin launch against dZ as split-K slabs
         from the forked dhd blocks (EpiDTanhTDz, the default; Z % 16 == 0) -- dZ from the
-        bf16-stored dA1 in 256-deep slices: the same bounds (Z = 32; Z = 128: the thin path)."""
+        bf16-stored dA1 in 256-deep slices: the same bounds (Z = 32; Z = 128: the thin path);
+      * VAEB_BF_ELBOMAIN=0: the ELBO's stage-1 partials on the second stream against the main
+        one (the default): the same launch: 1e-6."""
     from vaeb_amd import _lib
     cfg = O.Config(D=512, H=264, Z=Z)
     B = 520

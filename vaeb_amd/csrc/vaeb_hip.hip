@@ -160,6 +160,7 @@ struct vaeb_ctx {
     bool bf_split2 = false;       // VAEB_BF_SPLIT2: the forked dW2 / dW3 as two K slices (bf_wgrad256)
     int bf_smallk = 0;            // VAEB_BF_SMALLK mask: 1 dechid, 2 dh on 256 x 128 tiles, two blocks per CU
     int bf_forkpt = 1;            // VAEB_BF_FORKPT: where the bf16 step forks its second stream (1, 2, 3)
+    int bf_elbomain = 1;          // VAEB_BF_ELBOMAIN=0: the ELBO stage-1 partials on the second stream (round 4)
     int bf_dzfuse = 1;            // VAEB_BF_DZFUSE=0: dz + latent backward on the thin launch instead of in the forked dhd
     int bf_dtt = 1;               // VAEB_BF_DTT=0: dhd / dh on A W (EpiDTanh) instead of the transpose (EpiDTanhT)
     int bf_dect = 1;              // VAEB_BF_DECT=0: the Bernoulli decoder on hd W2 (EpiDecOut) instead of its transpose
@@ -1358,6 +1359,7 @@ int vaeb_create(const vaeb_config* cfg, vaeb_ctx** out) {
     if (const char* dt = getenv("VAEB_BF_DECT")) c->bf_dect = atoi(dt) != 0;
     if (const char* tt = getenv("VAEB_BF_DTT")) c->bf_dtt = atoi(tt) != 0;
     if (const char* zf = getenv("VAEB_BF_DZFUSE")) c->bf_dzfuse = atoi(zf) != 0;
+    if (const char* em = getenv("VAEB_BF_ELBOMAIN")) c->bf_elbomain = atoi(em) != 0;
     if (const char* wa = getenv("VAEB_BF_W2A")) c->bf_w2a = std::max(0, atoi(wa));
     if (const char* fp = getenv("VAEB_BF_FORKPT")) c->bf_forkpt = std::min(3, std::max(0, atoi(fp)));
     if (const char* bt = getenv("VAEB_BF_THIN")) c->bf_thin = atoi(bt) & 3;
