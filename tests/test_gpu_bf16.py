@@ -370,7 +370,8 @@ def test_bf16_forked_and_single_stream_steps_agree(monkeypatch, forkpt, w2a, gau
         assert np.abs(f[1] - u[1]).max() <= 1e-6 and np.abs(f[2] - u[2]).max() <= 1e-6 * max(1.0, np.abs(u[2]).max())
 
 
-@pytest.mark.parametrize("var,alt,base,tol,Z", [("VAEB_BF_SMALLK", "3", "0", 1e-6, 40), ("VAEB_BF_DECT", "0", "1", 1e-5, 40),
+@pytest.mark.parametrize("var,alt,base,tol,Z", [("VAEB_BF_SMALLK", "3", "0", 1e-6, 40), ("VAEB_BF_DECT", "0", "2", 1e-5, 40),
+                                                ("VAEB_BF_DECT", "1", "2", 1e-5, 40),
                                                 ("VAEB_BF_DTT", "0", "1", 1e-5, 40), ("VAEB_BF_DZFUSE", "0", "1", 1e-5, 32),
                                                 ("VAEB_BF_DZFUSE", "0", "1", 1e-5, 128), ("VAEB_BF_ELBOMAIN", "0", "1", 1e-6, 32)])
 def test_bf16_tile_form_switches_agree(monkeypatch, var, alt, base, tol, Z):
@@ -379,10 +380,11 @@ def test_bf16_tile_form_switches_agree(monkeypatch, var, alt, base, tol, Z):
       * VAEB_BF_SMALLK=3: dechid (K = Z) and dh (K = 2Z) on 256 x 128 tiles with two blocks
         per CU against the 256 x 256 8-phase tiles -- each output element sees the same MFMA
         sequence over k: parameters and ELBO to 1e-6;
-      * VAEB_BF_DECT=0: the Bernoulli decoder on hd W2 (EpiDecOut) against the transposed
-        product W2^T hd^T (EpiDecOutT, the default) -- the same dot products, but the per-row
-        log p and the bias column sums are added in another order: ELBO to 1e-5 relative,
-        parameters to a few Adagrad steps;
+      * VAEB_BF_DECT=0 / 1: the Bernoulli decoder on hd W2 (EpiDecOut) / on the transposed
+        product W2^T hd^T with two 256 x 128 blocks per CU, against the transposed product on
+        256 x 256 8-phase tiles (=2, the default) -- the same dot products, but the per-row log p
+        and the bias column sums are added in another order: ELBO to 1e-5 relative, parameters
+        to a few Adagrad steps;
       * VAEB_BF_DTT=0: dhd and dh on A W (EpiDTanh) against the transposed products
         (EpiDTanhT, the default) -- their bias column sums in another order: the same bounds;
       * VAEB_BF_DZFUSE=0: dz + latent backward on the thin launch against dZ as split-K slabs

@@ -872,7 +872,7 @@ struct EpiDecOutT {
         for (int i = 0; i < 4; ++i) cs[i] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            const int row = nw + 16 * j + li;
+            const int row = nw + CM::off(j) + li;
             const bool rok = row < M;
             float rs = 0.f, pd = 1.f;   // pd: prod (1 + e^-|a|) of the row's <= 16 elements (< 2^16)
 #pragma unroll
@@ -880,7 +880,7 @@ struct EpiDecOutT {
                 const int col = mw + 16 * i + 4 * q;
                 const bool ok = rok && col < D;
                 const f32x4 bias = bld4(bb, col < D ? (uint32_t)col * 4u : kOOB);
-                char* px = smem + (lr0 + 16 * j + li) * kPitch + (lc0 + 16 * i + 4 * q) * 2;
+                char* px = smem + (lr0 + CM::off(j) + li) * kPitch + (lc0 + 16 * i + 4 * q) * 2;
                 const uint2 xr = *reinterpret_cast<const uint2*>(px);
                 float gv[4];
 #pragma unroll
@@ -914,7 +914,7 @@ struct EpiDecOutT {
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     const float v = sum16(cs[i][r]);
-                    if (li == 0 && col < D) colpart[(int64_t)(nw >> 6) * D + col + r] = v;
+                    if (li == 0 && col < D) colpart[(int64_t)CM::slot(nw) * D + col + r] = v;
                 }
             }
         }

@@ -163,7 +163,8 @@ struct vaeb_ctx {
     int bf_elbomain = 1;          // VAEB_BF_ELBOMAIN=0: the ELBO stage-1 partials on the second stream (round 4)
     int bf_dzfuse = 1;            // VAEB_BF_DZFUSE=0: dz + latent backward on the thin launch instead of in the forked dhd
     int bf_dtt = 1;               // VAEB_BF_DTT=0: dhd / dh on A W (EpiDTanh) instead of the transpose (EpiDTanhT)
-    int bf_dect = 1;              // VAEB_BF_DECT=0: the Bernoulli decoder on hd W2 (EpiDecOut) instead of its transpose
+    int bf_dect = 2;              // VAEB_BF_DECT: the Bernoulli decoder on its transpose (EpiDecOutT) on 256 x 256 8-phase
+                                  // tiles (2) or 256 x 128 two-block tiles (1); 0: on hd W2 (EpiDecOut)
     int bf_w2a = 0;               // VAEB_BF_W2A: 256-column tiles of dW2 forked after dhd (0: all), the rest in dW3's grid
     hipStream_t s2 = nullptr;     // DP: the gradient buckets' all-reduces and their Adagrad
     hipEvent_t dp_ev[3] = {};     // fork after dW2, bucket A reduced, bucket A updated
@@ -1356,7 +1357,7 @@ int vaeb_create(const vaeb_config* cfg, vaeb_ctx** out) {
     if (const char* bk = getenv("VAEB_BF_FORK")) c->bf_fork = atoi(bk) != 0;
     if (const char* b2 = getenv("VAEB_BF_SPLIT2")) c->bf_split2 = atoi(b2) != 0;
     if (const char* sk = getenv("VAEB_BF_SMALLK")) c->bf_smallk = atoi(sk) & 3;
-    if (const char* dt = getenv("VAEB_BF_DECT")) c->bf_dect = atoi(dt) != 0;
+    if (const char* dt = getenv("VAEB_BF_DECT")) c->bf_dect = std::min(2, std::max(0, atoi(dt)));
     if (const char* tt = getenv("VAEB_BF_DTT")) c->bf_dtt = atoi(tt) != 0;
     if (const char* zf = getenv("VAEB_BF_DZFUSE")) c->bf_dzfuse = atoi(zf) != 0;
     if (const char* em = getenv("VAEB_BF_ELBOMAIN")) c->bf_elbomain = atoi(em) != 0;
