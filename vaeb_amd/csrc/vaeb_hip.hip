@@ -158,7 +158,7 @@ struct vaeb_ctx {
     int bf_thin = 3;              // VAEB_BF_THIN mask: 1 heads, 2 dz on thin_bf16.hpp (0: split-K + latent kernels)
     bool bf_fork = true;          // VAEB_BF_FORK=0: dW2 in the dhd grid (bf_fuse) or after it
     bool bf_split2 = false;       // VAEB_BF_SPLIT2: the forked dW2 / dW3 as two K slices (bf_wgrad256)
-    int bf_smallk = 0;            // VAEB_BF_SMALLK mask: 1 dechid, 2 dh on 256 x 128 tiles, two blocks per CU
+    int bf_smallk = 1;            // VAEB_BF_SMALLK mask: 1 dechid (default), 2 dh on 256 x 128 tiles, two blocks per CU
     int bf_forkpt = 1;            // VAEB_BF_FORKPT: where the bf16 step forks its second stream (1, 2, 3)
     int bf_elbomain = 1;          // VAEB_BF_ELBOMAIN=0: the ELBO stage-1 partials on the second stream (round 4)
     int bf_dzfuse = 1;            // VAEB_BF_DZFUSE=0: dz + latent backward on the thin launch instead of in the forked dhd
