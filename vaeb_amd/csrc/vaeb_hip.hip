@@ -1374,10 +1374,11 @@ int vaeb_create(const vaeb_config* cfg, vaeb_ctx** out) {
     if (const char* gu = getenv("VAEB_GRAPH_UPLOAD")) c->graph_upload = atoi(gu) != 0;
     {
         const char* g8 = getenv("VAEB_BF_GEMM8");
-        // default: the 8-phase loop for KC x KC (dhd) and KC x KO (enc, dechid); KO x KO (the
-        // forked dW2 | dW6 and dW3) keeps the ring: config 5 step 833 -> 816 us with this mask,
-        // 845 with all three, 858 with KO x KO added to enc (profiles/r3/gemm8_step_ab.txt)
-        g_gemm8 = g8 ? (int)strtol(g8, nullptr, 0) : 3;
+        // default: the 8-phase loop for KC x KC (dhd), KC x KO (enc) and, since round 5, KO x KO
+        // (the forked dW2 | dW6 and dW3): round 3 measured KO x KO on it slower (845 vs 816 us);
+        // with the round-5 step (dz in dhd, the decoder on the 8-phase loop) it is faster:
+        // 738.6 / 741.7 / 740.3 -> 726.8 / 728.7 / 727.4 us (profiles/r5/synth_ab.txt)
+        g_gemm8 = g8 ? (int)strtol(g8, nullptr, 0) : 11;
     }
     if (e != hipSuccess) { delete c; return fail(VAEB_ERR_HIP, "stream/event create: %s", hipGetErrorString(e)); }
     const int64_t D = g.D, H = g.H, Z = g.Z;
