@@ -101,7 +101,7 @@ KERNEL_SYMBOLS = {"p1_enc": "PEnc", "p23_heads_dechid": "heads_dechid_kernel", "
                   # (all listed substrings must appear: the tile width is a template argument)
                   "bf_enc": ("gemm_kernel<0, 1,", "EpiBiasAct>"), "bf_decout": ("EpiDecOut<false>",),
                   "bf_dhd": ("gemm_kernel<0, 0,", "EpiDTanh>"), "bf_dW26": ("EpiAdagrad",),
-                  "bf_dW3": ("EpiAdagrad",), "bf_dhd_dW26": ("gemm2_kernel",),
+                  "bf_dW3": ("EpiAdagrad",), "bf_dhd_dW26": ("2_kernel<1, 1,",),   # gemm2_kernel | gemm8x2_kernel
                   "p5_dhd_dz_w2": "vaeb::dhd_dz_wgrad_kernel", "p8_wgrad_w3w45w1": "vaeb::wgrad3_kernel",
                   "p1_enc_latent_w2": ("vaeb::enc_latent16_w2",), "p5_dhd_dz": "vaeb::dhd_dz_wgrad_kernel"}
 PMC_ROUNDS = ("r5", "r4")   # the newest round whose committed PMC passes give roofline.traffic (traffic_source)
