@@ -97,11 +97,18 @@ KERNEL_SYMBOLS = {"p1_enc": "PEnc", "p23_heads_dechid": "heads_dechid_kernel", "
                   "p8_wgrad_w3w45": "vaeb::wgrad_kernel",
                   "p1_enc_latent": ("vaeb::enc_latent",),   # enc_latent_kernel | enc_latent_fv_kernel
                   "p4_decout_z": ("vaeb::decout_z",),   # decout_z_kernel | decout_z2_kernel
-                  # bf16 GEMMs are one template: the epilogue / layout pair names the launch
-                  # (all listed substrings must appear: the tile width is a template argument)
-                  "bf_enc": ("gemm_kernel<0, 1,", "EpiBiasAct>"), "bf_decout": ("EpiDecOut<false>",),
-                  "bf_dhd": ("gemm_kernel<0, 0,", "EpiDTanh>"), "bf_dW26": ("EpiAdagrad",),
-                  "bf_dW3": ("EpiAdagrad",), "bf_dhd_dW26": ("2_kernel<1, 1,",),   # gemm2_kernel | gemm8x2_kernel
+                  # bf16 GEMMs are one template: the epilogue / layout pair names the launch (all
+                  # substrings of a tuple must appear; a list holds alternatives, the current form
+                  # first: the 8-phase 256 x 256 loop, then the ring forms of earlier rounds)
+                  "bf_enc": [("gemm8_kernel<0, 1,", "EpiBiasAct>"), ("gemm_kernel<0, 1, 256,", "EpiBiasAct")],
+                  "bf_dechid": [("gemm_kernel<0, 1, 128,", "EpiBiasAct"), ("gemm8_kernel<0, 1,", "EpiBiasAct>")],
+                  "bf_heads": [("EpiHeadsLatent",)], "bf_dz": [("EpiDzLatent",)],
+                  "bf_decout": [("EpiDecOutT>",), ("EpiDecOut<false>",)],
+                  "bf_dh": [("gemm8_kernel<0, 0,", "EpiDTanhT>"), ("gemm_kernel<0, 0,", "EpiDTanh>")],
+                  "bf_dhd": [("EpiDTanhTDz>",), ("gemm8_kernel<0, 0,", "EpiDTanhT>"), ("gemm_kernel<0, 0,", "EpiDTanh>")],
+                  "bf_dW26": ("EpiAdagrad",),
+                  "bf_dW3": [("gemm8_kernel<1, 1,", "EpiAdagrad>"), ("gemm_kernel<1, 1,", "EpiAdagrad,")],
+                  "bf_dhd_dW26": ("2_kernel<1, 1,",),   # gemm2_kernel | gemm8x2_kernel
                   "p5_dhd_dz_w2": "vaeb::dhd_dz_wgrad_kernel", "p8_wgrad_w3w45w1": "vaeb::wgrad3_kernel",
                   "p1_enc_latent_w2": ("vaeb::enc_latent16_w2",), "p5_dhd_dz": "vaeb::dhd_dz_wgrad_kernel"}
 PMC_ROUNDS = ("r5", "r4")   # the newest round whose committed PMC passes give roofline.traffic (traffic_source)
@@ -120,11 +127,13 @@ def committed_traffic(kernel, path=PMC_FILES["mnist"], symbols=KERNEL_SYMBOLS):
     except Exception:
         return None
     sym = symbols.get(kernel)
-    if isinstance(sym, str):
-        sym = (sym,)
-    for name, v in data.items():
-        if sym and all(t in name for t in sym) and "hbm_bytes_per_launch" in v:
-            return v["hbm_bytes_per_launch"]
+    if not sym:
+        return None
+    alts = sym if isinstance(sym, list) else [(sym,) if isinstance(sym, str) else sym]
+    for alt in alts:
+        for name, v in data.items():
+            if all(t in name for t in alt) and "hbm_bytes_per_launch" in v:
+                return v["hbm_bytes_per_launch"]
     return None
 
 

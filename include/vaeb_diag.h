@@ -52,6 +52,27 @@ int vaeb_comm_info(vaeb_ctx* ctx, int32_t* rccl_version, int32_t* dp_overlap, in
 int vaeb_dp_plan(const vaeb_config* cfg, int32_t world, int32_t rank, int32_t sharded, int32_t bucket,
                  int64_t* out_P, int64_t* runs, int32_t* out_nrun, int64_t* own, int32_t* out_nown,
                  int32_t* out_book, int64_t* foreign, int32_t* out_nforeign);
+/* Diagnostics: the world > 1 device path of the sharded data-parallel optimizer on ONE GPU.
+ * Runs rank `rank` of a `world`-rank step's optimizer for one gradient bucket (0 = A, 1 = B,
+ * 2 = all; as vaeb_dp_plan) on a context WITHOUT a communicator, with the collectives of
+ * dp_reduce_update replaced by host copies and its kernels and index ranges unchanged:
+ *   1. bucket 0 or 2 (a step's first bucket): the out arena (theta' and the bf16 shadow) is
+ *      filled with NaN, so every element the step leaves was written by it;
+ *   2. the reduce-scatter: grad_sum (P + 1 floats, the summed data gradient | SGVB) is uploaded
+ *      to this rank's destinations only (its own shards and the replicated remainders); every
+ *      other gradient element is NaN;
+ *   3. this rank's optimizer launch over its range (the step's adagrad kernel; bf16: with the
+ *      shadow of what it updates); the SGVB bookkeeping is not run;
+ *   4. theta_gathered (P floats, may be NULL): the all-gather -- the other ranks' theta' shards
+ *      are copied into the out arena -- then (bf16) the shadow rewrite of those elements
+ *      (shadow_runs_kernel).
+ * finish = 1 flips the arenas as a step does (vaeb_get_params then reads theta').  The
+ * Adagrad state is updated in place for this rank's range only (vaeb_get_adagrad_state). */
+int vaeb_dp_rank_update(vaeb_ctx* ctx, int32_t world, int32_t rank, int32_t bucket, const float* grad_sum,
+                        int64_t n_grad, const float* theta_gathered, int32_t finish);
+/* Diagnostics (bf16 engine): the current bf16 shadow of the weight elements, in arena
+ * (reference) order; n = the number of weight elements (the arena before the biases). */
+int vaeb_get_shadow(vaeb_ctx* ctx, uint16_t* out, int64_t n);
 /* Diagnostics: one eager step with a 100 MHz s_memrealtime stamp per workgroup at the
  * stage boundaries of every launch; out = [launch][1024 workgroups][8 slots]. */
 int vaeb_debug_timeline(vaeb_ctx* ctx, int32_t batch_index, uint64_t* out, int64_t cap,

@@ -159,7 +159,8 @@ int vaeb_get_step(vaeb_ctx* ctx, int64_t* step);
  * wrote it.  Loading checks that the file's D, H, Z, L, decoder and estimator match.
  * With a sharded data-parallel communicator (world > 1) saving is a collective: every rank
  * calls it (the Adagrad shards are all-gathered first); a rank passing path == NULL joins the
- * gather and writes nothing (rank 0 writes the file). */
+ * gather and writes nothing (rank 0 writes the file); NULL on a context without such a
+ * communicator is VAEB_ERR_ARG. */
 int vaeb_checkpoint_save(vaeb_ctx* ctx, const char* path);
 int vaeb_checkpoint_load(vaeb_ctx* ctx, const char* path);
 

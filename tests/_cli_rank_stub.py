@@ -3,7 +3,7 @@ each child of cli.main's launcher (dp.spawn_ranks), with the HIP library replace
 recording stand-in of tests/test_cli_dp.py (gloo all-reduce, no GPU).  Writes what it saw
 (its rank environment, its stdout) to $STUB_OUT/rank<r>.json.  STUB_MODE=fail makes rank 1
 exit 3 before joining the group; STUB_MODE=hang makes rank 1 exit 0 at once while rank 0
-never returns."""
+never returns; STUB_MODE=slowlead makes rank 0's .mdl save sleep STUB_SLOW_S seconds first."""
 import io
 import json
 import os
@@ -32,6 +32,15 @@ def main():
     from test_cli_dp import RecordingCtx
     from vaeb_amd import _lib, cli
     _lib.Context = RecordingCtx
+    if mode == "slowlead" and rank == 0:
+        # rank 0's lead-only tail (the .mdl write) outlasts the straggler deadline
+        from vaeb_amd import model as M
+        save = M.VAEB.save
+
+        def slow_save(self, f):
+            time.sleep(float(os.environ.get("STUB_SLOW_S", "4")))
+            save(self, f)
+        M.VAEB.save = slow_save
     buf = io.StringIO()
     with redirect_stdout(buf):
         cli.main(sys.argv[1:])

@@ -68,6 +68,32 @@ def test_round4_traffic_file_resolves_every_launch():
         assert v is not None and v > 1e6, (name, v)
 
 
+def test_bf16_symbols_resolve_in_the_newest_synth_pmc():
+    """every bf16 launch of the profiled (unforked) config-5 step maps to a kernel of
+    the newest committed synth PMC file under its current name, and the forms the profiled step
+    does not run (the forked dhd, dW2) do not silently take another launch's bytes."""
+    path = bench.PMC_FILES["synth"]
+    assert os.path.exists(path), path
+    import json
+    names = list(json.load(open(path)))
+    got = {}
+    for k in ("bf_enc", "bf_dechid", "bf_heads", "bf_dz", "bf_decout", "bf_dh", "bf_dhd_dW26", "bf_dW3"):
+        v = bench.committed_traffic(k, path)
+        assert v is not None and v > 1e6, (k, v)
+        got[k] = v
+    # the current forms are matched first: the 8-phase encoder, the transposed decoder
+    def first_match(k):
+        sym = bench.KERNEL_SYMBOLS[k]
+        for alt in sym:
+            for n in names:
+                if all(t in n for t in alt):
+                    return n
+    assert "gemm8_kernel<0, 1," in first_match("bf_enc")
+    assert "EpiDecOutT" in first_match("bf_decout")
+    assert "gemm_kernel<0, 1, 128," in first_match("bf_dechid")
+    assert got["bf_enc"] != got["bf_dechid"]
+
+
 def test_bf16_launch_flops_sum_to_step():
     fl = bench.phase_flops(4096, 2048, 128, 8192)
     parts = ["bf_enc", "bf_heads", "bf_dechid", "bf_decout", "bf_dhd", "bf_dW26", "bf_dz", "bf_dW1", "bf_dh",

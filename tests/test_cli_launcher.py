@@ -11,7 +11,9 @@ stopping the other ranks -- is what runs.  Checked:
 * a failing rank makes main exit with its code, and the other rank (blocked in the group
   rendezvous) is killed rather than left hanging;
 * a rank still running after its peer exited 0 is stopped after the straggler deadline
-   with dp.RANK_HUNG.
+  (ADVICE r4) with dp.RANK_HUNG;
+* rank 0's lead-only tail (the .mdl save) longer than that deadline is not a hang: the ranks
+  leave train_model together through a final barrier.
 """
 import os
 import sys
@@ -87,3 +89,13 @@ def test_cli_launcher_straggler_deadline(launcher, monkeypatch):
     assert ei.value.code == dp.RANK_HUNG
     assert time.monotonic() - t0 < 30
     assert not _alive(int(open(launcher / "started0").read()))
+
+
+def test_cli_launcher_slow_lead_tail_is_not_a_straggler(launcher, monkeypatch):
+    from vaeb_amd import cli
+    monkeypatch.setenv("STUB_MODE", "slowlead")
+    monkeypatch.setenv("STUB_SLOW_S", "4")
+    monkeypatch.setenv("VAEB_RANK_DEADLINE_S", "2")
+    assert cli.main(list(ARGV) + ['--save_file', 'm.mdl']) == (None, None)
+    assert os.path.exists(launcher / "rank0.json") and os.path.exists(launcher / "rank1.json")
+    assert os.path.getsize(launcher / "m.mdl") > 0

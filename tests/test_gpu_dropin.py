@@ -62,12 +62,10 @@ def test_row_offset_selects_this_ranks_rows(with_comm):
 
 
 @pytest.mark.parametrize("n", [1, 2, 3, 20, 37, 69])
-@pytest.mark.parametrize("upload", ["1", "0"])
-def test_graph_replay_any_length_equals_eager(n, upload, monkeypatch):
-    """Replays of the captured step family (uploaded at capture by default, VAEB_GRAPH_UPLOAD;
-    or at their first launch) equal eager launches bitwise, for any call length."""
+def test_graph_replay_any_length_equals_eager(n):
+    """Replays of the captured step family (uploaded at capture) equal eager launches bitwise,
+    for any call length."""
     from vaeb_amd import _lib
-    monkeypatch.setenv("VAEB_GRAPH_UPLOAD", upload)
     cfg = O.Config(D=784, H=500, Z=20)
     x = O.synthetic_mnist(n=2000)
     order = np.random.default_rng(n).integers(0, 20, n).astype(np.int32)
@@ -147,6 +145,9 @@ def test_native_checkpoint_resume_is_bit_identical(tmp_path):
     a = fresh()
     a.update_many(order[:29])            # odd: the writer sits on parameter arena 1
     f = str(tmp_path / "run.ckpt")
+    # a NULL path is only a non-writing rank's part of a multi-rank gather
+    with pytest.raises(_lib.VaebError, match="null path"):
+        a.checkpoint_save(None)
     a.checkpoint_save(f)
     a.epoch_elbo()
     a.update_many(order[29:])

@@ -378,13 +378,11 @@ def test_atomic_and_slab_handoffs_agree(kw, monkeypatch):
     """Every fp32 step form a switch can select, on the same 6 Philox steps: the default
     (VAEB_ATOMIC_HO=1: counted fixed-point atomics up to fan-in 16, slabs above), slabs +
     ticket + reducer everywhere (=0), the encoder slabs summed by the decoder launch
-    (VAEB_ENC_RED=1), the unfolded latent backward (VAEB_FOLD_BWD=0: the P67 launches) and
-    one 16-column tile per Bernoulli decoder workgroup (VAEB_DECOUT_CT=1), the encoders on
-    512-thread workgroups (VAEB_ENC16=0; =1: the atomic hand-off encoder only), the slab-form
-    latent backward finished in the dhd launch (VAEB_BWD_DEFER=0) instead of the last launch,
-    each step's dW2 in its own dhd launch (VAEB_DW2_DEFER=0) instead of the next encoder's, the
-    encoder's [mu | lv] partials as exact fixed-point sums (VAEB_ENC_FX=1) instead of fp32 slabs
-    summed by every decoder workgroup.
+    (VAEB_ENC_RED=1), the unfolded latent backward (VAEB_FOLD_BWD=0: the P67 launches), the
+    slab-form latent backward finished in the dhd launch (VAEB_BWD_DEFER=0) instead of the last
+    launch, each step's dW2 in its own dhd launch (VAEB_DW2_DEFER=0) instead of the next
+    encoder's.  (The measured-slower forms of rounds 3-5 -- one decoder column tile, 512-thread
+    encoders, fixed-point encoder sums, the two-tile dhd launch -- were removed in round 6.)
     They sum the same partials in different arithmetic (exact integer vs ordered fp32), so
     they agree to rounding, and each is bitwise deterministic (graph == eager)."""
     from vaeb_amd import _lib
@@ -394,34 +392,19 @@ def test_atomic_and_slab_handoffs_agree(kw, monkeypatch):
     order = np.array([3, 1, 4, 1, 5, 7], np.int32)
     out = {}
     # "decred": VAEB_ENC_RED=1, the encoder's slabs summed by every decoder workgroup;
-    # "dct1": one 16-column tile per Bernoulli decoder workgroup (default two)
-    # "enc8": no encoder on 1024 threads (VAEB_ENC16=0); "enc16slab": only the slab-only one
-    # (=1; default 2: the atomic hand-off encoder on 1024-thread workgroups too)
     # "ticket": VAEB_BWD_DEFER=0, the slab-form latent backward finished by the dhd launch's last
     # arriver (default 1: by reducer workgroups of the last launch, kernels_aux.hpp LatRed)
     # "dw2now": VAEB_DW2_DEFER=0, each step's dW2 (| dW6) in its own dhd launch (default 1: in the
     # next step's encoder launch, the last one flushed by get_params)
-    # "encfx": VAEB_ENC_FX=1, the encoder's [mu | lv] as exact fixed-point sums read by the decoder
-    # "dhd2": VAEB_DHD2=1, two dA1 column tiles per 1024-thread dhd workgroup where one-tile
-    # workgroups exceed the atomics' fan-in (MNIST: 16 instead of 32 contributors), the counted
-    # atomics completing [dMu | dLv] in the dhd launch (default 0: the last launch's reducers)
-    modes = {"atomic": ("1", "0", "1", "2", "2", "1", "1"), "slab": ("0", "0", "1", "2", "2", "1", "1"),
-             "decred": ("1", "1", "1", "2", "2", "1", "1"), "unfolded": ("1", "0", "0", "2", "2", "1", "1"),
-             "dct1": ("1", "0", "1", "1", "2", "1", "1"), "enc8": ("1", "1", "1", "2", "0", "1", "1"),
-             "enc16slab": ("1", "0", "1", "2", "1", "1", "1"), "ticket": ("0", "0", "1", "2", "2", "0", "1", "0", "0"),
-             "dw2now": ("1", "0", "1", "2", "2", "1", "0"), "encfx": ("1", "0", "1", "2", "2", "1", "1", "1"),
-             "dhd2": ("1", "0", "1", "2", "2", "1", "1", "0", "1")}
+    # (ATOMIC_HO, ENC_RED, FOLD_BWD, BWD_DEFER, DW2_DEFER)
+    modes = {"atomic": ("1", "0", "1", "1", "1"), "slab": ("0", "0", "1", "1", "1"),
+             "decred": ("1", "1", "1", "1", "1"), "unfolded": ("1", "0", "0", "1", "1"),
+             "ticket": ("0", "0", "1", "0", "1"), "dw2now": ("1", "0", "1", "1", "0")}
     for mode in modes:
         for use_graph in (True, False):
-            monkeypatch.setenv("VAEB_ATOMIC_HO", modes[mode][0])
-            monkeypatch.setenv("VAEB_ENC_RED", modes[mode][1])
-            monkeypatch.setenv("VAEB_FOLD_BWD", modes[mode][2])
-            monkeypatch.setenv("VAEB_DECOUT_CT", modes[mode][3])
-            monkeypatch.setenv("VAEB_ENC16", modes[mode][4])
-            monkeypatch.setenv("VAEB_BWD_DEFER", modes[mode][5])
-            monkeypatch.setenv("VAEB_DW2_DEFER", modes[mode][6])
-            monkeypatch.setenv("VAEB_ENC_FX", modes[mode][7] if len(modes[mode]) > 7 else "0")
-            monkeypatch.setenv("VAEB_DHD2", modes[mode][8] if len(modes[mode]) > 8 else "0")
+            for var, v in zip(("VAEB_ATOMIC_HO", "VAEB_ENC_RED", "VAEB_FOLD_BWD", "VAEB_BWD_DEFER", "VAEB_DW2_DEFER"),
+                              modes[mode]):
+                monkeypatch.setenv(var, v)
             ctx = _lib.Context(cfg.D, cfg.H, cfg.Z, B, L=cfg.L,
                                decoder=_lib.DEC_GAUSSIAN if cfg.continuous else _lib.DEC_BERNOULLI,
                                max_eval_rows=B, use_graph=use_graph)
@@ -438,15 +421,15 @@ def test_atomic_and_slab_handoffs_agree(kw, monkeypatch):
         assert np.array_equal(out[mode, True][1], out[mode, False][1])
     es = out["slab", True][0]
     frac = {}
-    for mode in ("atomic", "decred", "unfolded", "dct1", "enc8", "enc16slab", "ticket", "dw2now", "encfx", "dhd2"):
+    for mode in ("atomic", "decred", "unfolded", "ticket", "dw2now"):
         ea = out[mode, True][0]
         assert abs(ea - es) <= 1e-5 * abs(es), (mode, ea, es)
         d = np.abs(out[mode, True][1] - out["slab", True][1])
         assert d.max() <= 2 * len(order) * cfg.lr, mode    # a ~lr sign(g) step may flip where |g| ~ 1e-7
         frac[mode] = float((d > 1e-3 * cfg.lr).mean())
     # Parameters whose gradient is a cancellation-dominated sum (|g| near rounding of its terms)
-    # take Adagrad steps that follow that rounding; a different K split of the encoder (enc8:
-    # 8 instead of 16 partials) moves ~0.13 % of MNIST's parameters by more than 1e-3 lr.
+    # take Adagrad steps that follow that rounding (a different K split of the encoder moved
+    # ~0.13 % of MNIST's parameters by more than 1e-3 lr).
     assert max(frac.values()) <= 2e-3, frac
 
 
@@ -462,13 +445,9 @@ def test_deferred_dw2_is_bitwise_the_same_step(kw, monkeypatch):
     cfg = O.Config(**kw)
     x = data_for(cfg, 800)
     res = {}
-    # VAEB_DHD2=0: the latent backward's form held fixed (the deferred reducers), so the deferral
-    # alone differs; "dhd2" runs the two-tile dhd launch (VAEB_DHD2=1; only with the deferral), whose
-    # graph and eager runs must agree bitwise along the same sequence
-    for defer, dhd2 in (("1", "0"), ("0", "0"), ("1", "1")):
+    for defer in ("1", "0"):
         for use_graph in (True, False):
             monkeypatch.setenv("VAEB_DW2_DEFER", defer)
-            monkeypatch.setenv("VAEB_DHD2", dhd2)
             ctx = _lib.Context(cfg.D, cfg.H, cfg.Z, 100, decoder=int(cfg.continuous), max_eval_rows=200,
                                use_graph=use_graph)
             ctx.set_data(x)
@@ -491,14 +470,12 @@ def test_deferred_dw2_is_bitwise_the_same_step(kw, monkeypatch):
             out.append(ctx.get_adagrad_state())
             out.append(ctx.epoch_elbo()[0])
             ctx.close()
-            res[defer, dhd2, use_graph] = out
-    for group in (("1", "0"), ("0", "0")), (("1", "1"),):
-        ref = res[group[-1] + (True,)]
-        for key, out in res.items():
-            if key[:2] in group:
-                for a, b in zip(out, ref):
-                    assert np.array_equal(np.asarray(a), np.asarray(b)), key
-        assert np.array_equal(ref[4], ref[5])   # resume: the same two steps from the checkpoint
+            res[defer, use_graph] = out
+    ref = res["0", True]
+    for key, out in res.items():
+        for a, b in zip(out, ref):
+            assert np.array_equal(np.asarray(a), np.asarray(b)), key
+    assert np.array_equal(ref[4], ref[5])   # resume: the same two steps from the checkpoint
 
 
 def test_deferred_dw2_pending_after_a_replayed_single_step():
@@ -513,14 +490,13 @@ def test_deferred_dw2_pending_after_a_replayed_single_step():
     cfg = O.Config(D=784, H=500, Z=20)
     x = data_for(cfg, 800)
     res = {}
-    # (defer, dhd2, graph): the deferral against the in-step dW2 with the latent backward's form
-    # held fixed (VAEB_DHD2=0), and the two-tile dhd form (VAEB_DHD2=1) replayed against eager steps
-    for key in (("1", "0", True), ("0", "0", True), ("1", "1", True), ("1", "1", False)):
-        os.environ["VAEB_DW2_DEFER"], os.environ["VAEB_DHD2"] = key[0], key[1]
+    # (defer, graph): the deferral against the in-step dW2, and replayed against eager steps
+    for key in (("1", True), ("0", True), ("1", False)):
+        os.environ["VAEB_DW2_DEFER"] = key[0]
         try:
-            ctx = _lib.Context(cfg.D, cfg.H, cfg.Z, 100, max_eval_rows=200, use_graph=key[2])
+            ctx = _lib.Context(cfg.D, cfg.H, cfg.Z, 100, max_eval_rows=200, use_graph=key[1])
         finally:
-            del os.environ["VAEB_DW2_DEFER"], os.environ["VAEB_DHD2"]
+            del os.environ["VAEB_DW2_DEFER"]
         ctx.set_data(x)
         ctx.set_params(O.flatten(O.init_params(cfg)))
         ctx.set_eps_mode(_lib.EPS_PHILOX, 10)
@@ -540,7 +516,7 @@ def test_deferred_dw2_pending_after_a_replayed_single_step():
         out.append(ctx.epoch_elbo()[0])
         ctx.close()
         res[key] = out
-    for k1, k2 in ((("1", "0", True), ("0", "0", True)), (("1", "1", True), ("1", "1", False))):
+    for k1, k2 in ((("1", True), ("0", True)), (("1", True), ("1", False))):
         for i, (a, b) in enumerate(zip(res[k1], res[k2])):
             assert np.array_equal(np.asarray(a), np.asarray(b)), (k1, i)
 

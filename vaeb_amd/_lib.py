@@ -40,7 +40,7 @@ EXPORTS = [
 ]
 DIAG_EXPORTS = ["vaeb_profile_steps", "vaeb_kernel_name", "vaeb_debug_timeline", "vaeb_test_gemm_bf16",
                 "vaeb_bench_gemm_bf16", "vaeb_graph_status", "vaeb_comm_info", "vaeb_time_update_many", "vaeb_busy",
-                "vaeb_dp_plan"]
+                "vaeb_dp_plan", "vaeb_dp_rank_update", "vaeb_get_shadow"]
 GRAPH_MODES = {0: "off", 1: "not_captured", 2: "replay", 3: "eager_fallback"}
 AE_MAX_LAYERS = 8
 AE_BINARY, AE_CONT = 0, 1
@@ -137,6 +137,8 @@ def load():
                          [ctypes.POINTER(_I64), ctypes.POINTER(_I64), ctypes.POINTER(ctypes.c_int32),
                           ctypes.POINTER(_I64), ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int32),
                           ctypes.POINTER(_I64), ctypes.POINTER(ctypes.c_int32)], ctypes.c_int),
+        "vaeb_dp_rank_update": ([_P] + [ctypes.c_int32] * 3 + [_F, _I64, _F, ctypes.c_int32], ctypes.c_int),
+        "vaeb_get_shadow": ([_P, ctypes.POINTER(ctypes.c_uint16), _I64], ctypes.c_int),
         "vaeb_time_update_many": ([_P, ctypes.POINTER(ctypes.c_int32), ctypes.c_int32, _F,
                                    ctypes.POINTER(ctypes.c_double)], ctypes.c_int),
         "vaeb_debug_timeline": ([_P, ctypes.c_int32, ctypes.POINTER(ctypes.c_uint64), _I64,
@@ -423,6 +425,25 @@ class Context:
         n = ctypes.c_int32()
         check(self.lib.vaeb_comm_count(self.h, ctypes.byref(n)))
         return n.value
+
+    def dp_rank_update(self, world, rank, bucket, grad_sum, theta_gathered=None, finish=False):
+        """Diagnostics: rank `rank` of a `world`-rank sharded DP optimizer step for one bucket on
+        this (communicator-less) context, the collectives emulated by host copies
+        (include/vaeb_diag.h vaeb_dp_rank_update).  grad_sum: [P + 1] summed gradient | SGVB;
+        theta_gathered: [P] the other ranks' theta' (the all-gather) or None."""
+        g = np.ascontiguousarray(grad_sum, np.float32)
+        t = None if theta_gathered is None else np.ascontiguousarray(theta_gathered, np.float32)
+        if t is not None and t.size != self.P:
+            raise VaebError(f"theta_gathered holds {t.size} floats, expected {self.P}")
+        check(self.lib.vaeb_dp_rank_update(self.h, int(world), int(rank), int(bucket), fptr(g), g.size,
+                                           fptr(t) if t is not None else None, int(bool(finish))))
+
+    def get_shadow(self, n_weights):
+        """Diagnostics (bf16 engine): the bf16 shadow of the weight elements, arena order, as raw
+        uint16 bits."""
+        out = np.empty(int(n_weights), np.uint16)
+        check(self.lib.vaeb_get_shadow(self.h, out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint16)), out.size))
+        return out
 
     def bench_gemm_bf16(self, a_kouter, b_kouter, M, N, K, tile_n=0, reps=10):
         """Mean ms per launch of the bf16 GEMM on device-generated operands (diagnostics)."""

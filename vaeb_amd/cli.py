@@ -250,6 +250,11 @@ def train_model(args):
         # a collective with the sharded DP optimizer (the Adagrad shards are gathered): every
         # rank joins, rank 0 writes (rank 0 alone blocked in the all-gather)
         model.save_state(args['state_file'] if lead else None)
+    if use_comm and group is not None:
+        # every rank leaves together: the others wait here while rank 0 writes the .mdl and the
+        # trace, so the launcher's straggler deadline (dp.spawn_ranks) only ever measures a rank
+        # that is really stuck, never rank 0's lead-only tail
+        group.barrier()
     return model, data
 
 

@@ -347,14 +347,6 @@ DEV void gemm_body(const GemmArgs& g, const Epi& e, int bid, int kz, char* smem)
 template <int LA, int LB, int BNT, class Epi, int ST = 4>
 __global__ __launch_bounds__(NTHR, (2 * Shape<BNT, ST>::kBlocksPerCU)) void gemm_kernel(GemmArgs g, Epi e) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-#ifdef VAEB_DECO_STAGGER   // (A/B build: the second block slot of every CU starts later)
-    if constexpr (ST == 3) {
-        if (blockIdx.x >= 256 && blockIdx.x < 512) {
-            const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-            while (__builtin_amdgcn_s_memrealtime() - t0 < (uint64_t)(VAEB_DECO_STAGGER * 100)) __builtin_amdgcn_s_sleep(8);
-        }
-    }
-#endif
     gemm_body<LA, LB, BNT, Epi, ST>(g, e, blockIdx.x, blockIdx.y, smem);
 }
 
@@ -508,12 +500,7 @@ struct EpiBiasAct {
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     float v = acc[i][j][r] + b;
-#ifndef VAEB_DBG_NO_TANH   // (timing-only build: the epilogue without its activation)
                     if (tanh_act) v = ftanh_bf(v);
-#endif
-#ifdef VAEB_KO_BA_NOLDS   // (timing-only build: no per-element LDS writes)
-                    if (v == 12345.f)
-#endif
                     lds_st_bf<W>(smem, erow(lr0, i, r, lane), ecol<CM>(lc0, j, lane), v);
                 }
         }
@@ -548,15 +535,9 @@ struct EpiDTanh {
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     const int lr = erow(lr0, i, r, lane), lc = ecol<CM>(lc0, j, lane);
-#ifdef VAEB_KO_DT_NOLDS   // (timing-only build: no per-element LDS reads / writes)
-                    const float tv = 0.5f * (float)(lr & 1);
-                    const float v = acc[i][j][r] * (1.f - tv * tv);
-                    if (v == 12345.f) lds_st_bf<W>(smem, lr, lc, v);
-#else
                     const float tv = lds_bf<W>(smem, lr, lc);
                     const float v = acc[i][j][r] * (1.f - tv * tv);
                     lds_st_bf<W>(smem, lr, lc, v);
-#endif
                     cs += (erow(mw, i, r, lane) < M) ? v : 0.f;
                 }
             cs = colsum_lanes(cs);
@@ -711,9 +692,6 @@ struct EpiDecOut {
     float* yout;
     template <int W>
     DEV void load_in(int m0, int n0, char* smem) const {
-#ifdef VAEB_KO_DECO_NOX   // (timing-only build: the x tile is not fetched)
-        return;
-#endif
         const rsrc_t src = mkbuf(x + xb.offset(), (int64_t)Mx * ldx * 2);
         if constexpr (GAUSS) tile_load<W / 2, W, true>(smem, src, ldx, m0, n0 / 2, M, D, Mx);
         else tile_load<W, W>(smem, src, ldx, m0, n0, M, D, Mx);
@@ -749,18 +727,9 @@ struct EpiDecOut {
                 for (int r = 0; r < 4; ++r) {
                     const int row = erow(mw, i, r, lane), lr = erow(lr0, i, r, lane);
                     const bool ok = cok[j] && row < M;
-#ifdef VAEB_KO_DECO_NOLDS   // (timing-only build: no per-element LDS x reads / dA writes)
-                    const float xv = (float)(lr & 1);
-#else
                     const float xv = lds_bf<W>(smem, lr, ecol<CM>(lc0, j, lane));
-#endif
                     const float a2 = acc[i][j][r] + bb2[j];
                     float y, lpv, g2, g6 = 0.f;
-#ifdef VAEB_KO_DECO_NOMATH   // (timing-only build: the likelihood arithmetic replaced by copies)
-                    if constexpr (true) {
-                        y = a2; lpv = xv; g2 = a2 + xv;
-                    } else
-#endif
                     if constexpr (!GAUSS) {
                         // log p = x a - softplus(a) = x a - max(a, 0) - log(1 + e^-|a|): the
                         // logs of a row's JN elements are taken once, of their product (<= 2^JN)
@@ -781,9 +750,7 @@ struct EpiDecOut {
                     rs[r] += ok ? lpv : 0.f;
                     if (yout && ok) yout[(int64_t)row * D + d[j]] = y;
                     if (train) {
-#ifndef VAEB_KO_DECO_NOLDS
                         lds_st_bf<W>(smem, lr, ecol<CM>(lc0, j, lane), g2);
-#endif
                         cs2[j] += ok ? g2 : 0.f;
                         if constexpr (GAUSS) {
                             lds_st_bf<W>(smem, lr, ecol<CM>(lc0, j, lane) + 32, g6);
@@ -815,9 +782,7 @@ struct EpiDecOut {
     }
     template <int W>
     DEV void store_out(int m0, int n0, char* smem) const {
-#ifndef VAEB_KO_DECO_NOST   // (timing-only build: dA not stored)
         if (train) tile_store<W>(smem, dA, ldd, m0, n0, M, N);
-#endif
     }
 };
 

@@ -228,11 +228,7 @@ DEV float opt_rule(const OptArgs& o, float th, float& acc, float dsg) {
 // (4 accumulators sharing one A fragment).  The epilogue applies prior + Adagrad
 // (theta / acc prefetched before the panels) or stores the gradient (DP / introspection).
 typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
-#ifdef VAEB_NO_TV
-constexpr bool kNoTV = true;    // A/B build: the MFMA-layout epilogue (four 4-byte accesses per value group)
-#else
 constexpr bool kNoTV = false;
-#endif
 constexpr int kWT = 64;   // weight rows (i) per tile; the columns per tile are 16 * TS (wgrad_body)
 constexpr int kWKB = 128;
 constexpr int kWP = 68;
@@ -280,10 +276,7 @@ struct LatRed {
 // counter with those stores 35.06 / 35.17, the single counter with dword stores (the default)
 // 34.51 / 34.35; the timeline build saw the poll return ~2 µs earlier with replicas, the
 // production step did not.  Eight copies of [dMu | dLv] as well (one per XCD): 10.86 vs 10.57 µs.
-#ifndef VAEB_LAT_CNT
-#define VAEB_LAT_CNT 1
-#endif
-constexpr int kLatCnt = VAEB_LAT_CNT, kLatCntStride = 16;   // replicas 64 B apart
+constexpr int kLatCnt = 1, kLatCntStride = 16;   // replicas 64 B apart
 DEV int lat_slot() { return (int)(blockIdx.x & (kLatCnt - 1)); }
 struct Da3Src {
     const float *dml, *W4, *W5, *h;
@@ -380,11 +373,7 @@ DEV void lat_reduce_wg(const LatRed& r, int wi, f32x4* red, float (*dzs)[17], ui
     // publish, write-through (sc1): dword stores (VAEB_LAT_ST4: 16-byte runs staged through LDS);
     // then every storing wave drains, the barrier, one add per counter replica (one instruction)
     const rsrc_t bd = mkbuf(r.dml, (int64_t)r.Mbp * 2 * Z * 4);
-#ifdef VAEB_LAT_ST4   // (A/B build: 16-byte runs; measured no faster, see kLatCnt)
-    if ((nj & 3) == 0 && (Z & 3) == 0 && (j0 & 3) == 0) {
-#else
     if (false) {
-#endif
         float* stg = reinterpret_cast<float*>(red);   // [16 rows][2 nj + 1]
         const int sp = 2 * nj + 1;
         __syncthreads();   // (red held the partition sums)
@@ -417,17 +406,16 @@ DEV void lat_reduce_wg(const LatRed& r, int wi, f32x4* red, float (*dzs)[17], ui
 
 // Consumer side: one lane polls the counter (sc1 loads, s_sleep between polls, bounded), the
 // workgroup joins a barrier; every later load of [dMu | dLv] in the workgroup is an sc1 load.
-#ifndef VAEB_POLL_SLEEP
-#define VAEB_POLL_SLEEP 30   // s_sleep units (64 clocks) between polls: fewer polls of the one counter line
-                            // (A/B, 4000-step runs: 2 -> 34.66 / 34.72 us, 10 -> 34.48 / 34.51, 30 -> 34.34 / 34.35;
-                            // then 30 -> 34.26 / 34.29, 60 -> 34.38 / 34.33, 110 -> 35.61 / 35.55)
-#endif
+// s_sleep units (64 clocks) between polls: fewer polls of the one counter line (A/B, 4000-step
+// runs: 2 -> 34.66 / 34.72 us, 10 -> 34.48 / 34.51, 30 -> 34.34 / 34.35; then 30 -> 34.26 / 34.29,
+// 60 -> 34.38 / 34.33, 110 -> 35.61 / 35.55)
+constexpr int kPollSleep = 30;
 DEV void lat_wait(int* cnt, int nred, uint64_t* const* guard) {
     if (threadIdx.x == 0) {
         typedef __attribute__((address_space(1))) int gi32;
         uint32_t spins = 0;
         while (__hip_atomic_load((gi32*)cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < nred) {
-            __builtin_amdgcn_s_sleep(VAEB_POLL_SLEEP);
+            __builtin_amdgcn_s_sleep(kPollSleep);
             if (++spins >= (1u << 20)) {   // ~1 s: never a hang; the step reports a status instead
                 __hip_atomic_fetch_or((__attribute__((address_space(1))) unsigned long long*)*guard,
                                       (unsigned long long)kGuardHandoffTimeout, __ATOMIC_RELAXED,
@@ -519,11 +507,7 @@ DEV void da3_panel(const Da3Src& d, int kb, int j0, bool store, float (*sb)[kWP]
     for (int ts = 0; ts < TS; ++ts)
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
-#ifdef VAEB_KO_DA3_NOW45   // timing-only knock-out builds of the dA3 panel (wrong results)
-            bw[ts][c] = f32x4{1e-3f * c, 2e-3f, 3e-3f, 4e-3f};
-#else
             bw[ts][c] = ld_w45(bw4, bw5, Z, c < nkc ? H : 0, j0 + 16 * ts + li, c * 16 + 4 * q, vz);
-#endif
         }
 #pragma unroll
     for (int u = 0; u < NR; ++u) {
@@ -538,11 +522,7 @@ DEV void da3_panel(const Da3Src& d, int kb, int j0, bool store, float (*sb)[kWP]
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int mm = r0 + 4 * q + r;
-#ifdef VAEB_KO_DA3_NOH
-                hv[u][ts][r] = 0.5f + 1e-3f * r + (float)mm * 1e-6f; (void)n;
-#else
                 hv[u][ts][r] = bld(bh, (n < H && mm < d.Mb) ? (uint32_t)(mm * H + n) * 4u : kOOB);
-#endif
             }
         }
     }
@@ -555,11 +535,7 @@ DEV void da3_panel(const Da3Src& d, int kb, int j0, bool store, float (*sb)[kWP]
             const int rl = r0 < d.Mbp ? d.Mbp : 0;
 #pragma unroll
             for (int c = 0; c < 4; ++c) {
-#ifdef VAEB_KO_DA3_NODML
-                av[u][c] = f32x4{1e-3f * c, 2e-3f * u, 3e-3f, 4e-3f};
-#else
                 av[u][c] = kc4x<16>(bd, K2, r0 + li, c * 16 + 4 * q, c < nkc ? rl : 0, K2, vd);
-#endif
             }
         }
     }
@@ -571,14 +547,9 @@ DEV void da3_panel(const Da3Src& d, int kb, int j0, bool store, float (*sb)[kWP]
 #pragma unroll
         for (int ts = 0; ts < TS; ++ts) {
             f32x4 acc = zero4();
-#ifdef VAEB_KO_DA3_NOMFMA   // the loaded operands summed instead of multiplied (no MFMA chain)
-#pragma unroll
-            for (int c = 0; c < 4; ++c) acc += av[u][c] + bw[ts][c];
-#else
 #pragma unroll
             for (int c = 0; c < 4; ++c)
                 if (c < nkc) acc = mfma4(av[u][c], bw[ts][c], acc);
-#endif
             const int n = j0 + 16 * ts + li;
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
@@ -675,9 +646,6 @@ DEV void wgrad_body(const WA& p, const WGroup& g, int bid, float (*sa)[kWP], flo
             // unconditional loads (no branch): the waitcnt pass then sees them retired
             // by the first panel wait instead of re-waiting after every epilogue store
             uint32_t lo = (upd && kh == 0) ? off[t][r] : kOOB;
-#ifdef VAEB_KO_W3_NOPREF   // timing-only knock-out build (wrong results): no theta / acc prefetch
-            if constexpr (DA3) lo = kOOB;
-#endif
             th[t][r] = bld(bth, lo);
             ac[t][r] = bld(bac, lo);
         }
@@ -704,9 +672,6 @@ DEV void wgrad_body(const WA& p, const WGroup& g, int bid, float (*sa)[kWP], flo
             const int k = kb + kr;
             const int i = i0 + 4 * c4, j = j0 + 4 * c4;
             const bool jt = 4 * c4 < kWTJ;   // B columns beyond a narrow tile: no fetch
-#ifdef VAEB_KO_W3_NOX   // timing-only knock-out build: no X panel loads in the dW3 tiles
-            if constexpr (DA3) { ra[u] = zero4(); rb[u] = zero4(); continue; }
-#endif
             if (va) {
                 ra[u] = bld4(ba, (k < g.klim_at && i < g.rowsW) ? (uint32_t)(k * g.ld_at + i) * 4u : kOOB);
             } else {
@@ -765,16 +730,10 @@ DEV void wgrad_body(const WA& p, const WGroup& g, int bid, float (*sa)[kWP], flo
                 }
             }
         }
-#ifdef VAEB_KO_W3_NODA3   // timing-only knock-out build: the dA3 panel not formed (and no poll)
-        if constexpr (DA3) {
-            for (int e = tid; e < kWKB * 16; e += NTH) sb[e >> 4][e & 15] = 0.f;
-        }
-#else
         if constexpr (DA3 && DEFER)
             da3_panel<NWV, TS, true>(p.da3, kb, j0, i0 == 0, sb, p.hd.red_cnt, p.hd.nred,
                                      VAEB_DBG_ON(p.dbg) ? p.dbg + bid * 8 : nullptr);
         else if constexpr (DA3) da3_panel<NWV, TS>(p.da3, kb, j0, i0 == 0, sb);
-#endif
 #ifdef VAEB_TIMELINE
         if (VAEB_DBG_ON(p.dbg) && kb == 0 && tid == 0) p.dbg[bid * 8 + 2] = __builtin_amdgcn_s_memrealtime();
 #endif
@@ -857,15 +816,6 @@ DEV void wgrad_body(const WA& p, const WGroup& g, int bid, float (*sa)[kWP], flo
         if (VAEB_DBG_ON(p.dbg) && tid == 0) p.dbg[bid * 8 + 3] = __builtin_amdgcn_s_memrealtime();
         return;
     }
-#ifdef VAEB_KO_W3_NOSTORE   // timing-only knock-out build: the dW3 tiles store nothing
-    if constexpr (DA3) {
-        float sink = 0.f;
-        for (int t = 0; t < kWTS; ++t)
-            for (int r = 0; r < 4; ++r) { float a2 = ac[t][r]; sink += opt_rule(p.opt, th[t][r], a2, acc[t][r]) + a2; }
-        if (sink == 12345.678f) bst(bgr, 0, sink);
-        return;
-    }
-#endif
 #pragma unroll
     for (int t = 0; t < kWTS; ++t)
 #pragma unroll
@@ -886,13 +836,10 @@ template <bool VEC, int TS>
 __global__ __launch_bounds__(256) void wgrad_kernel(WGradArgs p) {
     __shared__ float sa[kWKB][kWP];
     __shared__ float sb[kWKB][kWP];
-#ifndef VAEB_ELBO_FIRST
-#define VAEB_ELBO_FIRST 1
-#endif
     // the ELBO workgroup (with_elbo) is block 0, dispatched first, so its reduction runs
     // beside the weight-gradient tiles instead of after the last of them was placed
     int bid;
-    if (VAEB_ELBO_FIRST && p.with_elbo)
+    if (p.with_elbo)
         bid = blockIdx.x == 0 ? p.total_wgs : xcd_remap((int)blockIdx.x - 1, p.total_wgs);
     else
         bid = (int)blockIdx.x < p.total_wgs ? xcd_remap(blockIdx.x, p.total_wgs) : (int)blockIdx.x;
@@ -949,9 +896,6 @@ __global__ __launch_bounds__(256) void wgrad3_kernel(WGradArgs3 p) {
             return;
         }
         b -= h.nred;
-#ifdef VAEB_TILE_DELAY   // A/B build: the tiles hold their bulk loads back so the reducers' slab loads go first
-        __builtin_amdgcn_s_sleep(VAEB_TILE_DELAY);
-#endif
     }
     const int bid = xcd_remap(b, h.total_wgs);
     if (VAEB_DBG_ON(p.dbg) && threadIdx.x == 0) p.dbg[bid * 8 + 0] = __builtin_amdgcn_s_memrealtime();

@@ -58,10 +58,9 @@ DEV f32x4 ld4_sc1(rsrc_t b, uint32_t off) {
 //       consumer, its other waves load after the __syncthreads below; hipMalloc'd
 //       memory, one workgroup per CU (224 / 256 tiles at MNIST-20).
 // The relaxed add and the wavefront fence only keep the compiler from hoisting the slab
-// loads above the ticket.  VAEB_SLAB_ACQREL builds the fenced form instead (agent release
-// before the add, agent acquire after it) for the A/B in DESIGN.md 4.1: the release writes
-// back the XCD L2 (buffer_wbl2) and the acquire invalidates the CU's L1, ~1.7 us each by
-// the guide's price list.
+// loads above the ticket.  The fenced form (agent release before the add, agent acquire after
+// it: the release writes back the XCD L2, the acquire invalidates the CU's L1) measured 2.9 us
+// per step slower in round 2 (its A/B build was removed in round 6).
 // NSW > 1: waves 0 .. NSW-1 stored slab bytes; each drains, the workgroup barrier follows,
 // then lane 0 makes the one ticket add (the guide's producer form "every storing wave's
 // s_waitcnt vmcnt(0), the workgroup's barrier, then ... flag/counter", the release replaced
@@ -75,10 +74,6 @@ DEV bool arrive_last(int* cnt, int target, int* sflag) {
     if (threadIdx.x < 64) {
         if constexpr (NSW == 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         if (threadIdx.x == 0) {
-#ifdef VAEB_SLAB_ACQREL
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the guide's compiler-hazard fix
-#endif
             const int old = __hip_atomic_fetch_add((gint*)cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             *sflag = (old == target - 1);
         }
@@ -86,14 +81,7 @@ DEV bool arrive_last(int* cnt, int target, int* sflag) {
     __syncthreads();
     const bool last = *sflag != 0;
     if (last && threadIdx.x == 0) __hip_atomic_store((gint*)cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#ifdef VAEB_SLAB_ACQREL
-    if (last) {
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-#else
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // keep the slab loads below the ticket
-#endif
     return last;
 }
 
@@ -151,28 +139,6 @@ constexpr int kFxStride = 33;
 constexpr int kFxMaxFanIn = 16;
 DEV uint64_t* fx_at(uint64_t* base, int64_t e) { return base + e * kFxStride; }
 
-// The encoder -> decoder form at fan-in > 16 (HO 4): every contributor adds round(v 2^32) to a
-// plain 64-bit sum with a NO-RETURN atomic (contiguous [row][2Z] words, 128-B segments per
-// wave instruction) and the kernel boundary publishes the sums: exact and order-independent
-// like the counted form, but nobody waits for a count -- the decoder launch decodes them
-// (fx_sum_get) and a later launch of the step zeroes them.  Range: |v| < 2^17, so <= 16 ... 32
-// contributors stay below 2^54; an out-of-range / NaN partial adds POISON = 2^58 instead (and
-// sets the guard word), which decodes to NaN: 32 of them still fit below 2^63.
-constexpr int64_t kFxSumPoison = (int64_t)1 << 58;
-DEV void fx_sum_add(uint64_t* p, uint64_t* guard, float v) {
-    int64_t q;
-    if (__builtin_expect(!(__builtin_fabsf(v) < kFxMax), 0)) {
-        __hip_atomic_fetch_or((gu64*)guard, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        q = kFxSumPoison;
-    } else {
-        q = (int64_t)__builtin_rint((double)v * kFxScale);
-    }
-    __hip_atomic_fetch_add((gu64*)p, (unsigned long long)q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-DEV float fx_sum_get(uint64_t w) {
-    const int64_t q = (int64_t)w;
-    return (q >= kFxSumPoison / 2 || q <= -kFxSumPoison / 2) ? __builtin_nanf("") : (float)((double)q * (1.0 / kFxScale));
-}
 
 // A tile's 16 rows x 2Z partials (Z <= 32) are handed off by all 512 threads of its
 // workgroup, repacked through LDS so that no lane adds for a padding column: thread t takes
@@ -393,19 +359,12 @@ DEV void enc_latent_body(const StepArgs& a, const FvFold& fvf, f32x4* red_ext = 
                 // made visible by the kernel boundary
                 __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, sv), bs,
                                                        nz < Z ? (uint32_t)(((base + (w & 1) * Z + nz) * 16 + 4 * q) * 4) : kOOB, 0, 0);
-            } else if constexpr (HO == 4) {
-                // no-return fixed-point adds into the row block's [mu | lv] sums (fx_sum_inc), the
-                // decoder launch reads the exact sums (decout_z_kernel<.., ZM = 3>)
-                if (nz < Z)
-#pragma unroll
-                    for (int r = 0; r < 4; ++r)
-                        fx_sum_add(a.acc_ml + (int64_t)(m0 + 4 * q + r) * 2 * Z + (w & 1) * Z + nz, a.acc_ml - 1, sv[r]);
             } else {
                 st4_sc1(bs, nz < Z ? (uint32_t)(((base + (w & 1) * Z + nz) * 16 + 4 * q) * 4) : kOOB, sv);
             }
         }
     }
-    if constexpr (HO == 3 || HO == 4) {
+    if constexpr (HO == 3) {
         VAEB_STAMP(a, 2);
         return;
     }
@@ -558,18 +517,12 @@ __global__ __launch_bounds__(1024) void enc_latent16_w2_kernel(StepArgs a, WGrad
     __shared__ __attribute__((aligned(16))) float lds[4 * kWKB * kWP];
     static_assert(sizeof(float) * 4 * kWKB * kWP >= sizeof(f32x4) * 64 * 16 * CT, "LDS union");
     if ((int)blockIdx.y >= rows_enc) {
-#ifdef VAEB_KO_ENC_NOW2   // timing-only knock-out build (wrong results): no deferred dW2 workers
-        return;
-#endif
         const int half = (int)threadIdx.x >> 9;
         const int bid = 2 * (((int)blockIdx.y - rows_enc) * (a.Mbp >> 4) + (int)blockIdx.x) + half;
         float (*sa)[kWP] = reinterpret_cast<float(*)[kWP]>(lds + half * 2 * kWKB * kWP);
         wgrad_body<VEC, 8, TS>(w, w.g[0], bid, sa, sa + kWKB, pend);
         return;
     }
-#ifdef VAEB_KO_ENC_NOENC   // timing-only knock-out build: the dW2 workers alone in the launch
-    return;
-#endif
     enc_latent_body<NCT, GCH, false, HO, CT, 16, true>(a, FvFold{}, reinterpret_cast<f32x4*>(lds));
 }
 
@@ -614,11 +567,7 @@ DEV void decout_z_body(const StepArgs& a) {
     // 2000-step runs, MNIST 34.30 / 34.32 / 34.34 us against 34.46 / 34.46 column-major
     // (-DVAEB_DEC_COLMAJOR).  CT = 1 (Gaussian, Frey) keeps the column-major order: 30.15 / 30.23
     // row-major against 29.77 / 29.83 us.
-#ifdef VAEB_DEC_COLMAJOR
-    constexpr bool kRowMajor = false;
-#else
     constexpr bool kRowMajor = CT == 2;
-#endif
     const int bxr = kRowMajor ? lin / gy : lin % gx, byr = kRowMajor ? lin % gy : lin / gx;
     const int m0 = bxr * 16, n0 = byr * CW;
     const int Z = a.Z, H = a.H;
@@ -655,11 +604,7 @@ DEV void decout_z_body(const StepArgs& a) {
 #pragma unroll
                 for (int w = 0; w < NT; ++w) {
                     const int k = kb + 16 * q + 4 * r + u;
-#ifdef VAEB_KO_DEC_NOW2   // timing-only knock-out build: no W2 loads
-                    w2b[u][r][w] = (float)k * 1e-9f;
-#else
                     w2b[u][r][w] = p.b1(n0 + 16 * (w / NB) + li, k, w % NB);
-#endif
                 }
     };
     // ZM 2: the first kSlabPer slab loads of each thread are issued BEFORE the weight block:
@@ -667,14 +612,6 @@ DEV void decout_z_body(const StepArgs& a) {
     // its own loads, not for the 25 weight-block loads behind them.
     constexpr int kSlabPer = 6;
     f32x4 sv0[ZM == 2 ? kSlabPer : 1];
-    // ZM 3: the row block's fixed-point [mu | lv] sums, [16 rows][2Z] 64-bit words: thread t <
-    // 16 Z loads one pair (16 bytes), issued before the weight block as the slab loads are
-    u32x4 fxp = {0u, 0u, 0u, 0u};
-    if constexpr (ZM == 3) {
-        const rsrc_t bfx = mkbuf(a.acc_ml, (int64_t)a.Mbp * 2 * a.Z * 8);
-        const uint32_t o = (int)threadIdx.x < 16 * a.Z ? (uint32_t)(((m0 % a.Mbp) * 2 * a.Z) * 8 + threadIdx.x * 16) : kOOB;
-        fxp = __builtin_amdgcn_raw_buffer_load_b128(bfx, o, 0, 0);
-    }
     const int nctS = (H + 31) >> 5, nf4S = 8 * Z;
     const int npS = 512 / nf4S;   // nf4 <= 256 (Z <= 32): np >= 2
     const int fS = (int)threadIdx.x % nf4S, partS = (int)threadIdx.x / nf4S;
@@ -684,11 +621,7 @@ DEV void decout_z_body(const StepArgs& a) {
 #pragma unroll
         for (int u = 0; u < kSlabPer; ++u) {
             const int ct = partS + u * npS;
-#ifdef VAEB_KO_DEC_NOSLAB   // timing-only knock-out build: no slab loads (mu, lv = biases)
-            sv0[u] = zero4(); (void)ct;
-#else
             sv0[u] = bld4(bsl, (partS < npS && ct < nctS) ? (uint32_t)((firstS + (int64_t)ct * nf4S) * 16) : kOOB);
-#endif
         }
     }
     load_block(64 * wave);
@@ -702,7 +635,7 @@ DEV void decout_z_body(const StepArgs& a) {
         // and eps of one element (coalesced), the waves then read their fragments from LDS
         __shared__ float zs[16][33];
         __shared__ float gs[16][33];
-        __shared__ float msum[ZM >= 2 ? 64 : 1][17];   // ZM 2 / 3: summed [mu | lv], [column][row]
+        __shared__ float msum[ZM >= 2 ? 64 : 1][17];   // ZM 2: summed [mu | lv], [column][row]
         __shared__ f32x4 spart[ZM == 2 ? 512 : 1];      // ZM 2: per-partition slab sums
         const int per = 16 * Z;
         const int l = m0 / a.Mbp;                 // a 16-row block never straddles two planes
@@ -732,11 +665,7 @@ DEV void decout_z_body(const StepArgs& a) {
             f32x4 sum = zero4();
 #pragma unroll
             for (int u = 0; u < kSlabPer; ++u) sum += sv0[u];
-#ifdef VAEB_KO_DEC_NOSLAB
-            for (int c0 = nct; c0 < nct; c0 += kSlabPer * np) {
-#else
             for (int c0 = part + kSlabPer * np; c0 < nct; c0 += kSlabPer * np) {
-#endif
                 f32x4 v[kSlabPer];
 #pragma unroll
                 for (int u = 0; u < kSlabPer; ++u) {
@@ -757,15 +686,6 @@ DEV void decout_z_body(const StepArgs& a) {
             }
             __syncthreads();
             VAEB_STAMP(a, 6);   // (timeline build) slab sum done
-        }
-        if constexpr (ZM == 3) {
-            if ((int)threadIdx.x < 16 * Z) {   // pair t: row t / Z, columns 2 (t % Z), + 1
-                const int r = (int)threadIdx.x / Z, c = 2 * ((int)threadIdx.x - r * Z);
-                msum[c][r] = fx_sum_get((uint64_t)fxp.x | ((uint64_t)fxp.y << 32));
-                msum[c + 1][r] = fx_sum_get((uint64_t)fxp.z | ((uint64_t)fxp.w << 32));
-            }
-            __syncthreads();
-            VAEB_STAMP(a, 6);
         }
         if ((int)threadIdx.x < per) {
             const int ml = threadIdx.x / Z, j = threadIdx.x - ml * Z;
@@ -886,10 +806,6 @@ DEV void decout_z_body(const StepArgs& a) {
         c[w] = t;
     }
     VAEB_STAMP_SYNC(a, 4);   // (timeline build) the epilogue's operands landed
-#ifdef VAEB_KO_DEC_NOEPI   // timing-only knock-out build: no likelihood epilogue, no stores
-    if (c[0] == 12345.678f) a.y[0] = c[NB - 1];
-    return;
-#endif
     p.epilogue_row(m0, n0 + 16 * et, er, c[0], c[NB - 1], pre);
     VAEB_STAMP(a, 3);
     VAEB_STAMP_SYNC(a, 5);   // (timeline build) the epilogue's stores drained

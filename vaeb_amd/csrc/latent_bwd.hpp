@@ -286,13 +286,9 @@ DEV void dhd_dz_body(const PDhdT<V>& p0, int bx, int by, f32x4* red, int sid) {
 
 // Side duties of the dhd launch.  pend (the deferred dW2: no dW2 tiles in this grid): set to 1
 // -- the next step's encoder launch, or the host's flush, runs this step's dW2 (| dW6)
-// (latent.hpp enc_latent16_w2_kernel).  zero[0 .. nzero): the encoder's fixed-point [mu | lv]
-// sums (latent.hpp fx_sum_add, HO 4), read by the decoder launch before this one; zeroed here
-// for the next step's encoder (plain stores, the kernel boundary publishes them).
+// (latent.hpp enc_latent16_w2_kernel).
 struct DhdAux {
     int* pend;
-    uint64_t* zero;
-    int nzero;
 };
 
 // dhd (+ dZ slabs, latent backward) tiles and the dW2 (| dW6) weight-gradient tiles in one
@@ -306,10 +302,6 @@ __global__ __launch_bounds__(512) void dhd_dz_wgrad_kernel(PDhdT<VEC> p, WGradAr
     const int nwg = w.total_wgs - ntile;   // grid = w.total_wgs (no implicit-argument load)
     const int b0 = blockIdx.x;
     if (aux.pend && b0 == 0 && threadIdx.x == 0) *aux.pend = 1;
-    if (aux.zero && b0 * 512 < aux.nzero) {
-        const int i = b0 * 512 + (int)threadIdx.x;
-        if (i < aux.nzero) aux.zero[i] = 0ull;
-    }
     const int bid = b0 < ntile ? xcd_remap(b0, ntile) : ntile + xcd_remap(b0 - ntile, nwg);
     if (bid < ntile) {
         dhd_dz_body<NCT, GCH, VEC, HO>(p, bid % gx, bid / gx, reinterpret_cast<f32x4*>(&sa[0][0]), bid);
@@ -317,23 +309,6 @@ __global__ __launch_bounds__(512) void dhd_dz_wgrad_kernel(PDhdT<VEC> p, WGradAr
     }
     if (VAEB_DBG_ON(w.dbg) && threadIdx.x == 0) w.dbg[bid * 8 + 0] = __builtin_amdgcn_s_memrealtime();
     wgrad_body<VEC, 8, TS>(w, w.g[0], bid, sa, sb);
-}
-
-// The latent backward completed in the dhd launch at MNIST's width (vaeb_hip.hip ho_dz 3):
-// 1024-thread workgroups of two 16-column dA1 tiles each (16 waves splitting K), the counted
-// atomic hand-off at fan-in ceil(H / 32) L <= 16.  No weight-gradient tiles: dW2 (| dW6) is
-// deferred to the next step's encoder launch.  aux: as dhd_dz_wgrad_kernel's.
-template <int NCT, int GCH, bool VEC>
-__global__ __launch_bounds__(1024) void dhd2_dz_kernel(PDhdT<VEC> p, int ntile, int gx, DhdAux aux) {
-    __shared__ f32x4 red[2048];
-    const int b0 = blockIdx.x;
-    if (aux.pend && b0 == 0 && threadIdx.x == 0) *aux.pend = 1;
-    if (aux.zero && b0 * 1024 < aux.nzero) {
-        const int i = b0 * 1024 + (int)threadIdx.x;
-        if (i < aux.nzero) aux.zero[i] = 0ull;
-    }
-    const int bid = xcd_remap(b0, ntile);
-    dhd_dz_body<NCT, GCH, VEC, 1, 2, 16>(p, bid % gx, bid / gx, red, bid);
 }
 
 }  // namespace vaeb

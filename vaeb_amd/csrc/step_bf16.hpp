@@ -57,6 +57,12 @@ __global__ __launch_bounds__(256) void shadow_runs_kernel(const float* th, bf16_
     }
 }
 
+// diagnostics (vaeb_get_shadow): the shadow entries of the weight elements, in arena order
+__global__ __launch_bounds__(256) void shadow_gather_kernel(const bf16_t* sh, bf16_t* out, ShadowMap m) {
+    const int64_t stride = (int64_t)gridDim.x * 256;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < m.nweights; i += stride) out[i] = sh[m.at(i)];
+}
+
 // theta (fp32 arena) -> bf16 shadow
 __global__ __launch_bounds__(256) void make_shadow_kernel(const float* th, bf16_t* sh, ShadowMap m) {
     const int64_t stride = (int64_t)gridDim.x * 256;
@@ -623,11 +629,6 @@ struct BfState {
     bool thin_h = false, thin_z = false;   // heads / dz on the thin launches
     int nkl = 1;
     ShadowMap smap{};
-    // two-slice split-K of the forked weight gradients (gemm8_body, split2_combine): fp32
-    // partials [tiles][256 x 256] and tickets, dW2 (| dW6) at offset 0, dW3 after it
-    float* part = nullptr;
-    int* ticket = nullptr;
-    int t26 = 0, t3 = 0;              // their tile counts (0: that product is not split)
 };
 
 }  // namespace bf

@@ -48,10 +48,7 @@ struct ThinShape {
     // 3-stage ring (prefetch distance 2); 6 x 24 KiB / 4 x 40 KiB rings measured slower
     // (heads 28.9 -> 32.2 us, dz 20.5 -> 21.4): the stream is throughput-, not latency-bound
 // heads (BMT 64): 4 stages of 24 KiB (round 5: 31.2 -> 28.4 us against 3; 6 stages 32.4)
-#ifndef VAEB_THIN_ST_H
-#define VAEB_THIN_ST_H 4
-#endif
-    static constexpr int kStages = BMT == 64 ? VAEB_THIN_ST_H : 3;
+    static constexpr int kStages = BMT == 64 ? 4 : 3;
     static constexpr int kSmem = kStages * kStage;
 };
 
@@ -64,11 +61,7 @@ struct ThinArgs {
 
 template <int N>
 DEV void thin_wait() {   // all but the N youngest vector-memory ops done, LDS ops done; barrier
-#ifdef VAEB_KO_THIN_NOWAIT   // (timing-only build: stages read before their DMAs land)
-    __builtin_amdgcn_s_waitcnt((15) | ((63 >> 4) << 14) | (7 << 4));
-#else
     __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4));
-#endif
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
 }
@@ -100,13 +93,7 @@ DEV void thin_body(const ThinArgs& t, const Epi& e, int bm, int bn, char* smem) 
     typename Epi::Pre pre = e.prefetch(m0, bn, wr, wc, lane);
 
     const int nst = (t.K + S::KT * BK - 1) / (S::KT * BK);
-#ifdef VAEB_THIN_ROT
-    // every block starts its K sweep at its own stage (blocks of one XCD then read different
-    // B rows at any moment instead of all the same few L2 lines); the sum order is fixed per block
-    const int rot = (int)(((uint32_t)(bm * gridDim.y + bn) * 7u) % (uint32_t)nst);
-#else
     constexpr int rot = 0;
-#endif
     auto issue = [&](int st_) {   // ring stage st_: K-tiles kt = st * KT + u of stage st = (st_ + rot) mod nst
         char* img = smem + (st_ % S::kStages) * S::kStage;
         const int st = st_ + rot < nst ? st_ + rot : st_ + rot - nst;
@@ -139,17 +126,7 @@ DEV void thin_body(const ThinArgs& t, const Epi& e, int bm, int bn, char* smem) 
                 }
                 lds = (uint32_t)(uintptr_t)(img + S::KT * S::kA + u * S::kB + (pb0 % PPI) * 1024);
             }
-#ifdef VAEB_KO_THIN_NOA   // (timing-only builds: one operand's DMAs read nothing)
-            if (piece < S::kPA) off = kOOB;
-#endif
-#ifdef VAEB_KO_THIN_NOB
-            if (piece >= S::kPA) off = kOOB;
-#endif
-#ifndef VAEB_KO_THIN_NODMA   // (timing-only build: no DMA at all)
             dma16(piece < S::kPA ? da : db, off, __builtin_amdgcn_readfirstlane(lds));
-#else
-            (void)off; (void)lds;
-#endif
         }
     };
 
@@ -173,32 +150,17 @@ DEV void thin_body(const ThinArgs& t, const Epi& e, int bm, int bn, char* smem) 
             const char* Bs = img + S::KT * S::kA + u * S::kB;
             const bf16x8 af = frag<KC, BMT>(As, 16 * wr, 0, lane);
             bf16x8 bfr[S::TPW];
-#ifdef VAEB_KO_THIN_NOBREAD   // (timing-only build: B fragments not read from LDS)
-#pragma unroll
-            for (int j = 0; j < S::TPW; ++j) bfr[j] = af;
-#else
 #pragma unroll
             for (int j = 0; j < S::TPW; ++j) bfr[j] = frag<LB, S::NT>(Bs, Epi::col(wc, j), 0, lane);
-#endif
-#ifdef VAEB_KO_THIN_NOMFMA   // (timing-only build: fragments summed instead of multiplied)
-#pragma unroll
-            for (int j = 0; j < S::TPW; ++j) acc[j][0] += (float)af[0] + (float)bfr[j][1];
-#else
 #pragma unroll
             for (int j = 0; j < S::TPW; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfr[j], acc[j], 0, 0, 0);
-#endif
         }
         if constexpr (!k1Bar) {
             __builtin_amdgcn_s_barrier();   // stage st's buffer is refilled by the issue of st + kStages
             asm volatile("" ::: "memory");
         }
     }
-#ifdef VAEB_KO_THIN_NOEPI   // (timing-only build: the accumulators stored, no latent block)
-    if ((acc[0][0] + acc[S::TPW - 1][3]) == 12345.f) *reinterpret_cast<volatile int*>(smem) = wr + wc;
-    (void)pre;
-#else
     e.apply(acc, pre, m0, bn, wr, wc, lane);
-#endif
 }
 
 template <int LB, int BMT, class Epi>

@@ -69,7 +69,12 @@ int dalloc(T** p, size_t n) {
     if (n == 0) n = 1;
     hipError_t e = hipMalloc((void**)p, n * sizeof(T));
     if (e != hipSuccess) return fail(VAEB_ERR_NOMEM, "hipMalloc(%zu) failed: %s", n * sizeof(T), hipGetErrorString(e));
-    hipMemset(*p, 0, n * sizeof(T));
+    // the zero fill runs on the null stream, which does not order against the contexts'
+    // non-blocking streams: wait for it here, or a kernel enqueued next on a context stream can
+    // run before (or beside) the fill and have its stores overwritten with zeros
+    e = hipMemset(*p, 0, n * sizeof(T));
+    if (e == hipSuccess) e = hipStreamSynchronize(nullptr);
+    if (e != hipSuccess) return fail(VAEB_ERR_HIP, "zero fill of %zu bytes: %s", n * sizeof(T), hipGetErrorString(e));
     return 0;
 }
 
@@ -157,15 +162,8 @@ struct vaeb_ctx {
     hipEvent_t fk_ev[4] = {};     // fork after dhd, s3's work done, [dMu | dLv] ready, ELBO partials
     int bf_thin = 3;              // VAEB_BF_THIN mask: 1 heads, 2 dz on thin_bf16.hpp (0: split-K + latent kernels)
     bool bf_fork = true;          // VAEB_BF_FORK=0: dW2 in the dhd grid (bf_fuse) or after it
-    bool bf_split2 = false;       // VAEB_BF_SPLIT2: the forked dW2 / dW3 as two K slices (bf_wgrad256)
-    int bf_smallk = 1;            // VAEB_BF_SMALLK mask: 1 dechid (default), 2 dh on 256 x 128 tiles, two blocks per CU
-    int bf_forkpt = 1;            // VAEB_BF_FORKPT: where the bf16 step forks its second stream (1, 2, 3)
-    int bf_elbomain = 1;          // VAEB_BF_ELBOMAIN=0: the ELBO stage-1 partials on the second stream (round 4)
     int bf_dzfuse = 1;            // VAEB_BF_DZFUSE=0: dz + latent backward on the thin launch instead of in the forked dhd
     int bf_dtt = 1;               // VAEB_BF_DTT=0: dhd / dh on A W (EpiDTanh) instead of the transpose (EpiDTanhT)
-    int bf_dect = 2;              // VAEB_BF_DECT: the Bernoulli decoder on its transpose (EpiDecOutT) on 256 x 256 8-phase
-                                  // tiles (2) or 256 x 128 two-block tiles (1); 0: on hd W2 (EpiDecOut)
-    int bf_w2a = 0;               // VAEB_BF_W2A: 256-column tiles of dW2 forked after dhd (0: all), the rest in dW3's grid
     hipStream_t s2 = nullptr;     // DP: the gradient buckets' all-reduces and their Adagrad
     hipEvent_t dp_ev[3] = {};     // fork after dW2, bucket A reduced, bucket A updated
     bool dp_overlap = false;      // bucket A on s2 (bf16 engine; VAEB_DP_OVERLAP=0/1 overrides)
@@ -175,39 +173,16 @@ struct vaeb_ctx {
     // reducer workgroups of the LAST launch (kernels_aux.hpp LatRed) instead of a ticket and
     // a last-arriver reducer in the dhd launch.  VAEB_BWD_DEFER=0: the ticketed form.
     bool bwd_defer = true;
-    // encoder -> decoder at fan-in > 16: the encoder adds its [mu | lv] partials as no-return
-    // fixed-point atomics (latent.hpp fx_sum_add, HO 4) and every decoder workgroup reads its
-    // row block's exact sums (5 KB) instead of summing 16 slabs (40 KB; ZM 3 instead of 2);
-    // the dhd launch zeroes the sums.  VAEB_ENC_FX=1 (not the default: MNIST 34.4-34.5 us with
-    // the slabs against 34.8-35.1 with the sums -- the encoder launch +0.4 us, decout +0.2)
-    bool enc_fx = false;
     // the deferred dW2: dW2 (| dW6) + Adagrad of step t run in step t+1's encoder launch, on
     // the CUs the encoder leaves idle (latent.hpp enc_latent16_w2_kernel), so the dhd launch
     // holds the dhd tiles alone; host reads of the state flush a pending one first (w2_flush).
     // fp32 LB / LA, no communicator, 16-wave encoder, the latent backward deferred too (ho_dz 2:
     // dw2_deferred).  VAEB_DW2_DEFER=0: dW2 in the dhd launch.
     bool dw2_defer = true;
-    // the latent backward completed inside the dhd launch at MNIST's width (ho_dz 3,
-    // latent_bwd.hpp dhd2_dz_kernel): two dA1 column tiles per 1024-thread workgroup halve the
-    // contributors per latent element to ceil(H / 32) L <= 16, so the counted atomics apply and
-    // the last launch needs no reducers, counter or poll.  Measured and not the default
-    // (VAEB_DHD2=1 selects it; round 5, alternating 2000-step runs): 39.41 / 39.35 us per step
-    // against 34.44 / 34.42 -- the dhd launch 5.61 -> 10.87 us (two tiles per CU on 112 CUs,
-    // 72 k returning 64-bit adds), the last launch only 10.62 -> 10.2 us.
-    bool dhd2 = false;
     int* w2pend = nullptr;        // device: 1 = a step's dW2 is pending (set by its dhd launch)
     bool w2_dirty = false;        // host: a step was enqueued since the last flush
     bool w2_graph = false;        // host: the captured graphs hold deferred-dW2 steps (run_steps sets w2_dirty)
     int atomic_ho = 1;            // folded latent hand-offs: 1 by fan-in (ho_mode), 0 slabs
-    bool graph_upload = true;     // hipGraphUpload at capture (VAEB_GRAPH_UPLOAD=0: at first launch)
-    // the slab-only encoder on 1024-thread workgroups (16 waves splitting K: twice the loads in
-    // flight per CU): MNIST 38.82 -> 37.87 us/step in alternating runs (encoder 7.76 -> 7.22
-    // us).  VAEB_ENC16=0: 512 threads.
-    bool enc16 = true;
-    // the atomic hand-off encoder (HO 1, fan-in <= 16) on 16 waves too: Frey 29.19 -> 29.01
-    // us/step (encoder 6.98 -> 6.93 us).  VAEB_ENC16=1: the slab-only encoder only.
-    bool enc16_at = true;
-    int decout_ct = -1;           // Bernoulli decoder column tiles per workgroup: -1 auto (2), VAEB_DECOUT_CT=1
     int enc_red = -1;             // encoder slabs summed by the decoder launch: -1 auto, VAEB_ENC_RED=0|1
     // profiling
     hipEvent_t pev[kMaxProfKernels + 1] = {};
@@ -308,14 +283,8 @@ bool fused_latent(const vaeb_ctx* c) { return c->c.Z <= 32; }
 // MNIST-20, 64 -> 32 wide took the dW2 launch 11.7 -> 9.5 us and the dW3 | dW45 launch
 // 10.9 -> 8.1 us; 16 wide takes the latter to 7.5 us but the dW2 launch (beside 224 dhd
 // tiles) back up to 11.1 us.
-#ifndef VAEB_WTJ_P5
-#define VAEB_WTJ_P5 32
-#endif
-constexpr int kWTJ_P5 = VAEB_WTJ_P5;    // dW2 (| dW6), beside the dhd tiles
-#ifndef VAEB_W3_TS
-#define VAEB_W3_TS 1
-#endif
-constexpr int kW3TS = VAEB_W3_TS;       // 16-column groups per tile of the last launch (dW3 | dW45 | dW1)
+constexpr int kWTJ_P5 = 32;    // dW2 (| dW6), beside the dhd tiles (64 wide: 40.1 vs 38.8 us per step)
+constexpr int kW3TS = 1;       // 16-column groups per tile of the last launch (dW3 | dW45 | dW1; 2: 40.1 vs 38.8)
 constexpr int kWTJ_P67 = 16;   // dW1, beside the dz / dh phase
 constexpr int kWTJ_W = 16;     // standalone launches: dW3 | dW45 (+ ELBO), non-fused dW1
 constexpr int kDzSplit = 8;    // P67 column splits per row block (fused.hpp dz_dh_body)
@@ -341,12 +310,11 @@ int ho_mode(const vaeb_ctx* c, int fan_in) {
 }
 int ho_ml(const vaeb_ctx* c, int ct) { return ho_mode(c, cdiv(c->c.H, 16 * ct)); }
 bool dw2_deferrable(const vaeb_ctx* c);
-// backward: 1 atomic, 3 atomic on two-column-tile workgroups (where one-tile workgroups would
-// exceed the fan-in limit; vaeb_ctx::dhd2), else 2 (deferred to the last launch's reducers,
-// VAEB_BWD_DEFER) or 0 (ticket)
+// backward: 1 atomic, else 2 (deferred to the last launch's reducers, VAEB_BWD_DEFER) or 0
+// (ticket).  (Round 5's form 3 -- two dA1 column tiles per 1024-thread dhd workgroup so MNIST's
+// fan-in fits the counted atomics -- measured 39.4 vs 34.4 us per step and was removed in round 6.)
 int ho_dz(const vaeb_ctx* c) {
     const int m = ho_mode(c, cdiv(c->c.H, 16) * c->c.L);
-    if (m == 0 && c->dhd2 && c->atomic_ho && cdiv(c->c.H, 32) * c->c.L <= kFxMaxFanIn && dw2_deferrable(c)) return 3;
     return m == 0 && c->bwd_defer ? 2 : m;
 }
 
@@ -465,26 +433,21 @@ void launch_enc16_w2(hipStream_t s, dim3 g1, const StepArgs& a, const W2Launch& 
     }
 }
 
+// The slab-only encoder (HO 3: partials summed by the decoder launch, CT = 2, no FV) and the
+// atomic hand-off encoder (HO 1, one column tile, no FV) run on 1024-thread workgroups, 16
+// waves splitting K (twice the loads in flight per CU): MNIST 38.82 -> 37.87 us/step, Frey
+// 29.19 -> 29.01 in round 3's alternating runs (the 512-thread forms' switch, VAEB_ENC16, was
+// removed in round 6).  The ticketed reducer (HO 0) and the FV-stream encoder keep 512 threads.
 template <int HO>
-void launch_enc_latent(hipStream_t s, dim3 g1, const StepArgs& a, const FvFold& fvf, bool deep, int ct, bool e16,
-                       bool c16, const W2Launch* w2 = nullptr) {
-    if constexpr (HO >= 3) {   // partials read by the decoder launch (3 slabs, 4 fixed-point sums): CT = 2, no FV
-        if (e16) {   // 1024-thread workgroups, 16 waves splitting K (vaeb_ctx::enc16)
-            if (w2) { launch_enc16_w2<HO, 2>(s, g1, a, *w2); return; }
-            if (a.Z <= 16) hipLaunchKernelGGL((enc_latent16_kernel<1, 4, HO, 2>), g1, dim3(1024), 0, s, a);
-            else hipLaunchKernelGGL((enc_latent16_kernel<2, 4, HO, 2>), g1, dim3(1024), 0, s, a);
-            return;
-        }
-        if (a.Z <= 16) {
-            if (deep) hipLaunchKernelGGL((enc_latent_kernel<1, 8, HO, 2>), g1, dim3(512), 0, s, a);
-            else hipLaunchKernelGGL((enc_latent_kernel<1, 4, HO, 2>), g1, dim3(512), 0, s, a);
-        } else {
-            if (deep) hipLaunchKernelGGL((enc_latent_kernel<2, 8, HO, 2>), g1, dim3(512), 0, s, a);
-            else hipLaunchKernelGGL((enc_latent_kernel<2, 4, HO, 2>), g1, dim3(512), 0, s, a);
-        }
+void launch_enc_latent(hipStream_t s, dim3 g1, const StepArgs& a, const FvFold& fvf, bool deep, int ct,
+                       const W2Launch* w2 = nullptr) {
+    if constexpr (HO == 3) {
+        if (w2) { launch_enc16_w2<HO, 2>(s, g1, a, *w2); return; }
+        if (a.Z <= 16) hipLaunchKernelGGL((enc_latent16_kernel<1, 4, HO, 2>), g1, dim3(1024), 0, s, a);
+        else hipLaunchKernelGGL((enc_latent16_kernel<2, 4, HO, 2>), g1, dim3(1024), 0, s, a);
         return;
     }
-    if (HO == 1 && e16 && c16 && fvf.rows == 0 && ct == 1) {   // the atomic hand-off on 16 waves
+    if (HO == 1 && fvf.rows == 0 && ct == 1) {   // the atomic hand-off on 16 waves
         if constexpr (HO == 1) if (w2) { launch_enc16_w2<1, 1>(s, g1, a, *w2); return; }
         if (a.Z <= 16) hipLaunchKernelGGL((enc_latent16_kernel<1, 4, 1, 1>), g1, dim3(1024), 0, s, a);
         else hipLaunchKernelGGL((enc_latent16_kernel<2, 4, 1, 1>), g1, dim3(1024), 0, s, a);
@@ -507,11 +470,13 @@ bool folded_latent(const vaeb_ctx* c, const StepArgs& a) {
 bool enc_form(const vaeb_ctx* c, const StepArgs& a, const FvFold& fvf, int* ho_out, int* ct_out, bool* red_out) {
     const bool red = (c->enc_red < 0 ? ho_ml(c, 1) == 0 : c->enc_red == 1) && fvf.rows == 0 && cdiv(a.H, 32) <= 32;
     const int ct = (red || fvf.rows > 0) ? 2 : 1;
-    const int ho = red ? (c->enc_fx && c->fold_bwd ? 4 : 3) : ho_ml(c, ct);   // (the fold's dhd launch zeroes HO 4's sums)
+    // (round 4's HO 4 -- the [mu | lv] partials as exact fixed-point sums read by the decoder,
+    // VAEB_ENC_FX -- measured 34.8-35.1 vs 34.4-34.5 us per step and was removed in round 6)
+    const int ho = red ? 3 : ho_ml(c, ct);
     if (ho_out) *ho_out = ho;
     if (ct_out) *ct_out = ct;
     if (red_out) *red_out = red;
-    return (ho >= 3 && c->enc16) || (ho == 1 && c->enc16 && c->enc16_at && fvf.rows == 0 && ct == 1);
+    return ho == 3 || (ho == 1 && fvf.rows == 0 && ct == 1);
 }
 
 int enqueue_forward(vaeb_ctx* c, const StepArgs& a0, Prof& pr, const FvFold& fvf = FvFold{},
@@ -533,29 +498,27 @@ int enqueue_forward(vaeb_ctx* c, const StepArgs& a0, Prof& pr, const FvFold& fvf
         enc_form(c, a, fvf, &ho, &ct, &red);
         const dim3 g1(a.Mbp / 16, cdiv(a.H, 16 * ct) + fvf.rows);
         const bool deep = cdiv(cdiv(a.D, 16), 8) > 4;
-        const int at = red ? (ho == 4 ? 3 : 2) : (ho == 1 ? 1 : 0);
+        const int at = red ? 2 : (ho == 1 ? 1 : 0);
         pr.mark(w2 ? 42 : 16);
         REP(pr) {
-            if (ho == 4) launch_enc_latent<4>(s, g1, a, fvf, deep, ct, c->enc16, c->enc16_at, w2);
-            else if (ho == 3) launch_enc_latent<3>(s, g1, a, fvf, deep, ct, c->enc16, c->enc16_at, w2);
-            else if (ho == 1) launch_enc_latent<1>(s, g1, a, fvf, deep, ct, c->enc16, c->enc16_at, w2);
-            else launch_enc_latent<0>(s, g1, a, fvf, deep, ct, c->enc16, c->enc16_at);
+            if (ho == 3) launch_enc_latent<3>(s, g1, a, fvf, deep, ct, w2);
+            else if (ho == 1) launch_enc_latent<1>(s, g1, a, fvf, deep, ct, w2);
+            else launch_enc_latent<0>(s, g1, a, fvf, deep, ct);
         }
         CHECK_LAUNCH();
         a.dbg = next_dbg(c);
-        // Bernoulli: two 16-column tiles per workgroup (decout_z2_kernel)
-        const int dct = (!gaussian(c) && c->decout_ct != 1) ? 2 : 1;
+        // Bernoulli: two 16-column tiles per workgroup (decout_z2_kernel; one tile: 42.0 vs
+        // 39.4 us per step in round 3, its switch VAEB_DECOUT_CT removed in round 6)
+        const int dct = gaussian(c) ? 1 : 2;
         const dim3 g4(a.Me / 16, cdiv(a.D, 16 * dct));
         pr.mark(17);
         REP(pr) {
             if (gaussian(c)) {
-                if (at == 3) launch_decout_z<2, 3>(s, g4, a);
-                else if (at == 2) launch_decout_z<2, 2>(s, g4, a);
+                if (at == 2) launch_decout_z<2, 2>(s, g4, a);
                 else if (at == 1) launch_decout_z<2, 1>(s, g4, a);
                 else launch_decout_z<2, 0>(s, g4, a);
             } else {
-                if (at == 3) launch_decout_z<1, 3>(s, g4, a, dct);
-                else if (at == 2) launch_decout_z<1, 2>(s, g4, a, dct);
+                if (at == 2) launch_decout_z<1, 2>(s, g4, a, dct);
                 else if (at == 1) launch_decout_z<1, 1>(s, g4, a, dct);
                 else launch_decout_z<1, 0>(s, g4, a, dct);
             }
@@ -733,7 +696,6 @@ int w2_args(vaeb_ctx* c, const StepArgs& a, const OptArgs& opt, int base, WGradA
 // dW2 tiles bound the dhd launch.  With the counted atomic backward (small fan-in: Frey) the dhd
 // launch is bound by that hand-off and hides dW2, while the encoder would pay for it: Frey
 // 29.78 / 29.87 µs in-step vs 31.54 / 31.55 deferred.
-// (ho_dz 3 carries no dW2 tiles of its own: it is chosen only where the deferral applies)
 bool dw2_deferrable(const vaeb_ctx* c) {
     const int est = c->c.estimator;
     StepArgs a{};
@@ -743,7 +705,7 @@ bool dw2_deferrable(const vaeb_ctx* c) {
 }
 bool dw2_deferred(const vaeb_ctx* c, const StepArgs& a) {
     const int hd = ho_dz(c);
-    return dw2_deferrable(c) && (hd == 2 || hd == 3) && folded_latent(c, a);
+    return dw2_deferrable(c) && hd == 2 && folded_latent(c, a);
 }
 
 // Run the pending step's dW2 (| dW6) + Adagrad now (their own launch; the device flag makes it
@@ -831,6 +793,18 @@ DpRange dp_foreign_range(const vaeb_ctx* c, const DpBucket& bk) {
         if (c->rank < c->world - 1) { r.lo[k] = bk.lo[j] + (c->rank + 1) * S; r.n[k++] = (c->world - c->rank - 1) * S; }
     }
     return r;
+}
+
+// The fp32 engine's DP optimizer launch over range r (prior + Adagrad; r.book: also the SGVB
+// bookkeeping): the step's dp_opt, and what vaeb_dp_rank_update runs for one emulated rank.
+int dp_opt_launch(vaeb_ctx* c, hipStream_t st, const OptArgs& o, const DpRange& r, const ElboArgs& e) {
+    int64_t n = 0;
+    for (int k = 0; k < kDpRuns; ++k) n += r.n[k];
+    // (sharded: a 1/W share of the arena; the grid scales down with it)
+    const int nb = (int)std::max<int64_t>(1, std::min<int64_t>(r.book ? 512 : 256, cdiv(n, 256 * 8)));
+    hipLaunchKernelGGL(adagrad_kernel, dim3(nb), dim3(256), 0, st, o, c->P, r, e);
+    CHECK_LAUNCH();
+    return 0;
 }
 
 int nccl_ok(ncclResult_t r, const char* what) {
@@ -1015,14 +989,7 @@ int enqueue_train_step(vaeb_ctx* c, int par, bool prof, bool fresh = true, int d
     const int bo = gaussian(c) ? 6 : 5;
     const bool gs = gaussian(c);
     const OptArgs dopt = make_opt(c, par, true, false);
-    auto dp_opt = [&](hipStream_t st, const DpRange& r) -> int {
-        // (sharded: a 1/W share of the arena; the grid scales down with it)
-        const int64_t n = [&] { int64_t t = 0; for (int k = 0; k < kDpRuns; ++k) t += r.n[k]; return t; }();
-        const int nb = (int)std::max<int64_t>(1, std::min<int64_t>(r.book ? 512 : 256, cdiv(n, 256 * 8)));
-        hipLaunchKernelGGL(adagrad_kernel, dim3(nb), dim3(256), 0, st, dopt, c->P, r, e);
-        CHECK_LAUNCH();
-        return 0;
-    };
+    auto dp_opt = [&](hipStream_t st, const DpRange& r) -> int { return dp_opt_launch(c, st, dopt, r, e); };
 
     // folded latent backward (Z <= 32, latent_bwd.hpp): the dhd launch also finishes dZ and
     // [dMu | dLv]; dA3 is formed inside the dW3 workgroups of the last launch (with dW1)
@@ -1040,34 +1007,15 @@ int enqueue_train_step(vaeb_ctx* c, int par, bool prof, bool fresh = true, int d
         if (int rc = prep_wgrad(c, &g4, 1, opt, nullptr, a, ntile, w, vec, kWTJ_P5)) return rc;
         // the dhd loaders' 16-byte form needs D % 4 == 0 and aligned dA2 / W2 too
         vec = vec && dhd_vec(a);
-        DhdAux pend{nullptr, nullptr, 0};
+        DhdAux pend{nullptr};
         if (w2d) {   // no dW2 tiles here: the next step's encoder launch (or a flush) runs them
             w.total_wgs = ntile;
             pend.pend = c->w2pend;
         }
-        int eho;
-        enc_form(c, a, FvFold{}, &eho, nullptr, nullptr);
-        if (eho == 4) {   // the encoder's fixed-point [mu | lv] sums, consumed by the decoder: zero them
-            pend.zero = c->acc_ml;
-            pend.nzero = a.Mbp * 2 * a.Z;
-        }
         const dim3 grid(w.total_wgs);
         const bool deep = cdiv(cdiv(p5.K, 16), 8) > 4;
         pr.mark(w2d ? 43 : 39);
-        if (ho_dz(c) == 3) {
-            // two column tiles per 1024-thread workgroup, the counted atomic latent backward
-            if (!w2d) return fail(VAEB_ERR_ARG, "internal: the two-tile dhd launch needs the deferred dW2");
-            const int nt2 = gx * cdiv(p5.N, 32);
-            REP(pr) {
-                if (a.Z <= 16) {
-                    if (vec) hipLaunchKernelGGL((dhd2_dz_kernel<1, 4, true>), dim3(nt2), dim3(1024), 0, s, p5, nt2, gx, pend);
-                    else hipLaunchKernelGGL((dhd2_dz_kernel<1, 4, false>), dim3(nt2), dim3(1024), 0, s, p5s, nt2, gx, pend);
-                } else {
-                    if (vec) hipLaunchKernelGGL((dhd2_dz_kernel<2, 4, true>), dim3(nt2), dim3(1024), 0, s, p5, nt2, gx, pend);
-                    else hipLaunchKernelGGL((dhd2_dz_kernel<2, 4, false>), dim3(nt2), dim3(1024), 0, s, p5s, nt2, gx, pend);
-                }
-            }
-        } else REP(pr) {
+        REP(pr) {
             switch (ho_dz(c)) {
                 case 1: launch_dhd_dz<kWTJ_P5 / 16, 1>(s, grid, p5, p5s, w, ntile, gx, vec, deep, pend); break;
                 case 2: launch_dhd_dz<kWTJ_P5 / 16, 2>(s, grid, p5, p5s, w, ntile, gx, vec, deep, pend); break;
@@ -1215,7 +1163,7 @@ int capture(vaeb_ctx* c, int nsteps, int par, hipGraphExec_t* out) {
     if (e != hipSuccess) return fail(VAEB_ERR_HIP, "hipGraphInstantiate: %s", hipGetErrorString(e));
     // upload now, with the capture: a graph's first launch otherwise pays it inside the call
     // that replays it (the driver's 20-step form replays a graph the warm-up never launched)
-    if (c->graph_upload && hipGraphUpload(*out, c->s) != hipSuccess) (void)hipGetLastError();
+    if (hipGraphUpload(*out, c->s) != hipSuccess) (void)hipGetLastError();
     return 0;
 }
 
@@ -1349,29 +1297,17 @@ int vaeb_create(const vaeb_config* cfg, vaeb_ctx** out) {
     hipError_t e = hipSetDevice(g.device);
     if (e != hipSuccess) { delete c; return fail(VAEB_ERR_HIP, "hipSetDevice(%d): %s", g.device, hipGetErrorString(e)); }
     e = hipStreamCreateWithFlags(&c->s, hipStreamNonBlocking);
+    // Runtime switches (read here only; each alternative is a product path elsewhere or the
+    // independent form an agreement test compares the default against -- DESIGN.md 4.4)
     if (const char* fb = getenv("VAEB_FOLD_BWD")) c->fold_bwd = atoi(fb) != 0;
     if (const char* bd = getenv("VAEB_BWD_DEFER")) c->bwd_defer = atoi(bd) != 0;
-    if (const char* ef = getenv("VAEB_ENC_FX")) c->enc_fx = atoi(ef) != 0;
     if (const char* wd = getenv("VAEB_DW2_DEFER")) c->dw2_defer = atoi(wd) != 0;
-    if (const char* d2 = getenv("VAEB_DHD2")) c->dhd2 = atoi(d2) != 0;
-    if (const char* bk = getenv("VAEB_BF_FORK")) c->bf_fork = atoi(bk) != 0;
-    if (const char* b2 = getenv("VAEB_BF_SPLIT2")) c->bf_split2 = atoi(b2) != 0;
-    if (const char* sk = getenv("VAEB_BF_SMALLK")) c->bf_smallk = atoi(sk) & 3;
-    if (const char* dt = getenv("VAEB_BF_DECT")) c->bf_dect = std::min(2, std::max(0, atoi(dt)));
-    if (const char* tt = getenv("VAEB_BF_DTT")) c->bf_dtt = atoi(tt) != 0;
-    if (const char* zf = getenv("VAEB_BF_DZFUSE")) c->bf_dzfuse = atoi(zf) != 0;
-    if (const char* em = getenv("VAEB_BF_ELBOMAIN")) c->bf_elbomain = atoi(em) != 0;
-    if (const char* wa = getenv("VAEB_BF_W2A")) c->bf_w2a = std::max(0, atoi(wa));
-    if (const char* fp = getenv("VAEB_BF_FORKPT")) c->bf_forkpt = std::min(3, std::max(0, atoi(fp)));
-    if (const char* bt = getenv("VAEB_BF_THIN")) c->bf_thin = atoi(bt) & 3;
     if (const char* ah = getenv("VAEB_ATOMIC_HO")) c->atomic_ho = atoi(ah) != 0 ? 1 : 0;
     if (const char* er = getenv("VAEB_ENC_RED")) c->enc_red = atoi(er) != 0 ? 1 : 0;
-    if (const char* dc = getenv("VAEB_DECOUT_CT")) c->decout_ct = atoi(dc) == 1 ? 1 : 2;
-    if (const char* e16 = getenv("VAEB_ENC16")) {
-        c->enc16 = atoi(e16) != 0;
-        c->enc16_at = atoi(e16) >= 2;
-    }
-    if (const char* gu = getenv("VAEB_GRAPH_UPLOAD")) c->graph_upload = atoi(gu) != 0;
+    if (const char* bk = getenv("VAEB_BF_FORK")) c->bf_fork = atoi(bk) != 0;
+    if (const char* tt = getenv("VAEB_BF_DTT")) c->bf_dtt = atoi(tt) != 0;
+    if (const char* zf = getenv("VAEB_BF_DZFUSE")) c->bf_dzfuse = atoi(zf) != 0;
+    if (const char* bt = getenv("VAEB_BF_THIN")) c->bf_thin = atoi(bt) & 3;
     {
         const char* g8 = getenv("VAEB_BF_GEMM8");
         // default: the 8-phase loop for KC x KC (dhd), KC x KO (enc) and, since round 5, KO x KO
@@ -1917,9 +1853,13 @@ struct FileCloser { FILE* f; ~FileCloser() { if (f) fclose(f); } };
 
 int vaeb_checkpoint_save(vaeb_ctx* c, const char* path) {
     if (!c) return fail(VAEB_ERR_ARG, "null argument");
+    // path NULL: a non-writing rank of a multi-rank communicator joining the gather;
+    // anywhere else it is a caller error, reported before anything runs
+    if (!path && !(c->comm && c->world > 1))
+        return fail(VAEB_ERR_ARG, "checkpoint: null path (only a non-writing rank of a multi-rank communicator passes NULL)");
     if (int rc = w2_flush(c)) return rc;   // a pending deferred dW2 (vaeb_ctx::dw2_defer)
     if (int rc = dp_gather_acc(c)) return rc;   // sharded DP: the whole Adagrad state (every rank calls)
-    if (!path) return 0;   // a non-writing rank: it joined the gather
+    if (!path) return 0;
     const vaeb_config& g = c->c;
     CkptHeader h{};
     memcpy(h.magic, kCkptMagic, 8);
@@ -2145,7 +2085,7 @@ int vaeb_get_activation(vaeb_ctx* c, const char* name, float* out, int64_t n) {
     if (!c || !name || !out) return fail(VAEB_ERR_ARG, "null argument");
     float* ptrs[] = {c->h, c->mu, c->lv, c->eps, c->z, c->hd, c->dA2, c->dA6, c->dA1, c->dZ, c->dMuLv, c->dA3, c->y,
                      c->kl_part, c->lp_part};
-    if (strcmp(name, "dZ") == 0 && fused_latent(c) && c->fold_bwd && !is_bf16(c) && (ho_dz(c) == 1 || ho_dz(c) == 3))
+    if (strcmp(name, "dZ") == 0 && fused_latent(c) && c->fold_bwd && !is_bf16(c) && ho_dz(c) == 1)
         return fail(VAEB_ERR_STATE, "dZ is not stored by the atomic latent hand-off (fan-in <= 16, latent_bwd.hpp): "
                                     "create the context with VAEB_ATOMIC_HO=0 to read it");
     const int64_t R = c->cap, RL = (int64_t)c->cap * c->c.L, D = c->c.D, H = c->c.H, Z = c->c.Z;
@@ -2467,6 +2407,88 @@ int vaeb_dp_plan(const vaeb_config* cfg, int32_t world, int32_t rank, int32_t sh
     put(o, own, out_nown);
     if (out_book) *out_book = o.book;
     put(dp_foreign_range(&c, bk), foreign, out_nforeign);
+    return 0;
+}
+
+}  // extern "C"
+
+// vaeb_dp_rank_update's body, with the context's (world, rank, dp_shard) already set to the
+// emulated rank's: the reduce-scatter's result uploaded, this rank's optimizer launch, the
+// all-gather's result uploaded, the bf16 shadow fix -- dp_reduce_update with its collectives
+// replaced by host copies, the kernels and index ranges unchanged.
+static int dp_rank_update_body(vaeb_ctx* c, int bucket, const float* gsum, const float* thg) {
+    const int par = c->par;
+    hipStream_t s = c->s;
+    const bool bf = is_bf16(c);
+    const DpBucket bk = bucket == 0 ? dp_bucket_a_runs(c) : bucket == 1 ? dp_bucket_b_runs(c) : dp_bucket_all_runs(c);
+    DpRange own = dp_opt_range(c, bk);
+    own.book = 0;   // the SGVB bookkeeping (value, epoch sums, cursor, step) is not emulated
+    const DpRange fr = dp_foreign_range(c, bk);
+    // a step's first bucket (A, or all): the out arena -- theta' and the bf16 shadow -- NaN first,
+    // so every element the step leaves there was written by it
+    if (bucket != 1) {
+        HIP_TRY(hipMemsetAsync(c->theta2[par ^ 1], 0xff, sizeof(float) * (size_t)c->P, s));
+        if (bf) HIP_TRY(hipMemsetAsync(c->bf.shadow2[par ^ 1], 0xff, sizeof(bf16_t) * (size_t)c->bf.S, s));
+    }
+    // the reduce-scatter (+ all-reduce of the remainders): this rank's destinations hold the sum;
+    // every other gradient element is NaN (the optimizer must not read it)
+    HIP_TRY(hipMemsetAsync(c->grad, 0xff, sizeof(float) * (size_t)(c->P + 1), s));
+    for (int k = 0; k < kDpRuns; ++k)
+        if (own.n[k])
+            HIP_TRY(hipMemcpyAsync(c->grad + own.lo[k], gsum + own.lo[k], sizeof(float) * (size_t)own.n[k],
+                                   hipMemcpyHostToDevice, s));
+    const OptArgs o32 = make_opt(c, par, true, false);
+    const bf::Opt o16 = bf ? bf_opt(c, par, true, false) : bf::Opt{};
+    if (int rc = bf ? bf_dp_opt_launch(c, s, o16, own, ElboArgs{}) : dp_opt_launch(c, s, o32, own, ElboArgs{})) return rc;
+    if (thg) {
+        // the all-gather: the other ranks' theta' shards into the out arena, then their shadow
+        for (int k = 0; k < kDpRuns; ++k)
+            if (fr.n[k])
+                HIP_TRY(hipMemcpyAsync(c->theta2[par ^ 1] + fr.lo[k], thg + fr.lo[k], sizeof(float) * (size_t)fr.n[k],
+                                       hipMemcpyHostToDevice, s));
+        if (bf) if (int rc = bf_dp_fix_launch(c, s, o16, fr)) return rc;
+    }
+    HIP_TRY(hipStreamSynchronize(s));
+    return 0;
+}
+
+extern "C" {
+
+int vaeb_dp_rank_update(vaeb_ctx* c, int32_t world, int32_t rank, int32_t bucket, const float* grad_sum,
+                        int64_t n_grad, const float* theta_gathered, int32_t finish) {
+    if (!c || !grad_sum || world <= 0 || world > 64 || rank < 0 || rank >= world || bucket < 0 || bucket > 2)
+        return fail(VAEB_ERR_ARG, "bad dp_rank_update arguments");
+    if (c->comm) return fail(VAEB_ERR_STATE, "vaeb_dp_rank_update emulates the collectives: use a context without a communicator");
+    if (c->c.estimator == VAEB_EST_FV || c->c.estimator == VAEB_EST_FVS)
+        return fail(VAEB_ERR_STATE, "the FV estimators have no data-parallel optimizer");
+    if (n_grad != c->P + 1) return fail(VAEB_ERR_ARG, "size mismatch: got %lld, expected %lld", (long long)n_grad, (long long)(c->P + 1));
+    if (int rc = w2_flush(c)) return rc;
+    HIP_TRY(hipStreamSynchronize(c->s));
+    const int w0 = c->world, r0 = c->rank;
+    const bool s0 = c->dp_shard;
+    c->world = world; c->rank = rank; c->dp_shard = world > 1;
+    const int rc = dp_rank_update_body(c, bucket, grad_sum, theta_gathered);
+    c->world = w0; c->rank = r0; c->dp_shard = s0;
+    if (rc) return rc;
+    if (finish) c->par ^= 1;
+    return 0;
+}
+
+int vaeb_get_shadow(vaeb_ctx* c, uint16_t* out, int64_t n) {
+    if (!c || !out) return fail(VAEB_ERR_ARG, "null argument");
+    if (!is_bf16(c)) return fail(VAEB_ERR_STATE, "only the bf16 engine keeps a shadow arena");
+    const int64_t nw = c->bf.smap.nweights;
+    if (n != nw) return fail(VAEB_ERR_ARG, "size mismatch: got %lld, expected %lld", (long long)n, (long long)nw);
+    if (int rc = w2_flush(c)) return rc;
+    bf16_t* tmp = nullptr;
+    if (int rc = dalloc(&tmp, (size_t)nw)) return rc;
+    hipLaunchKernelGGL(bf::shadow_gather_kernel, dim3(1024), dim3(256), 0, c->s, (const bf16_t*)c->bf.shadow2[c->par], tmp,
+                       c->bf.smap);
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess) e = hipStreamSynchronize(c->s);
+    if (e == hipSuccess) e = hipMemcpy(out, tmp, sizeof(bf16_t) * (size_t)nw, hipMemcpyDeviceToHost);
+    hipFree(tmp);
+    if (e != hipSuccess) return fail(VAEB_ERR_HIP, "vaeb_get_shadow: %s", hipGetErrorString(e));
     return 0;
 }
 

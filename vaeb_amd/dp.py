@@ -57,7 +57,9 @@ def spawn_ranks(n, cmd, poll_s=0.2, env_extra=None, straggler_s=None):
     returns the first non-zero exit code, else 0.  Once any rank has exited 0 the others get
     `straggler_s` seconds (VAEB_RANK_DEADLINE_S, default 600) to follow: a rank left alone in a
     collective would otherwise hold the launcher forever.  Past it they are killed, the
-    still-running ranks are named on stderr, and the code is RANK_HUNG."""
+    still-running ranks are named on stderr, and the code is RANK_HUNG.  (cli.train_model ends
+    with a barrier of all ranks after rank 0's lead-only work -- the .mdl, the trace -- so healthy
+    ranks exit together and the deadline never runs against that tail.)"""
     if straggler_s is None:
         straggler_s = float(os.environ.get("VAEB_RANK_DEADLINE_S", "600"))
     port = free_port()
