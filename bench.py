@@ -287,6 +287,9 @@ def spawn_ranks(n, argv, poll_s=0.2, script=None):
     return _spawn(n, [sys.executable, script or os.path.abspath(__file__)] + list(argv), poll_s=poll_s)
 
 
+DTYPES = {"f32": 0, "bf16": 1, "fp16": 2}   # vaeb_dtype (include/vaeb_hip.h)
+
+
 def make_context(C, D, H, Z, B, Bg, row_off, local, args, gauss, bf16, dist, rank, world):
     """One library context (and, with world > 1, its RCCL communicator; the 128-byte id
     travels over the gloo group)."""
@@ -295,7 +298,7 @@ def make_context(C, D, H, Z, B, Bg, row_off, local, args, gauss, bf16, dist, ran
                        decoder=_lib.DEC_GAUSSIAN if gauss else _lib.DEC_BERNOULLI,
                        estimator={"FV": _lib.EST_FV, "FVS": _lib.EST_FVS}.get(C.get("estimator"), _lib.EST_LB),
                        use_graph=not args.no_graph, max_eval_rows=B if bf16 else 1000,
-                       dtype=_lib.DTYPE_BF16 if bf16 else _lib.DTYPE_F32)
+                       dtype=DTYPES[C["dtype"]])
     if world > 1:
         from vaeb_amd.dp import comm_setup
         comm_setup(ctx, dist, rank, world)
@@ -399,12 +402,19 @@ def main(argv=None):
     ap.add_argument("--scaling", choices=["weak", "strong"], default="weak",
                     help="weak: B rows per GPU (default); strong: one B-row global minibatch split "
                          "contiguously over the ranks (100 over 8 = 13,13,13,13,12,12,12,12; SURVEY 8(e))")
+    ap.add_argument("--dtype", choices=sorted(DTYPES), default=None,
+                    help="operand type (default: the config's; synth: bf16).  fp16 runs config 5 on "
+                         "v_mfma_f32_16x16x32_f16 as BASELINE.json names it (DESIGN.md 4.2)")
     argv = sys.argv[1:] if argv is None else list(argv)
     args = ap.parse_args(argv)
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         # no launcher: one process per GPU, started here before any GPU call
         sys.exit(spawn_ranks(args.gpus, argv))
     C = CONFIGS[args.config]
+    if args.dtype and args.dtype != C["dtype"]:
+        C = dict(C, dtype=args.dtype)
+        for k in ("metric", "workload"):
+            C[k] = C[k].replace("bf16", args.dtype)
     steps = args.steps if args.steps is not None else C["steps"]
     warmup = args.warmup if args.warmup is not None else C["warmup"]
 
@@ -426,7 +436,7 @@ def main(argv=None):
     Bn = args.batch if args.batch is not None else C["B"]
     B, row_off, Bg = row_split(Bn, world, rank, args.scaling)
     N = max(C["N"], 4 * Bg)
-    bf16 = C["dtype"] == "bf16"
+    bf16 = C["dtype"] in ("bf16", "fp16")   # the 16-bit engine
     gauss = C.get("continuous", False)
     if bf16:
         x = synth_like(N, D=D)             # synth x ~ Bernoulli(0.5)

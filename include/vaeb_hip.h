@@ -35,8 +35,12 @@ enum vaeb_objective { VAEB_OBJ_SUM_PRIOR = 0,                             /* VAE
                       VAEB_OBJ_MEAN_MAP = 1 };                            /* VAEBfullbayes.py:142,183 */
 enum vaeb_eps_mode  { VAEB_EPS_PHILOX = 0, VAEB_EPS_HOST = 1 };
 enum vaeb_dtype     { VAEB_DTYPE_F32 = 0,      /* fp32 MFMA, the reference's floatX (run_on_gpu.sh:2) */
-                      VAEB_DTYPE_BF16 = 1 };   /* bf16 MFMA operands, fp32 accumulation and fp32
+                      VAEB_DTYPE_BF16 = 1,     /* bf16 MFMA operands, fp32 accumulation and fp32
                                                   master weights / Adagrad state (BASELINE config 5) */
+                      VAEB_DTYPE_F16 = 2 };    /* fp16 MFMA operands ("fp16 MFMA", BASELINE config 5),
+                                                  the same engine and fp32 state; the mean objective's
+                                                  backward carries its 16-bit data gradients scaled by
+                                                  a power of two ~ B_global (undone in fp32) */
 enum vaeb_status    { VAEB_OK = 0, VAEB_ERR_ARG = -1, VAEB_ERR_HIP = -2, VAEB_ERR_STATE = -3,
                       VAEB_ERR_COMM = -4, VAEB_ERR_NOMEM = -5,
                       VAEB_ERR_NUMERIC = -6 };  /* a step's values left the fixed-point latent hand-off's

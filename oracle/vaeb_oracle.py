@@ -127,6 +127,24 @@ def _unpack(params, cfg):
     return d
 
 
+def fp16_round(a):
+    """Round to the nearest IEEE binary16 (ties to even, gradual underflow), returned in a's
+    dtype: the storage rounding of the 16-bit engine's fp16 instantiation
+    (vaeb_amd/csrc/gemm_bf16.hpp f2bf with VAEB_H16_F16, v_cvt_f16_f32)."""
+    a = np.asarray(a)
+    return a.astype(np.float32).astype(np.float16).astype(a.dtype)
+
+
+def fp16_round_scaled(S):
+    """fp16 storage of values carried scaled by the power of two S (the fp16 engine's loss
+    scale for the mean objective, engine_bf16.inc h16_scale): round(a S) / S -- the same bits
+    as fp16_round for normal values, without its underflow below 6.1e-5 / S."""
+    def q(a):
+        a = np.asarray(a)
+        return (fp16_round(a.astype(np.float64) * S) / S).astype(a.dtype)
+    return q
+
+
 def bf16_round(a):
     """Round to the nearest bfloat16 (ties to even), returned in a's dtype: the storage
     rounding of the bf16 engine (vaeb_amd/csrc/gemm_bf16.hpp f2bf)."""

@@ -215,8 +215,11 @@ def test_cli_dtype_key(tmp_path, monkeypatch):
     c, _, _, _, _ = _run(ARGV)
     assert c["dtype"] == _lib.DTYPE_F32
     assert dtype_name("float32") == "float32" and dtype_name("bfloat16") == "bf16"
+    assert dtype_name("float16") == "fp16" and dtype_name("half") == "fp16"
+    c, _, _, _, out = _run(ARGV + ['--dtype', 'float16'])
+    assert c["dtype"] == _lib.DTYPE_F16
     with pytest.raises(ValueError):
-        dtype_name("float16")
+        dtype_name("int8")
 
 
 def test_cli_world_size_must_match_the_launcher(monkeypatch):

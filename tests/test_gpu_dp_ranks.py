@@ -33,6 +33,7 @@ CASES = {
     "frey_gauss_fp32": (560, 200, 2, True, "f32", 0),
     "bf16_bern": (512, 264, 40, False, "bf16", 0),
     "bf16_gauss": (512, 264, 40, True, "bf16", 0),
+    "fp16_bern": (512, 264, 40, False, "fp16", 0),
     "mnist_fp32_mean_map": (784, 500, 20, False, "f32", 1),
 }
 
@@ -40,6 +41,11 @@ CASES = {
 def bf16_bits(x):
     """bf16 bits of float32 x, round to nearest even (O.bf16_round, whose low 16 bits are 0)."""
     return (O.bf16_round(np.asarray(x, np.float32)).view(np.uint32) >> 16).astype(np.uint16)
+
+
+def fp16_bits(x):
+    """IEEE binary16 bits of float32 x, round to nearest even."""
+    return np.asarray(x, np.float32).astype(np.float16).view(np.uint16)
 
 
 def run_rank(ctx, world, rank, buckets, gsum, theta0, acc0, thg, n_w):
@@ -72,7 +78,7 @@ def case(request):
     from vaeb_amd import _lib
     D, H, Z, gauss, dt, obj = CASES[request.param]
     ctx = _lib.Context(D, H, Z, 64, decoder=_lib.DEC_GAUSSIAN if gauss else _lib.DEC_BERNOULLI, objective=obj,
-                       max_eval_rows=64, dtype=_lib.DTYPE_BF16 if dt == "bf16" else _lib.DTYPE_F32)
+                       max_eval_rows=64, dtype={"f32": _lib.DTYPE_F32, "bf16": _lib.DTYPE_BF16, "fp16": _lib.DTYPE_F16}[dt])
     P = ctx.P
     rng = np.random.default_rng(D + H + Z + 7 * gauss + 3 * obj)
     theta0 = (0.01 * rng.standard_normal(P)).astype(np.float32)
@@ -82,11 +88,11 @@ def case(request):
     plan_all = _lib.dp_plan(D, H, Z, 1, 0, bucket=2, sharded=False,
                             decoder=_lib.DEC_GAUSSIAN if gauss else _lib.DEC_BERNOULLI)
     n_w = 0
-    if dt == "bf16":
+    if dt in ("bf16", "fp16"):
         # the weight elements: the arena before the biases (b3 is the first bias)
         n_w = P - (H + 2 * Z + H + D + (D if gauss else 0))
     yield dict(ctx=ctx, D=D, H=H, Z=Z, gauss=gauss, obj=obj, P=P, theta0=theta0, acc0=acc0, gsum=gsum, n_w=n_w,
-               P_plan=plan_all["P"])
+               P_plan=plan_all["P"], bits=fp16_bits if dt == "fp16" else bf16_bits)
     ctx.close()
 
 
@@ -108,7 +114,7 @@ def test_replicated_update_is_the_reference_adagrad(case):
     assert np.abs(ac - a).max() <= 1e-6 * np.abs(a).max()
     assert np.all(np.abs(th - want) <= 1e-7 + 2e-6 * np.abs(want)), float(np.abs(th - want).max())
     if sh is not None:
-        assert np.array_equal(sh, bf16_bits(th[:c["n_w"]]))
+        assert np.array_equal(sh, c["bits"](th[:c["n_w"]]))
 
 
 @pytest.mark.parametrize("world", [2, 3, 8])
@@ -153,7 +159,7 @@ def test_sharded_ranks_compose_to_the_replicated_update(case, world, form):
         th, ac, sh = run_rank(ctx, world, r, buckets, c["gsum"], c["theta0"], c["acc0"], th_g, n_w)
         assert np.array_equal(th, th_rep), f"rank {r}: theta' after the all-gather differs"
         if n_w:
-            want = bf16_bits(th_rep[:n_w])
+            want = c["bits"](th_rep[:n_w])
             bad = np.flatnonzero(sh != want)
             assert bad.size == 0, f"rank {r}: {bad.size} shadow entries differ, first at {bad[:5]}"
 

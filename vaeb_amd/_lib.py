@@ -21,7 +21,7 @@ DEC_BERNOULLI, DEC_GAUSSIAN = 0, 1
 EST_LB, EST_LA, EST_FV, EST_FVS = 0, 1, 2, 3   # FVS: weight-sampling extension (include/vaeb_hip.h)
 OBJ_SUM_PRIOR, OBJ_MEAN_MAP = 0, 1
 EPS_PHILOX, EPS_HOST = 0, 1
-DTYPE_F32, DTYPE_BF16 = 0, 1
+DTYPE_F32, DTYPE_BF16, DTYPE_F16 = 0, 1, 2
 
 # Every symbol declared in include/vaeb_hip.h (the drop-in boundary) and in
 # include/vaeb_diag.h (measurement / test hooks); checked by tests/test_abi.py.

@@ -55,7 +55,7 @@ command_line_args = {'seed': (15485863, int),
                      'world_size': (0, int),        # data-parallel ranks (0: one GPU, no communicator;
                                                     # N >= 1: N ranks with the RCCL all-reduce step)
                      'dp_scaling': ('strong', str), # strong: batch_size split over the ranks; weak: per rank
-                     'dtype': ('float32', str)}     # float32 (floatX, run_on_gpu.sh:2) | bf16
+                     'dtype': ('float32', str)}     # float32 (floatX, run_on_gpu.sh:2) | bf16 | fp16
 #   to add a new flag, add its name (VAEB.py:37-38)
 command_line_flags = ['continuous', 'generic_estimator', 'full_varational',
                       'synthetic']                 # added: synthetic data when the pickles are absent

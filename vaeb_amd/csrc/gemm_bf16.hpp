@@ -35,16 +35,22 @@
 //    time so concurrently running blocks share operand panels in that XCD's L2.
 // Epilogues are functors applied to the wave's accumulator block (128 x 64 or 64 x 64) in
 // registers.
-#pragma once
+//
+// Included twice by h16_engines.hpp: namespace VAEB_H16NS = bf with VAEB_H16_F16 = 0 (bf16
+// operands, v_mfma_f32_16x16x32_bf16) and VAEB_H16NS = hf with VAEB_H16_F16 = 1 (fp16 operands,
+// v_mfma_f32_16x16x32_f16, the same rate on gfx950).  Everything but the conversions and the
+// MFMA below is the same code: both formats are 16 bits per element in LDS, in the transposing
+// reads and in memory.  (The names bf16_t / bf16x8 / f2bf / bf2f stand for "this
+// instantiation's 16-bit type".)
 #include <type_traits>
 #include "tile_engine.hpp"
+#include "h16_common.hpp"
 
 namespace vaeb {
-namespace bf {
+namespace VAEB_H16NS {
 
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef short s16x8 __attribute__((ext_vector_type(8)));
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef unsigned int v4u __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 typedef uint16_t bf16_t;   // raw bf16 bits in memory
@@ -71,14 +77,26 @@ struct Shape {
     static constexpr int kBlocksPerCU = ST == 3 ? 2 : 1;
 };
 
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
+#if VAEB_H16_F16
+// fp16: f32 -> fp16 round to nearest even (v_cvt_f16_f32; fp16 subnormals kept, the HIP
+// default mode for 16-bit), fp16 -> f32 exact.
+typedef _Float16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 bf16x2_t __attribute__((ext_vector_type(2)));
+DEV uint32_t f2bf(float f) { return __builtin_bit_cast(uint16_t, (_Float16)f); }
+DEV float bf2f(uint32_t b) { return (float)__builtin_bit_cast(_Float16, (uint16_t)b); }
+DEV f32x4 mfma16(bf16x8 a, bf16x8 b, f32x4 c) { return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0); }
+#else
 // f32 -> bf16, round to nearest even: gfx950's v_cvt_pk_bf16_f32 (one instruction; the
 // integer form (u + 0x7FFF + ((u >> 16) & 1)) >> 16 gives the same bits for finite inputs in
 // four).  f2bf2: two values in one instruction, a in the low half.
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
-typedef float f32x2_t __attribute__((ext_vector_type(2)));
 DEV uint32_t f2bf(float f) { return __builtin_bit_cast(uint16_t, (__bf16)f); }
-DEV uint32_t f2bf2(float a, float b) { return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2_t){a, b}, bf16x2_t)); }
 DEV float bf2f(uint32_t b) { return __builtin_bit_cast(float, b << 16); }
+DEV f32x4 mfma16(bf16x8 a, bf16x8 b, f32x4 c) { return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0); }
+#endif
+DEV uint32_t f2bf2(float a, float b) { return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2_t){a, b}, bf16x2_t)); }
 // Epilogue functors with a post(m0, n0, smem) step after store_out (kPost; gemm8_body only)
 template <class E, class = void> struct HasPost : std::false_type {};
 template <class E> struct HasPost<E, std::void_t<decltype(E::kPost)>> : std::bool_constant<E::kPost> {};
@@ -173,13 +191,7 @@ DEV bf16x8 frag(const char* img, int row, int kk, int lane) {
     }
 }
 
-// Device-side minibatch resolution: rows of batch order[*cursor] start `stride`
-// elements after the base (the cursor advances in the step's last kernel), so a whole
-// epoch replays as graphs with no host round trip.  order == nullptr: offset 0.
-struct BatchRef {
-    const int* order; const int* cursor; int64_t stride;
-    DEV int64_t offset() const { return order ? (int64_t)order[*cursor] * stride : 0; }
-};
+using ::vaeb::h16c::BatchRef;
 
 struct GemmArgs {
     const bf16_t* A; int lda; int64_t a_bytes;   // a_bytes: readable extent from A
@@ -307,7 +319,7 @@ DEV void gemm_body(const GemmArgs& g, const Epi& e, int bid, int kz, char* smem)
         for (int i = 0; i < TM; ++i)
 #pragma unroll
             for (int j = 0; j < TN; ++j)
-                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+                acc[i][j] = mfma16(af[i], bfr[j], acc[i][j]);
         __builtin_amdgcn_s_setprio(0);
         if constexpr (PP) {
             __builtin_amdgcn_sched_barrier(0);
@@ -653,7 +665,7 @@ struct EpiDTanhTDz : EpiDTanhT {
 #pragma unroll
             for (int rt = 0; rt < 16; ++rt) {
                 const bf16x8 af = *reinterpret_cast<const bf16x8*>(smem + (16 * rt + li) * kPitch + (32 * ks + 8 * q) * 2);
-                acc[rt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfr, acc[rt], 0, 0, 0);
+                acc[rt] = mfma16(af, bfr, acc[rt]);
             }
         }
         float* out = dz_slab + (int64_t)(m0 >> 8) * slab;
@@ -916,13 +928,18 @@ struct ColMap {
 
 // Weight update from the data gradient dsg of one element (VAEB.py:386-444):
 // g = dsg - prior theta; acc += g^2; theta' = theta + lr g / (sqrt(acc) + eps) - decay theta^2.
+// gs: the backward's loss scale undone (the fp16 engine carries the 16-bit data gradients
+// scaled by a power of two, 1 / gs, so that the mean objective's 1/B-sized gradients stay
+// normal fp16 numbers; exact: a power of two); the stored gradient is the unscaled one.
 struct Opt {
     const float* th_in; float* th_out; float* accum; float* grad;
-    bf16_t* shadow_out;   // bf16 copy of theta' in GEMM layout (index m * N + n)
+    bf16_t* shadow_out;   // 16-bit copy of theta' in GEMM layout (index m * N + n)
     float lr, eps, prior, decay;
     int update, store_grad;
     int64_t n;            // arena elements (buffer-descriptor extent)
+    float gs = 1.f;       // gradient unscale (1: none)
     DEV void apply(int64_t idx, int64_t sidx, float dsg) const {   // sidx < 0: no shadow
+        dsg *= gs;
         if (store_grad) grad[idx] = dsg;
         if (!update) return;
         const float th = th_in[idx];
@@ -968,7 +985,7 @@ struct EpiAdagrad {
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     const int row = erow(mw, i, r, lane), col = ecol<CM>(nw, j, lane);
-                    const float dsg = acc[i][j][r];
+                    const float dsg = acc[i][j][r] * opt.gs;
                     if (opt.store_grad) bst(bgr, off[j][r], dsg);
                     if (opt.update) {
                         const float gg = dsg - opt.prior * th[j][r];
@@ -1115,7 +1132,7 @@ DEV void gemm8_body(const GemmArgs& g, const Epi& e, int bid, int kz, char* smem
             for (int i = 0; i < 4; ++i)
 #pragma unroll
                 for (int j = 0; j < 2; ++j)
-                    c[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][kk], bf[j][kk], c[i][j], 0, 0, 0);
+                    c[i][j] = mfma16(af[i][kk], bf[j][kk], c[i][j]);
         __builtin_amdgcn_s_setprio(0);
     };
     // first barrier of a phase (after its reads, its stage and the counted wait), the
@@ -1216,5 +1233,5 @@ __global__ __launch_bounds__(NTHR, 2) void gemm8x2_kernel(GemmArgs g1, E1 e1, Ge
 constexpr int lds8_bytes() { return ((2 * 65536 > BM * epitch<256>()) ? 2 * 65536 : BM * epitch<256>()) + 16; }
 static_assert(BM * epitch<256>() == kSplitFlag && 2 * 65536 <= kSplitFlag, "split-K flag slot");
 
-}  // namespace bf
+}  // namespace VAEB_H16NS
 }  // namespace vaeb

@@ -19,33 +19,15 @@
 // path) plus a bf16 "shadow" arena in GEMM layout that the optimizer rewrites each step:
 //   W3 [D x H] | W45 [H x 2Z] (row h = [W4 row h | W5 row h]) | W1 [Z x H] |
 //   W26 [H x Dn] (Bernoulli: W2; Gaussian: W2 / W6 interleaved in 32-column groups).
-#pragma once
-#include "gemm_bf16.hpp"
+// Included twice by h16_engines.hpp (namespace VAEB_H16NS = bf / hf), after gemm_bf16.hpp.
 #include "kernels_aux.hpp"
 
 namespace vaeb {
-namespace bf {
+namespace VAEB_H16NS {
 
-// Arena (reference order) -> shadow index map.
-struct ShadowMap {
-    int64_t offW3, offW4, offW5, offW1, offW2, offW6;   // arena offsets (offW6 < 0: Bernoulli)
-    int64_t s3, s45, s1, s26;                           // shadow offsets
-    int D, H, Z;
-    int64_t nweights;                                   // arena elements before the biases
-    DEV int64_t at(int64_t i) const {
-        if (i >= nweights) return -1;
-        const int Z2 = 2 * Z;
-        if (i < offW4) return s3 + (i - offW3);
-        if (i < offW5) { const int64_t e = i - offW4; return s45 + (e / Z) * Z2 + e % Z; }
-        if (i < offW1) { const int64_t e = i - offW5; return s45 + (e / Z) * Z2 + Z + e % Z; }
-        if (i < offW2) return s1 + (i - offW1);
-        const bool w6 = offW6 >= 0 && i >= offW6;
-        const int64_t e = i - (w6 ? offW6 : offW2);
-        const int64_t h = e / D, d = e % D;
-        if (offW6 < 0) return s26 + h * D + d;
-        return s26 + h * 2 * D + ((d >> 5) << 6) + (w6 ? 32 : 0) + (d & 31);
-    }
-};
+using ::vaeb::h16c::BfState;
+
+using ::vaeb::h16c::ShadowMap;
 
 // Sharded DP (vaeb_hip.hip dp_reduce_update): after the all-gather of theta', the bf16 shadow
 // entries of the elements other ranks updated
@@ -601,35 +583,5 @@ __global__ __launch_bounds__(256) void adagrad_bf16_kernel(Opt o, int64_t P, DpR
     }
 }
 
-}  // namespace bf
-}  // namespace vaeb
-
-namespace vaeb {
-namespace bf {
-
-// Device buffers of the bf16 engine (one context).  Row capacity R = max(B, eval chunk).
-struct BfState {
-    bool on = false;
-    int Dn = 0;                        // decoder output width (D, or 2D interleaved)
-    int64_t S = 0;                     // shadow elements
-    int64_t s3 = 0, s45 = 0, s1 = 0, s26 = 0;
-    bf16_t* shadow2[2] = {nullptr, nullptr};
-    bf16_t* x = nullptr;               // dataset [N x D] bf16
-    bf16_t* xeval = nullptr;           // eval chunk [R x D]
-    bf16_t* xval = nullptr;            // resident validation set [nval x D] (vaeb_set_valid_data)
-    bf16_t *h = nullptr, *z = nullptr, *hd = nullptr, *dA = nullptr, *dA1 = nullptr, *dml = nullptr,
-           *dA3 = nullptr;
-    float *ml_slab = nullptr, *dz_slab = nullptr, *w_slab = nullptr;
-    float *cp3 = nullptr, *cp45 = nullptr, *cp1 = nullptr, *cp26 = nullptr, *lp = nullptr, *kl = nullptr;
-    float *mu = nullptr, *lv = nullptr, *eps = nullptr;
-    double* elbo_parts = nullptr;      // [kElboBlocks][2] stage-1 ELBO sums
-    int ks_heads = 1, ks_dz = 1, ks_w1 = 1, ks_w45 = 1;
-    // latent-width products with the latent block fused into their epilogues (thin_bf16.hpp;
-    // LB, L = 1, Z % 128 == 0): no split-K slabs; nkl KL partials per row (Z / 64)
-    bool thin_h = false, thin_z = false;   // heads / dz on the thin launches
-    int nkl = 1;
-    ShadowMap smap{};
-};
-
-}  // namespace bf
+}  // namespace VAEB_H16NS
 }  // namespace vaeb

@@ -26,11 +26,10 @@
 // pieces (BMT 64: KT 2, 3 pieces per wave; BMT 32: KT 4, 5 per wave), which the counted
 // vmcnt waits rely on.  Eight waves: wave (wr, wc) owns the 16-row block wr and TPW
 // 16-column MFMA tiles of column group wc.
-#pragma once
-#include "step_bf16.hpp"
+// Included twice by h16_engines.hpp (namespace VAEB_H16NS = bf / hf), after step_bf16.hpp.
 
 namespace vaeb {
-namespace bf {
+namespace VAEB_H16NS {
 
 template <int BMT>
 struct ThinShape {
@@ -153,7 +152,7 @@ DEV void thin_body(const ThinArgs& t, const Epi& e, int bm, int bn, char* smem) 
 #pragma unroll
             for (int j = 0; j < S::TPW; ++j) bfr[j] = frag<LB, S::NT>(Bs, Epi::col(wc, j), 0, lane);
 #pragma unroll
-            for (int j = 0; j < S::TPW; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfr[j], acc[j], 0, 0, 0);
+            for (int j = 0; j < S::TPW; ++j) acc[j] = mfma16(af, bfr[j], acc[j]);
         }
         if constexpr (!k1Bar) {
             __builtin_amdgcn_s_barrier();   // stage st's buffer is refilled by the issue of st + kStages
@@ -303,5 +302,5 @@ struct EpiDzLatent {
     }
 };
 
-}  // namespace bf
+}  // namespace VAEB_H16NS
 }  // namespace vaeb

@@ -11,6 +11,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cmath>
 #include <cstdarg>
 #include <cstdlib>
 #include <cstdio>
@@ -23,8 +24,7 @@
 #include "hfuse.hpp"
 #include "latent.hpp"
 #include "latent_bwd.hpp"
-#include "step_bf16.hpp"
-#include "thin_bf16.hpp"
+#include "h16_engines.hpp"
 #include "ae_mlp.hpp"
 
 using namespace vaeb;
@@ -192,7 +192,7 @@ struct vaeb_ctx {
     uint64_t* dbg = nullptr;
     int dbg_slot = 0;
     // bf16 large-batch engine (step_bf16.hpp); off for dtype == VAEB_DTYPE_F32
-    bf::BfState bf;
+    h16c::BfState bf;
 };
 
 namespace {
@@ -905,7 +905,51 @@ int dp_bucket_b(vaeb_ctx* c, Prof& pr, int opt_mark, float* theta_out, Opt opt, 
     return 0;
 }
 
+// ------------------------------------------------------------------ the 16-bit engine
+// One host engine (engine_bf16.inc) over two device instantiations (h16_engines.hpp): bf16
+// (VAEB_DTYPE_BF16) and fp16 (VAEB_DTYPE_F16) operands, fp32 accumulation, fp32 masters.
+using bf::bf16_t;
+bool is_bf16(const vaeb_ctx* c) { return c->c.dtype == VAEB_DTYPE_BF16 || c->c.dtype == VAEB_DTYPE_F16; }   // the 16-bit engine
+bool is_f16(const vaeb_ctx* c) { return c->c.dtype == VAEB_DTYPE_F16; }
+// A/B (round 3): 256 x 256 tiles on the 8-phase BK = 64 main loop (gemm8_kernel) instead of
+// gemm_body's BK = 32 ring, per operand-layout pair: bit (2 LA + LB) of VAEB_BF_GEMM8 (set at
+// context creation) -- 1: KC x KC (dhd), 2: KC x KO (enc), 8: KO x KO (dW2, dW3).
+int g_gemm8 = 0;
+template <int LA, int LB> bool use8() { return (g_gemm8 >> (2 * LA + LB)) & 1; }
+// A forward pass of the 16-bit engine for `Mb` rows starting at x (device, 16-bit) with the
+// parameters of arena par.  train: store dA / bias partials for the backward.  yout: decoder means.
+struct BfFwd {
+    int Mb, mode; bool train;
+    const bf16_t* x; h16c::BatchRef xb;
+    int64_t row_base_mul, row_base_add;
+    const float* eps_in; int64_t eps_in_ld; uint32_t domain;
+    float* yout;
+};
+namespace eng_bf {
+namespace bf = ::vaeb::bf;
+constexpr bool kF16 = false;
 #include "engine_bf16.inc"
+}  // namespace eng_bf
+namespace eng_hf {
+namespace bf = ::vaeb::hf;
+constexpr bool kF16 = true;
+#include "engine_bf16.inc"
+}  // namespace eng_hf
+#define H16_CALL(fn, ...) (is_f16(c) ? eng_hf::fn(__VA_ARGS__) : eng_bf::fn(__VA_ARGS__))
+int bf_train_step(vaeb_ctx* c, int par, bool prof, int direct) { return H16_CALL(bf_train_step, c, par, prof, direct); }
+int bf_alloc(vaeb_ctx* c) { return H16_CALL(bf_alloc, c); }
+void bf_free(vaeb_ctx* c) { eng_bf::bf_free(c); }   // (type-independent: frees the state's buffers)
+int bf_make_shadow(vaeb_ctx* c, int par) { return H16_CALL(bf_make_shadow, c, par); }
+int bf_upload_rows(vaeb_ctx* c, const float* x, int64_t n, bf16_t* dst) { return H16_CALL(bf_upload_rows, c, x, n, dst); }
+int bf_forward(vaeb_ctx* c, int par, const BfFwd& f, Prof& pr) { return H16_CALL(bf_forward, c, par, f, pr); }
+int bf_eval_chunk(vaeb_ctx* c, const float* x, int rows, int64_t r0, int mode, float* out_y) {
+    return H16_CALL(bf_eval_chunk, c, x, rows, r0, mode, out_y);
+}
+int bf_eval_chunk_dev(vaeb_ctx* c, const bf16_t* x, int rows, int64_t r0, int mode, float* out_y) {
+    return H16_CALL(bf_eval_chunk_dev, c, x, rows, r0, mode, out_y);
+}
+int h16_dp_opt(vaeb_ctx* c, int par, const DpRange& own) { return H16_CALL(h16_dp_opt, c, par, own); }
+int h16_dp_fix(vaeb_ctx* c, int par, const DpRange& fr) { return H16_CALL(h16_dp_fix, c, par, fr); }
 
 // One training step reading parameter arena `par` and writing arena par ^ 1.
 // One stream: P1 -> P23 -> P4 -> [P5 | dW2 (| dW6)] -> [P67 | dW1] -> [dW3 | dW45 + ELBO]
@@ -1280,8 +1324,9 @@ int vaeb_create(const vaeb_config* cfg, vaeb_ctx** out) {
     const bool fvx = g.estimator == VAEB_EST_FV || g.estimator == VAEB_EST_FVS;
     if (fvx && g.L != 1)
         return fail(VAEB_ERR_ARG, "the full-variational estimators support L == 1 only (VAEB.py:361)");
-    if (g.dtype != VAEB_DTYPE_F32 && g.dtype != VAEB_DTYPE_BF16) return fail(VAEB_ERR_ARG, "bad dtype %d", g.dtype);
-    if (g.dtype == VAEB_DTYPE_BF16) {
+    if (g.dtype != VAEB_DTYPE_F32 && g.dtype != VAEB_DTYPE_BF16 && g.dtype != VAEB_DTYPE_F16)
+        return fail(VAEB_ERR_ARG, "bad dtype %d", g.dtype);
+    if (g.dtype == VAEB_DTYPE_BF16 || g.dtype == VAEB_DTYPE_F16) {
         if (g.D % 8 || g.H % 8 || g.Z % 8)
             return fail(VAEB_ERR_ARG, "bf16 engine: D, H, Z must be multiples of 8 (got %d, %d, %d)", g.D, g.H, g.Z);
         if (g.decoder == VAEB_DEC_GAUSSIAN && g.D % 32)
@@ -1971,7 +2016,7 @@ int vaeb_reconstruct_full(vaeb_ctx* c, const float* x, int64_t n, int32_t n_samp
             Prof pr{c, false};
             if (is_bf16(c)) {
                 BfFwd f{};
-                f.Mb = rows; f.mode = MODE_EVAL; f.train = false; f.x = c->bf.xeval; f.xb = bf::BatchRef{};
+                f.Mb = rows; f.mode = MODE_EVAL; f.train = false; f.x = c->bf.xeval; f.xb = h16c::BatchRef{};
                 f.row_base_mul = 0; f.row_base_add = r0;
                 f.eps_in = eps; f.eps_in_ld = c->eps_rows; f.domain = domain;
                 f.yout = c->y;
@@ -2167,159 +2212,16 @@ int vaeb_debug_timeline(vaeb_ctx* c, int32_t batch_index, uint64_t* out, int64_t
 
 int vaeb_test_gemm_bf16(vaeb_ctx* c, int32_t ako, int32_t bko, int32_t M, int32_t N, int32_t K, const float* A,
                         const float* B, float* C, int32_t ksplit) {
-    // ksplit < 0: the 256 x 256 8-phase main loop (gemm8_kernel) with -ksplit slices;
-    // -22: two slices combined in the launch (split2_combine), one output
-    const bool split2 = ksplit == -22;
-    if (split2) ksplit = -2;
-    const bool force8 = ksplit < 0;
-    if (force8) ksplit = -ksplit;
-    if (!c || !A || !B || !C || M <= 0 || N <= 0 || K <= 0 || ksplit <= 0) return fail(VAEB_ERR_ARG, "bad arguments");
-    if (K % 8 || (ako && M % 8) || (bko && N % 8))
-        return fail(VAEB_ERR_ARG, "bf16 GEMM: K (and a K-outer operand's rows) must be multiples of 8");
-    const size_t na = (size_t)M * K, nb = (size_t)N * K;
-    const int nz = bf_slices(K, ksplit);
-    float *fa = nullptr, *fb = nullptr, *fc = nullptr;
-    bf16_t *ba = nullptr, *bb = nullptr;
-    int rc = 0;
-    rc = rc ? rc : dalloc(&fa, na);
-    rc = rc ? rc : dalloc(&fb, nb);
-    rc = rc ? rc : dalloc(&ba, na);
-    rc = rc ? rc : dalloc(&bb, nb);
-    rc = rc ? rc : dalloc(&fc, (size_t)nz * M * N);
-    float* part = nullptr;
-    int* ticket = nullptr;
-    const int tiles256 = cdiv(M, bf::BM) * cdiv(N, 256);
-    if (split2) {
-        rc = rc ? rc : dalloc(&part, (size_t)tiles256 * 65536);
-        rc = rc ? rc : dalloc(&ticket, (size_t)tiles256);
-    }
-    if (!rc) {
-        hipMemcpy(fa, A, na * 4, hipMemcpyHostToDevice);
-        hipMemcpy(fb, B, nb * 4, hipMemcpyHostToDevice);
-        hipLaunchKernelGGL(bf::to_bf16_kernel, dim3(256), dim3(256), 0, c->s, fa, ba, (int64_t)na);
-        hipLaunchKernelGGL(bf::to_bf16_kernel, dim3(256), dim3(256), 0, c->s, fb, bb, (int64_t)nb);
-        const bf::EpiF32 e{fc, N, M, N, (int64_t)M * N};
-        const int lda = ako ? M : K, ldb = bko ? N : K;
-        const int64_t ab = (int64_t)na * 2, bbytes = (int64_t)nb * 2;
-        if (force8) {
-            bf::GemmArgs g = bf_args256(ba, lda, ab, bb, ldb, bbytes, M, N, K, ksplit);
-            if (split2) {
-                g.part = part;
-                g.ticket = ticket;
-                g.kslice = ((cdiv(K, 2) + 63) / 64) * 64;
-            }
-            if (!ako && !bko) rc = bf_launch8<bf::KC, bf::KC>(c->s, g, nz, e);
-            else if (!ako && bko) rc = bf_launch8<bf::KC, bf::KO>(c->s, g, nz, e);
-            else if (ako && !bko) rc = bf_launch8<bf::KO, bf::KC>(c->s, g, nz, e);
-            else rc = bf_launch8<bf::KO, bf::KO>(c->s, g, nz, e);
-        } else if (!ako && !bko) rc = bf_gemm<bf::KC, bf::KC>(c->s, ba, lda, ab, bb, ldb, bbytes, M, N, K, ksplit, e);
-        else if (!ako && bko) rc = bf_gemm<bf::KC, bf::KO>(c->s, ba, lda, ab, bb, ldb, bbytes, M, N, K, ksplit, e);
-        else if (ako && !bko) rc = bf_gemm<bf::KO, bf::KC>(c->s, ba, lda, ab, bb, ldb, bbytes, M, N, K, ksplit, e);
-        else rc = bf_gemm<bf::KO, bf::KO>(c->s, ba, lda, ab, bb, ldb, bbytes, M, N, K, ksplit, e);
-    }
-    if (!rc) {
-        std::vector<float> slabs((size_t)nz * M * N);
-        hipError_t e = hipStreamSynchronize(c->s);
-        if (e == hipSuccess) e = hipMemcpy(slabs.data(), fc, slabs.size() * 4, hipMemcpyDeviceToHost);
-        if (e != hipSuccess) rc = fail(VAEB_ERR_HIP, "test gemm: %s", hipGetErrorString(e));
-        for (size_t i = 0; !rc && i < (size_t)M * N; ++i) {
-            float v = 0.f;
-            for (int z = 0; z < nz; ++z) v += slabs[(size_t)z * M * N + i];
-            C[i] = v;
-        }
-    }
-    if (!rc && split2) {   // every ticket back at zero
-        std::vector<int> tk(tiles256);
-        if (hipMemcpy(tk.data(), ticket, tk.size() * 4, hipMemcpyDeviceToHost) != hipSuccess)
-            rc = fail(VAEB_ERR_HIP, "test gemm: ticket copy");
-        for (int t : tk) if (!rc && t != 0) rc = fail(VAEB_ERR_HIP, "test gemm: split-K ticket left at %d", t);
-    }
-    for (void* p : {(void*)fa, (void*)fb, (void*)fc, (void*)ba, (void*)bb, (void*)part, (void*)ticket}) if (p) hipFree(p);
-    return rc;
+    if (!c) return fail(VAEB_ERR_ARG, "null ctx");
+    return is_f16(c) ? eng_hf::h16_test_gemm(c, ako, bko, M, N, K, A, B, C, ksplit)
+                     : eng_bf::h16_test_gemm(c, ako, bko, M, N, K, A, B, C, ksplit);
 }
-
-extern "C++" {
-// Diagnostics: device-side uniform [-1, 1) bf16 fill (a hash of the index), no host copy.
-__global__ __launch_bounds__(256) void fill_bf16_kernel(bf16_t* p, int64_t n, uint32_t seed) {
-    const int64_t stride = (int64_t)gridDim.x * 256;
-    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) {
-        uint32_t h = (uint32_t)i * 0x9E3779B1u ^ seed;
-        h ^= h >> 15; h *= 0x2C1B3C6Du; h ^= h >> 12; h *= 0x297A2D39u; h ^= h >> 15;
-        p[i] = (bf16_t)bf::f2bf((float)(h >> 8) * (2.0f / 16777216.0f) - 1.0f);
-    }
-}
-
-template <int LA, int LB>
-static int bench_gemm_launch(hipStream_t s, const bf16_t* A, const bf16_t* B, int M, int N, int K, int bn,
-                             const bf::EpiBiasAct& e, float* part, int* ticket) {
-    bf::GemmArgs g{};
-    g.A = A; g.lda = LA == bf::KO ? M : K; g.a_bytes = (int64_t)M * K * 2;
-    g.B = B; g.ldb = LB == bf::KO ? N : K; g.b_bytes = (int64_t)N * K * 2;
-    g.M = M; g.N = N; g.K = K;
-    g.tiles_m = cdiv(M, bf::BM); g.tiles_n = cdiv(N, bn);
-    g.kslice = ((K + bf::BK - 1) / bf::BK) * bf::BK;
-    if (bn == 8 || bn == 9) {
-        g.tiles_n = cdiv(N, 256);
-        if (bn == 9) {   // two K slices combined in the launch (split2_combine)
-            g.part = part;
-            g.ticket = ticket;
-            g.kslice = ((cdiv(K, 2) + 63) / 64) * 64;
-        }
-        return bf_launch8<LA, LB>(s, g, bn == 9 ? 2 : 1, e);
-    }
-    if (bn == 256) return bf_launch<LA, LB, 256>(s, g, 1, e);
-    return bf_launch<LA, LB, 128>(s, g, 1, e);
-}
-}  // extern "C++"
 
 int vaeb_bench_gemm_bf16(vaeb_ctx* c, int32_t ako, int32_t bko, int32_t M, int32_t N, int32_t K, int32_t bn,
                          int32_t reps, float* out_ms) {
-    if (!c || !out_ms || M <= 0 || N <= 0 || K <= 0 || reps <= 0) return fail(VAEB_ERR_ARG, "bad arguments");
-    if (K % 8 || M % 8 || N % 8) return fail(VAEB_ERR_ARG, "bench gemm: M, N, K must be multiples of 8");
-    if (bn == 0) bn = bf_bn(M, N);
-    if (bn != 128 && bn != 256 && bn != 8 && bn != 9)
-        return fail(VAEB_ERR_ARG, "bench gemm: tile width 128 or 256 (8: 256 x 256 on the 8-phase loop, "
-                                  "9: the same as two K slices)");
-    bf16_t *a = nullptr, *b = nullptr, *o = nullptr;
-    float *bias = nullptr, *part = nullptr;
-    int* ticket = nullptr;
-    int rc = 0;
-    if (bn == 9) {
-        const int tiles = cdiv(M, bf::BM) * cdiv(N, 256);
-        rc = rc ? rc : dalloc(&part, (size_t)tiles * 65536);
-        rc = rc ? rc : dalloc(&ticket, (size_t)tiles);
-    }
-    rc = rc ? rc : dalloc(&a, (size_t)M * K);
-    rc = rc ? rc : dalloc(&b, (size_t)N * K);
-    rc = rc ? rc : dalloc(&o, (size_t)M * N);
-    rc = rc ? rc : dalloc(&bias, (size_t)N);
-    hipEvent_t e0 = nullptr, e1 = nullptr;
-    if (!rc) {
-        hipLaunchKernelGGL(fill_bf16_kernel, dim3(1024), dim3(256), 0, c->s, a, (int64_t)M * K, 1u);
-        hipLaunchKernelGGL(fill_bf16_kernel, dim3(1024), dim3(256), 0, c->s, b, (int64_t)N * K, 2u);
-        const bf::EpiBiasAct e{bias, 0, M, N, o, N};
-        auto one = [&]() {
-            if (!ako && !bko) return bench_gemm_launch<bf::KC, bf::KC>(c->s, a, b, M, N, K, bn, e, part, ticket);
-            if (!ako && bko) return bench_gemm_launch<bf::KC, bf::KO>(c->s, a, b, M, N, K, bn, e, part, ticket);
-            if (ako && !bko) return bench_gemm_launch<bf::KO, bf::KC>(c->s, a, b, M, N, K, bn, e, part, ticket);
-            return bench_gemm_launch<bf::KO, bf::KO>(c->s, a, b, M, N, K, bn, e, part, ticket);
-        };
-        rc = one();   // warm-up
-        hipEventCreate(&e0);
-        hipEventCreate(&e1);
-        hipEventRecord(e0, c->s);
-        for (int r = 0; !rc && r < reps; ++r) rc = one();
-        hipEventRecord(e1, c->s);
-        if (!rc && hipEventSynchronize(e1) == hipSuccess) {
-            float ms = 0.f;
-            hipEventElapsedTime(&ms, e0, e1);
-            *out_ms = ms / (float)reps;
-        }
-    }
-    if (e0) hipEventDestroy(e0);
-    if (e1) hipEventDestroy(e1);
-    for (void* p : {(void*)a, (void*)b, (void*)o, (void*)bias, (void*)part, (void*)ticket}) if (p) hipFree(p);
-    return rc;
+    if (!c) return fail(VAEB_ERR_ARG, "null ctx");
+    return is_f16(c) ? eng_hf::h16_bench_gemm(c, ako, bko, M, N, K, bn, reps, out_ms)
+                     : eng_bf::h16_bench_gemm(c, ako, bko, M, N, K, bn, reps, out_ms);
 }
 
 int vaeb_time_update_many(vaeb_ctx* c, const int32_t* idx, int32_t n, float* out_gpu_ms, double* out_enqueue_ms) {
@@ -2437,16 +2339,15 @@ static int dp_rank_update_body(vaeb_ctx* c, int bucket, const float* gsum, const
         if (own.n[k])
             HIP_TRY(hipMemcpyAsync(c->grad + own.lo[k], gsum + own.lo[k], sizeof(float) * (size_t)own.n[k],
                                    hipMemcpyHostToDevice, s));
-    const OptArgs o32 = make_opt(c, par, true, false);
-    const bf::Opt o16 = bf ? bf_opt(c, par, true, false) : bf::Opt{};
-    if (int rc = bf ? bf_dp_opt_launch(c, s, o16, own, ElboArgs{}) : dp_opt_launch(c, s, o32, own, ElboArgs{})) return rc;
+    if (int rc = bf ? h16_dp_opt(c, par, own) : dp_opt_launch(c, s, make_opt(c, par, true, false), own, ElboArgs{}))
+        return rc;
     if (thg) {
         // the all-gather: the other ranks' theta' shards into the out arena, then their shadow
         for (int k = 0; k < kDpRuns; ++k)
             if (fr.n[k])
                 HIP_TRY(hipMemcpyAsync(c->theta2[par ^ 1] + fr.lo[k], thg + fr.lo[k], sizeof(float) * (size_t)fr.n[k],
                                        hipMemcpyHostToDevice, s));
-        if (bf) if (int rc = bf_dp_fix_launch(c, s, o16, fr)) return rc;
+        if (bf) if (int rc = h16_dp_fix(c, par, fr)) return rc;
     }
     HIP_TRY(hipStreamSynchronize(s));
     return 0;

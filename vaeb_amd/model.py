@@ -44,14 +44,22 @@ def initial_params(D, H, Z, continuous):
 
 
 def dtype_name(dtype):
-    """The engine a dtype name selects: "float32" (aliases f32, fp32) or "bf16" (bfloat16).
-    fp16 is not an engine: bf16 runs at the same MFMA rate without a loss scale."""
+    """The engine a dtype name selects: "float32" (aliases f32, fp32), "bf16" (bfloat16) or
+    "fp16" (float16, f16, half): the 16-bit MFMA engine with bf16 or fp16 operands."""
     d = str(dtype).lower()
     if d in ("float32", "f32", "fp32"):
         return "float32"
     if d in ("bf16", "bfloat16"):
         return "bf16"
-    raise ValueError(f"dtype {dtype!r}: float32 or bf16 (fp16 operands are served by the bf16 engine, DESIGN.md 4.2)")
+    if d in ("fp16", "float16", "f16", "half"):
+        return "fp16"
+    raise ValueError(f"dtype {dtype!r}: float32, bf16 or fp16")
+
+
+def lib_dtype(name):
+    """The library's vaeb_dtype for a dtype_name()."""
+    from . import _lib
+    return {"float32": _lib.DTYPE_F32, "bf16": _lib.DTYPE_BF16, "fp16": _lib.DTYPE_F16}[dtype_name(name)]
 
 
 def train_rows(data):
@@ -153,7 +161,7 @@ class VAEB:
                                  objective=_lib.OBJ_MEAN_MAP if objective == "mean_map" else _lib.OBJ_SUM_PRIOR,
                                  lr=learning_rate, adagrad_eps=self.eps, device=device, B_global=B_global,
                                  row_offset=row_offset, max_eval_rows=max_eval_rows, use_graph=use_graph,
-                                 dtype=_lib.DTYPE_BF16 if self.dtype == "bf16" else _lib.DTYPE_F32)
+                                 dtype=lib_dtype(self.dtype))
         self.B_global = B_global or batch_size
         self.row_offset = row_offset
         self.world, self.rank = 1, 0
