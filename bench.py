@@ -13,7 +13,7 @@ Configs (BASELINE.json):
   --config fv    (config 4): literal --full_varational step, MNIST 784-500-20, B=100, fp32
   --config fvs   (config 4, weight-posterior reparam extension): FV with theta~ = mu + |sigma| zeta
   --config synth (config 5, roofline stress): 4096-2048-128 Bernoulli, B=8192 per GPU,
-                 bf16 MFMA operands / fp32 accumulation and master weights
+                 fp16 MFMA operands (--dtype bf16: bf16) / fp32 accumulation and master weights
 
 Usage:  python bench.py [--gpus N] [--steps K] [--warmup W] [--config mnist|frey|fv|fvs|synth]
                        [--scaling weak|strong]
@@ -34,7 +34,7 @@ sys.path.insert(0, ROOT)
 import numpy as np  # noqa: E402
 
 PEAK_F32_TFLOPS = 157.3    # MI355X f32 MFMA / vector peak (MI355X_MICROARCH.md)
-PEAK_BF16_TFLOPS = 2500.0  # MI355X dense bf16 MFMA peak (no sparsity)
+PEAK_BF16_TFLOPS = 2500.0  # MI355X dense bf16 / fp16 MFMA peak (no sparsity; the same rate for both)
 PEAK_HBM_GBS = 8000.0
 
 
@@ -274,9 +274,10 @@ CONFIGS = {
                 workload="MNIST 784-500-20 Bernoulli decoder, FVS estimator (extension: weights sampled from "
                          "N(mu, sigma^2) each step, VAEB.py:127-129; Adagrad on mu / sigma), L=1, lr 0.01 "
                          "(BASELINE config 4's weight-posterior reparam)"),
-    "synth": dict(D=4096, H=2048, Z=128, B=8192, N=16 * 8192, dtype="bf16", steps=50, warmup=5,
-                  metric="SGVB training images/sec, synthetic 4096-2048-128, batch 8192 per GPU, bf16 MFMA",
-                  workload="synthetic 4096-2048-128 Bernoulli decoder, LB, L=1, Adagrad lr 0.01, bf16 operands / "
+    # BASELINE config 5 names fp16 MFMA: fp16 operands by default (--dtype bf16: the bf16 instantiation)
+    "synth": dict(D=4096, H=2048, Z=128, B=8192, N=16 * 8192, dtype="fp16", steps=50, warmup=5,
+                  metric="SGVB training images/sec, synthetic 4096-2048-128, batch 8192 per GPU, fp16 MFMA",
+                  workload="synthetic 4096-2048-128 Bernoulli decoder, LB, L=1, Adagrad lr 0.01, fp16 operands / "
                            "fp32 accumulate + fp32 master weights (BASELINE config 5)"),
 }
 
@@ -403,7 +404,7 @@ def main(argv=None):
                     help="weak: B rows per GPU (default); strong: one B-row global minibatch split "
                          "contiguously over the ranks (100 over 8 = 13,13,13,13,12,12,12,12; SURVEY 8(e))")
     ap.add_argument("--dtype", choices=sorted(DTYPES), default=None,
-                    help="operand type (default: the config's; synth: bf16).  fp16 runs config 5 on "
+                    help="operand type (default: the config's; synth: fp16).  fp16 runs config 5 on "
                          "v_mfma_f32_16x16x32_f16 as BASELINE.json names it (DESIGN.md 4.2)")
     argv = sys.argv[1:] if argv is None else list(argv)
     args = ap.parse_args(argv)
@@ -414,7 +415,7 @@ def main(argv=None):
     if args.dtype and args.dtype != C["dtype"]:
         C = dict(C, dtype=args.dtype)
         for k in ("metric", "workload"):
-            C[k] = C[k].replace("bf16", args.dtype)
+            C[k] = C[k].replace(CONFIGS[args.config]["dtype"], args.dtype)
     steps = args.steps if args.steps is not None else C["steps"]
     warmup = args.warmup if args.warmup is not None else C["warmup"]
 

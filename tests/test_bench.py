@@ -112,8 +112,10 @@ def test_cpu_baseline_leg_runs(continuous):
 
 def test_configs_name_their_metric():
     for name, c in bench.CONFIGS.items():
-        assert c["metric"] and c["workload"] and c["dtype"] in ("f32", "bf16")
+        assert c["metric"] and c["workload"] and c["dtype"] in bench.DTYPES
     assert bench.CONFIGS["mnist"]["metric"] == "SGVB training images/sec + ELBO at MNIST 784-500-20, batch 100"
+    # BASELINE.json config 5: "fp16 MFMA"
+    assert bench.CONFIGS["synth"]["dtype"] == "fp16" and "fp16 MFMA" in bench.CONFIGS["synth"]["metric"]
 
 
 def test_cpu_baseline_fv_leg_runs():
