@@ -111,7 +111,7 @@ KERNEL_SYMBOLS = {"p1_enc": "PEnc", "p23_heads_dechid": "heads_dechid_kernel", "
                   "bf_dhd_dW26": ("2_kernel<1, 1,",),   # gemm2_kernel | gemm8x2_kernel
                   "p5_dhd_dz_w2": "vaeb::dhd_dz_wgrad_kernel", "p8_wgrad_w3w45w1": "vaeb::wgrad3_kernel",
                   "p1_enc_latent_w2": ("vaeb::enc_latent16_w2",), "p5_dhd_dz": "vaeb::dhd_dz_wgrad_kernel"}
-PMC_ROUNDS = ("r5", "r4")   # the newest round whose committed PMC passes give roofline.traffic (traffic_source)
+PMC_ROUNDS = ("r6", "r5", "r4")   # the newest round whose committed PMC passes give roofline.traffic (traffic_source)
 PMC_FILES = {c: next((p for p in (os.path.join(ROOT, "profiles", r, f"pmc_{c}_per_launch.json") for r in PMC_ROUNDS)
                       if os.path.exists(p)), os.path.join(ROOT, "profiles", PMC_ROUNDS[-1], f"pmc_{c}_per_launch.json"))
              for c in ("mnist", "frey", "fv", "fvs", "synth")}
