@@ -6,7 +6,7 @@ import time
 
 import numpy as np
 
-sys.path.insert(0, ".")
+sys.path.insert(0, __import__("os").path.dirname(__import__("os").path.dirname(__import__("os").path.abspath(__file__))))
 from vaeb_amd import _lib  # noqa: E402
 from vaeb_amd.model import initial_params  # noqa: E402
 from vaeb_amd.synthetic import mnist_like  # noqa: E402

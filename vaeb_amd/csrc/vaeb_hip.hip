@@ -151,8 +151,7 @@ struct vaeb_ctx {
     bool async_pending = false;   // steps enqueued by vaeb_update_many / _async not yet synchronised
     hipEvent_t ctl_ev = nullptr;
     // graphs
-    hipGraphExec_t g1[2] = {nullptr, nullptr};
-    hipGraphExec_t gN[kGraphSteps + 1] = {};  // gN[n]: n steps from arena 0 (run_steps)
+    hipGraphExec_t gN[2][kGraphSteps + 1] = {};  // gN[p][n]: n steps from arena p (run_steps)
     bool graph_failed = false;
     std::string graph_err;        // why the capture failed (vaeb_graph_status)
     // comm
@@ -1177,10 +1176,11 @@ int enqueue_train_step(vaeb_ctx* c, int par, bool prof, bool fresh = true, int d
 bool flips(const vaeb_ctx* c) { return c->c.estimator != VAEB_EST_FV && c->c.estimator != VAEB_EST_FVS; }
 
 void free_graphs(vaeb_ctx* c) {
-    for (auto& g1 : c->g1) if (g1) hipGraphExecDestroy(g1);
-    for (auto& gn : c->gN) if (gn) hipGraphExecDestroy(gn);
-    c->g1[0] = c->g1[1] = nullptr;
-    for (auto& gn : c->gN) gn = nullptr;
+    for (auto& fam : c->gN)
+        for (auto& gn : fam) {
+            if (gn) hipGraphExecDestroy(gn);
+            gn = nullptr;
+        }
     c->w2_graph = false;
 }
 
@@ -1217,18 +1217,20 @@ int step_eager(vaeb_ctx* c, int direct = -1) {
     return 0;
 }
 
-// Enqueue n steps (graph replay when enabled, else eager launches).  Graphs: g1[par] is
-// one step from arena par; gN[m] is m steps from arena 0 (m = 1 .. 32), the whole family
-// captured at the first call (a capture inside a later, timed call would cost more than
-// the launches it saves).  A call replays as [one step back to arena 0] + n / 32 launches
-// of gN[32] + ONE launch of gN[n % 32]: a 20-step call is one graph, not 16 + 4 (each
-// graph-to-graph boundary left the GPU idle for ~9 us).
+// Enqueue n steps (graph replay when enabled, else eager launches).  Graphs: gN[p][m] is m
+// steps from arena p (m = 1 .. 32; p = 1 only for the estimators that flip arenas), both
+// families captured at the first call (a capture inside a later, timed call would cost more
+// than the launches it saves).  A call replays as n / 32 launches of gN[par][32] + ONE launch
+// of gN[par][n % 32] from whichever arena it starts: a graph-to-graph boundary leaves the GPU
+// idle for ~8 us (kernel trace, profiles/r6/call_timeline.txt), so a 20-step call is one
+// graph, not 16 + 4, and the 19 steps after update_many's eager first step are one graph,
+// not [one step back to arena 0] + the arena-0 graph (rounds 3-5).
 int run_steps(vaeb_ctx* c, int n) {
     if (c->c.use_graph && !c->graph_failed) {
-        if (!c->g1[0]) {
-            int rc = capture(c, 1, 0, &c->g1[0]);
-            if (rc == 0) rc = capture(c, 1, 1, &c->g1[1]);
-            for (int m = 1; m <= kGraphSteps && rc == 0; ++m) rc = capture(c, m, 0, &c->gN[m]);
+        if (!c->gN[0][1]) {
+            int rc = 0;
+            for (int p = 0; p < (flips(c) ? 2 : 1); ++p)
+                for (int m = 1; m <= kGraphSteps && rc == 0; ++m) rc = capture(c, m, p, &c->gN[p][m]);
             if (rc) {
                 // never silent: the reason is kept for vaeb_graph_status.  With a
                 // communicator of more than one rank the call fails instead of degrading:
@@ -1246,17 +1248,11 @@ int run_steps(vaeb_ctx* c, int n) {
             }
         }
         if (!c->graph_failed) {
-            int i = 0;
-            // FV / FVS never flip the arena: c->par stays 0 and every family graph applies
-            if (c->par != 0 && n > 0) {
-                HIP_TRY(hipGraphLaunch(c->g1[c->par], c->s));
-                c->par ^= 1;
-                ++i;
-            }
-            while (n - i > 0) {
-                const int m = std::min(kGraphSteps, n - i);
-                HIP_TRY(hipGraphLaunch(c->gN[m], c->s));
-                if (flips(c)) c->par = m & 1;
+            // FV / FVS never flip the arena: c->par stays 0 and only family 0 exists
+            for (int i = 0; i < n;) {
+                const int m = std::min(kGraphSteps, n - i), p = flips(c) ? c->par : 0;
+                HIP_TRY(hipGraphLaunch(c->gN[p][m], c->s));
+                if (flips(c)) c->par = p ^ (m & 1);
                 i += m;
             }
             if (n > 0 && c->w2_graph) c->w2_dirty = true;   // the last replayed step left its dW2 pending
@@ -1671,18 +1667,18 @@ int vaeb_update_many(vaeb_ctx* c, const int32_t* idx, int32_t n) {
     // host eps holds ONE step's noise: a multi-step call would train every step on it
     if (c->eps_mode == VAEB_EPS_HOST && n > 1)
         return fail(VAEB_ERR_STATE, "host eps mode: one step per call (push eps before each vaeb_update)");
-    int32_t done = 0;
     if (n > 0) c->async_pending = true;
-    if (n >= 2 && c->c.use_graph && c->g1[0] && !c->graph_failed && flips(c)) {
-        // the call's first step goes out eagerly with its minibatch index in the launch
-        // arguments: the GPU starts it while the host still submits the order upload and the
-        // graph of the remaining steps (which would otherwise lead every call)
-        if (int rc = step_eager(c, idx[0])) return rc;
-        done = 1;
-    }
-    while (done < n) {
+    // the call's first step goes out eagerly with its minibatch index in the launch arguments
+    // (it reads no order and no cursor): the GPU runs it while the host submits the graph of
+    // the remaining steps (which would otherwise lead every call).  The order of those steps
+    // is uploaded BEFORE it: launched after the eager step, the upload kernel started ~6 us
+    // after the GPU had finished the step (kernel trace, profiles/r6/call_timeline.txt)
+    const bool eager = n >= 2 && c->c.use_graph && c->gN[0][1] && !c->graph_failed && flips(c);
+    for (int32_t done = eager ? 1 : 0; done < n;) {
         const int32_t m = std::min<int32_t>(n - done, kOrderCap);
         if (int rc = upload_order(c, idx + done, m)) return rc;
+        if (eager && done == 1)
+            if (int rc = step_eager(c, idx[0])) return rc;
         if (int rc = run_steps(c, m)) return rc;
         done += m;
     }
@@ -2256,7 +2252,7 @@ int vaeb_graph_status(vaeb_ctx* c, int32_t* mode, char* msg, int32_t cap) {
     if (!c || !mode) return fail(VAEB_ERR_ARG, "null argument");
     if (!c->c.use_graph) *mode = VAEB_GRAPH_OFF;
     else if (c->graph_failed) *mode = VAEB_GRAPH_EAGER_FALLBACK;
-    else *mode = c->g1[0] ? VAEB_GRAPH_REPLAY : VAEB_GRAPH_NOT_CAPTURED;
+    else *mode = c->gN[0][1] ? VAEB_GRAPH_REPLAY : VAEB_GRAPH_NOT_CAPTURED;
     if (msg && cap > 0) snprintf(msg, (size_t)cap, "%s", c->graph_failed ? c->graph_err.c_str() : "");
     return 0;
 }
