@@ -183,6 +183,10 @@ struct vaeb_ctx {
     bool w2_graph = false;        // host: the captured graphs hold deferred-dW2 steps (run_steps sets w2_dirty)
     int atomic_ho = 1;            // folded latent hand-offs: 1 by fan-in (ho_mode), 0 slabs
     int enc_red = -1;             // encoder slabs summed by the decoder launch: -1 auto, VAEB_ENC_RED=0|1
+    // update_many's order upload held back until the eager first step's first launch is out
+    // (order_hook): the upload kernel then runs behind the encoder instead of ahead of it
+    bool order_pending = false;
+    OrderArg order_pend;
     // profiling
     hipEvent_t pev[kMaxProfKernels + 1] = {};
     int prof_n = 0, prof_reps = 1;
@@ -213,6 +217,8 @@ void set_arena_layout(vaeb_ctx* c) {
 }
 
 uint64_t* next_dbg(vaeb_ctx* c) { return c->dbg ? c->dbg + (size_t)(c->dbg_slot++) * kDbgWG * 8 : nullptr; }
+
+int order_hook(vaeb_ctx* c);
 
 StepArgs make_args(vaeb_ctx* c, int par, int Mb, int mode, const float* xbase, bool train) {
     StepArgs a{};
@@ -505,6 +511,7 @@ int enqueue_forward(vaeb_ctx* c, const StepArgs& a0, Prof& pr, const FvFold& fvf
             else launch_enc_latent<0>(s, g1, a, fvf, deep, ct);
         }
         CHECK_LAUNCH();
+        if (int rc = order_hook(c)) return rc;
         a.dbg = next_dbg(c);
         // Bernoulli: two 16-column tiles per workgroup (decout_z2_kernel; one tile: 42.0 vs
         // 39.4 us per step in round 3, its switch VAEB_DECOUT_CT removed in round 6)
@@ -1264,6 +1271,18 @@ int run_steps(vaeb_ctx* c, int n) {
     return 0;
 }
 
+// The order upload update_many held back for its eager first step (vaeb_ctx::order_pending):
+// launched right after that step's first kernel, or after the step where no launch site
+// takes it.  The eager step addresses its rows from its launch arguments and reads neither the
+// order nor the cursor, so the upload may run between its launches.
+int order_hook(vaeb_ctx* c) {
+    if (!c->order_pending) return 0;
+    c->order_pending = false;
+    hipLaunchKernelGGL(set_order_kernel, dim3(1), dim3(256), 0, c->s, c->ictl, c->order_pend);
+    CHECK_LAUNCH();
+    return 0;
+}
+
 // Upload a batch order (cursor reset to 0).  Up to kArgOrder entries travel as a kernel
 // argument of set_order_kernel (a kernel on the step stream starts sooner than a host ->
 // device copy: the fixed cost of a short update_many call), longer ones through the
@@ -1671,14 +1690,28 @@ int vaeb_update_many(vaeb_ctx* c, const int32_t* idx, int32_t n) {
     // the call's first step goes out eagerly with its minibatch index in the launch arguments
     // (it reads no order and no cursor): the GPU runs it while the host submits the graph of
     // the remaining steps (which would otherwise lead every call).  The order of those steps
-    // is uploaded BEFORE it: launched after the eager step, the upload kernel started ~6 us
-    // after the GPU had finished the step (kernel trace, profiles/r6/call_timeline.txt)
+    // is uploaded right behind the step's first launch (order_hook): launched after the whole
+    // eager step it started ~6 us after the GPU had finished the step, launched before it the
+    // step's first kernel started ~4.5 us after the upload (kernel traces,
+    // profiles/r6/call_timeline.txt)
     const bool eager = n >= 2 && c->c.use_graph && c->gN[0][1] && !c->graph_failed && flips(c);
     for (int32_t done = eager ? 1 : 0; done < n;) {
         const int32_t m = std::min<int32_t>(n - done, kOrderCap);
-        if (int rc = upload_order(c, idx + done, m)) return rc;
-        if (eager && done == 1)
-            if (int rc = step_eager(c, idx[0])) return rc;
+        if (eager && done == 1) {
+            if (m <= kArgOrder) {   // the upload rides behind the eager step's first launch
+                c->order_pend.n = m;
+                memcpy(c->order_pend.v, idx + done, sizeof(int) * (size_t)m);
+                c->order_pending = true;
+            } else if (int rc = upload_order(c, idx + done, m)) {
+                return rc;
+            }
+            const int rc = step_eager(c, idx[0]);
+            const int rh = order_hook(c);   // where the step's launch path took no hook
+            if (rc) return rc;
+            if (rh) return rh;
+        } else if (int rc = upload_order(c, idx + done, m)) {
+            return rc;
+        }
         if (int rc = run_steps(c, m)) return rc;
         done += m;
     }
