@@ -372,6 +372,40 @@ def test_epoch_throughput_mode_matches_sync_mode():
     assert np.array_equal(res[0][1], res[1][1])
 
 
+def test_update_many_call_forms_match_per_step_updates():
+    """Every form an update_many call takes (vaeb_hip.hip vaeb_update_many / run_steps): one step
+    (order upload + a graph from arena 0), two and twenty steps (the eager first step with the
+    order upload launched behind its first kernel, then ONE graph from arena 1), 33 steps (a
+    32-step graph + the remainder), 961 steps (above the kernel-argument order cap: the pinned
+    staging copy ahead of the eager step), calls starting from either arena -- against the same
+    minibatches as per-step synchronous updates: theta, Adagrad state and the epoch ELBO bit for
+    bit (same Philox noise)."""
+    cfg = O.Config(D=784, H=64, Z=8)
+    B = 16
+    x = data_for(cfg, 64 * B)
+    rng = np.random.default_rng(3)
+    calls = [rng.integers(0, 64, n).astype(np.int32) for n in (1, 2, 20, 1, 33, 961, 3)]
+    res = []
+    for mode in ("sync", "many"):
+        ctx = make_ctx(cfg, B, keep_grads=False, max_eval_rows=B)
+        ctx.set_data(x)
+        ctx.set_params(O.flatten(O.init_params(cfg)))
+        ctx.set_eps_mode(0, seed=5)
+        ctx.set_step(0)
+        if mode == "sync":
+            tot = sum(ctx.update(int(b)) for o in calls for b in o)
+        else:
+            for o in calls:
+                ctx.update_many(o)
+            tot, n = ctx.epoch_elbo()
+            assert n == sum(len(o) for o in calls)
+        res.append((tot, ctx.get_params(), ctx.get_adagrad_state()))
+        ctx.close()
+    assert abs(res[0][0] - res[1][0]) <= 1e-6 * abs(res[0][0])
+    assert np.array_equal(res[0][1], res[1][1])
+    assert np.array_equal(res[0][2], res[1][2])
+
+
 @pytest.mark.parametrize("kw", [dict(D=560, H=200, Z=2, continuous=True), dict(D=784, H=128, Z=24, L=2),
                                 dict(D=784, H=500, Z=20)], ids=["frey2", "latent24_L2", "mnist20"])
 def test_atomic_and_slab_handoffs_agree(kw, monkeypatch):
