@@ -5,7 +5,7 @@ import csv
 import sys
 
 rows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: int(r["Start_Timestamp"]))
-name = lambda r: r["Kernel_Name"].split("(")[0].replace("void ", "").replace("vaeb::", "").replace("bf::", "")[:52]
+name = lambda r: r["Kernel_Name"].split("(")[0].replace("void ", "").replace("vaeb::", "").replace("bf::", "").replace("hf::", "")[:52]
 qid = lambda r: r.get("Queue_Id") or r.get("Stream_Id") or "?"
 starts = [i for i, r in enumerate(rows[:-1]) if "EpiBiasAct" in r["Kernel_Name"] and "EpiHeadsLatent" in rows[i + 1]["Kernel_Name"]]
 for a, b in list(zip(starts, starts[1:]))[5:7]:
