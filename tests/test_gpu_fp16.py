@@ -193,6 +193,41 @@ def test_fp16_graph_epoch_matches_eager_and_tracks_f32():
     assert abs(res["graph"][0] - res["f32"][0]) <= 5e-3 * abs(res["f32"][0])
 
 
+@pytest.mark.parametrize("dt", ["fp16", "bf16"])
+def test_binary_dataset_bit_tile_is_bitwise_the_16bit_tile(dt):
+    """A binary dataset (every value 0 or 1, D % 32 == 0) is also kept as bits, and the Bernoulli
+    decoder epilogue expands its x tile from them (gemm_bf16.hpp EpiDecOutT::load_in).  The same
+    rows with one extra, never-sampled row of 0.5 appended take the 16-bit x tile instead.  Graph
+    and eager steps on either must agree bit for bit -- theta, Adagrad state, epoch ELBO --
+    including a tail tile past D (D = 544: 17 words, the tile's last 7 read nothing) and rows past
+    the batch (B = 100)."""
+    from vaeb_amd import _lib
+    cfg = O.Config(D=544, H=264, Z=40)
+    B = 100
+    x = data_for(cfg, 8 * B)
+    assert set(np.unique(x)) <= {0.0, 1.0}
+    xg = np.concatenate([x, np.full((1, cfg.D), 0.5, np.float32)])   # not binary: the 16-bit tile
+    params = O.flatten(O.init_params(cfg))
+    order = np.array([3, 1, 4, 1, 5, 7, 2, 6, 0, 2], np.int32)
+    res = {}
+    for data_name, data in (("bits", x), ("half", xg)):
+        for use_graph in (True, False):
+            ctx = _lib.Context(cfg.D, cfg.H, cfg.Z, B, max_eval_rows=B, use_graph=use_graph,
+                               dtype=_lib.DTYPE_F16 if dt == "fp16" else _lib.DTYPE_BF16)
+            ctx.set_data(data)
+            ctx.set_params(params)
+            ctx.set_eps_mode(0, seed=10)
+            ctx.update_many(order)
+            s, n = ctx.epoch_elbo()
+            res[data_name, use_graph] = (s / n, ctx.get_params(), ctx.get_adagrad_state())
+            ctx.close()
+    ref = res["half", True]
+    for key, got in res.items():
+        assert got[0] == ref[0], key
+        assert np.array_equal(got[1], ref[1]), key
+        assert np.array_equal(got[2], ref[2]), key
+
+
 def test_fp16_validate_and_reconstruct():
     cfg = O.Config(D=256, H=128, Z=32)
     B = 128

@@ -819,11 +819,44 @@ struct EpiDecOutT {
     float* lp; int nlp;
     float* colpart;
     float* yout;                        // 16-byte aligned or null
+    // x as bits [rows][ldx / 32] (the dataset is binary, ldx % 32 == 0; same rows as x, same
+    // BatchRef), or null: the tile is then expanded from 8 KiB instead of fetched as 128 KiB --
+    // a timing-only build without the x fetch put it at ~11 us of config 5's 142-us decoder
+    // (profiles/r6/decoder_xpf_ab.txt)
+    const uint32_t* xbits;
     // LDS tile [W rows][256 columns] bf16, pitch 528 B = 132 dwords = 4 (mod 64): the 8-byte
     // accesses of a 32-lane group (16 rows x 2 column quads) hit 64 distinct banks
     static constexpr int kPitch = 528;
     template <int W>
     DEV void load_in(int m0, int n0, char* smem) const {
+        if (xbits) {
+            // thread t: tile row t / 2, columns 128 (t & 1) .. + 127 = four words; a word past D
+            // (a tail tile) or a row past M reads 0, as the 16-bit path's out-of-range chunks
+            static_assert(W == 256 && NTHR == 512, "bit tile: 256 rows x 2 halves");
+            const int wpr = ldx >> 5;   // words per data row
+            const rsrc_t src = mkbuf(xbits + xb.offset() / 32, (int64_t)Mx * wpr * 4);
+            const int row = (int)threadIdx.x >> 1, hf = (int)threadIdx.x & 1;
+            const int gr = n0 + row, w0 = (m0 >> 5) + 4 * hf;
+            const uint32_t one = f2bf(1.f);
+            uint32_t wv[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                wv[k] = __builtin_amdgcn_raw_buffer_load_b32(
+                    src, (gr < M && (w0 + k) * 32 < D) ? ((uint32_t)(gr % Mx) * (uint32_t)wpr + (uint32_t)(w0 + k)) * 4u : kOOB, 0, 0);
+            char* dst = smem + row * kPitch + hf * 256;
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {   // 8 columns (16 bytes) per store
+                    const uint32_t b8 = wv[k] >> (8 * q);
+                    v4u v;
+#pragma unroll
+                    for (int e = 0; e < 4; ++e)
+                        v[e] = ((b8 >> (2 * e)) & 1u ? one : 0u) | ((b8 >> (2 * e + 1)) & 1u ? one << 16 : 0u);
+                    *reinterpret_cast<v4u*>(dst + (k * 32 + q * 8) * 2) = v;
+                }
+            return;
+        }
         const rsrc_t src = mkbuf(x + xb.offset(), (int64_t)Mx * ldx * 2);
         constexpr int CPR = BM / 8, N = W * CPR / NTHR;
 #pragma unroll

@@ -48,6 +48,9 @@ struct BfState {
     h16_t* x = nullptr;               // dataset [N x D], 16-bit
     h16_t* xeval = nullptr;           // eval chunk [R x D]
     h16_t* xval = nullptr;            // resident validation set [nval x D] (vaeb_set_valid_data)
+    // the dataset as bits [N x D / 32] when every value is exactly 0 or 1 and D % 32 == 0 (the
+    // Bernoulli decoder epilogue's x tile then costs 1/16 of the bytes; x itself is unchanged)
+    uint32_t* xbits = nullptr;
     h16_t *h = nullptr, *z = nullptr, *hd = nullptr, *dA = nullptr, *dA1 = nullptr, *dml = nullptr,
            *dA3 = nullptr;
     float *ml_slab = nullptr, *dz_slab = nullptr, *w_slab = nullptr;

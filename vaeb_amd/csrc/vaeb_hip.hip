@@ -927,6 +927,7 @@ template <int LA, int LB> bool use8() { return (g_gemm8 >> (2 * LA + LB)) & 1; }
 struct BfFwd {
     int Mb, mode; bool train;
     const bf16_t* x; h16c::BatchRef xb;
+    const uint32_t* xbits = nullptr;   // x as bits (binary datasets; the training step's rows), or null
     int64_t row_base_mul, row_base_add;
     const float* eps_in; int64_t eps_in_ld; uint32_t domain;
     float* yout;
@@ -1515,6 +1516,19 @@ int vaeb_set_data(vaeb_ctx* c, const float* x, int64_t n_rows) {
     if (is_bf16(c)) {
         // the bf16 engine keeps only a bf16 copy; c->data stays a 16-byte placeholder
         if (c->bf.x) { hipFree(c->bf.x); c->bf.x = nullptr; }
+        if (c->bf.xbits) { hipFree(c->bf.xbits); c->bf.xbits = nullptr; }
+        // a binary dataset (every value exactly 0 or 1) also as bits, for the Bernoulli decoder
+        // epilogue's x tile (EpiDecOutT::load_in): 1/16 of its bytes, the same values
+        const int64_t D = c->c.D, nel = n_rows * D;
+        bool binary = D % 32 == 0;
+        for (int64_t i = 0; binary && i < nel; ++i) binary = x[i] == 0.f || x[i] == 1.f;
+        if (binary) {
+            std::vector<uint32_t> bits((size_t)(nel / 32), 0u);
+            for (int64_t i = 0; i < nel; ++i)
+                if (x[i] != 0.f) bits[(size_t)(i >> 5)] |= 1u << (i & 31);
+            if (int rc = dalloc(&c->bf.xbits, bits.size())) return rc;
+            HIP_TRY(hipMemcpy(c->bf.xbits, bits.data(), sizeof(uint32_t) * bits.size(), hipMemcpyHostToDevice));
+        }
         if (int rc = dalloc(&c->bf.x, (size_t)n_rows * c->c.D)) return rc;
         if (int rc = dalloc(&c->data, 4)) return rc;
         if (int rc = bf_upload_rows(c, x, n_rows, c->bf.x)) return rc;
