@@ -80,7 +80,10 @@ int vaeb_destroy(vaeb_ctx* ctx);
 int vaeb_num_params(const vaeb_ctx* ctx, int64_t* n);
 
 /* Training data: copied into a device-resident store owned by ctx (replaces the
- * th.shared x_train of VAEB.py:184).  Row-major float32 [n_rows x D]. */
+ * th.shared x_train of VAEB.py:184).  Row-major float32 [n_rows x D].  16-bit contexts
+ * keep it as fp16 / bf16 and, when every value is exactly 0 or 1 and D % 32 == 0, also as
+ * bits (1/16 of that), from which the Bernoulli decoder expands its x tiles: the same
+ * values, so the same steps bit for bit (one host pass over x decides). */
 int vaeb_set_data(vaeb_ctx* ctx, const float* x, int64_t n_rows);
 
 /* Parameters / optimizer state in reference order.  For the FV estimator the
