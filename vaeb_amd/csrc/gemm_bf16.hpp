@@ -990,13 +990,74 @@ struct EpiAdagrad {
     static constexpr bool kIn = false, kOut = false;
     ColMap map; Opt opt; int M, N;
     int sld;   // row stride of the bf16 shadow (0: N; a column range of a wider weight: its width)
+    // vec (host-checked: the arena runs, widths and strides multiples of 4, N % 4 == 0): on the
+    // 256-wide tiles each wave transposes its 64 x 64 gradient block through its own 17 KiB of
+    // the (free) LDS, so a lane updates four consecutive columns of a row with 16-byte theta /
+    // accumulator loads and stores and one 8-byte shadow store -- a quarter of the memory
+    // instructions of the per-element form
+    int vec;
+    template <int W, class CM>
+    DEV void apply_vec(int mw, int nw, f32x4 (&acc)[4][4], char* smem) const {
+        constexpr int TP = 68;   // row pitch (floats): 16-byte rows, the 4-row write groups on disjoint banks
+        const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+        float* t = reinterpret_cast<float*>(smem) + wave * (64 * TP);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) t[(16 * i + 4 * (lane >> 4) + r) * TP + 16 * j + (lane & 15)] = acc[i][j][r] * opt.gs;
+        const rsrc_t bth = mkbuf(opt.th_in, opt.n * 4), bac = mkbuf(opt.accum, opt.n * 4);
+        const rsrc_t bto = mkbuf(opt.th_out, opt.n * 4), bgr = mkbuf(opt.grad, opt.n * 4);
+        const int sl = sld ? sld : N;
+#pragma unroll
+        for (int h = 0; h < 4; ++h) {   // 4 groups of 4 float4 per lane: loads first, then the stores
+            uint32_t off[4];
+            int64_t so[4];
+            f32x4 g[4], th[4], ac[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int e = (4 * h + u) * 64 + lane;        // float4 e of the 64 x 64 block
+                const int lr = e >> 4, c4 = (e & 15) * 4;      // local row, first local column
+                const int row = mw + lr, col = nw + CM::off(c4 >> 4) + (c4 & 15);
+                const bool ok = row < M && col < N;            // N % 4 == 0: all four or none
+                off[u] = ok ? (uint32_t)map.at(row, col) * 4u : kOOB;
+                so[u] = ok ? (int64_t)row * sl + col : -1;
+                g[u] = *reinterpret_cast<const f32x4*>(t + lr * TP + c4);
+                th[u] = bld4(bth, opt.update ? off[u] : kOOB);
+                ac[u] = bld4(bac, opt.update ? off[u] : kOOB);
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                if (opt.store_grad) __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, g[u]), bgr, off[u], 0, 0);
+                if (!opt.update) continue;
+                f32x4 a, tn;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const float gg = g[u][k] - opt.prior * th[u][k];
+                    a[k] = ac[u][k] + gg * gg;
+                    tn[k] = th[u][k] + opt.lr * gg / (__builtin_amdgcn_sqrtf(a[k]) + opt.eps) - opt.decay * th[u][k] * th[u][k];
+                }
+                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, a), bac, off[u], 0, 0);
+                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, tn), bto, off[u], 0, 0);
+                if (so[u] >= 0)
+                    *reinterpret_cast<uint2*>(opt.shadow_out + so[u]) = make_uint2(f2bf2(tn[0], tn[1]), f2bf2(tn[2], tn[3]));
+            }
+        }
+    }
     // The optimizer rule of Opt::apply on the wave's 64 x 64 block, one 16-row fragment
     // row (16 elements per lane) per memory round trip: all theta / accumulator loads of
     // the fragment row are issued before its stores (buffer loads, masked elements read
     // out of range), instead of a load -> store chain per element that hipcc cannot
     // reorder (theta_in / accum may alias the stores, as far as it can tell).
     template <int W, class CM = ColStd>
-    DEV void apply(int mw, int nw, f32x4 (&acc)[4][4], int, char*) const {
+    DEV void apply(int mw, int nw, f32x4 (&acc)[4][4], int, char* smem) const {
+        if constexpr (W == 256) {
+            if (vec) {
+                apply_vec<W, CM>(mw, nw, acc, smem);
+                return;
+            }
+        }
         const int lane = threadIdx.x & 63;
         const rsrc_t bth = mkbuf(opt.th_in, opt.n * 4), bac = mkbuf(opt.accum, opt.n * 4);
         const rsrc_t bto = mkbuf(opt.th_out, opt.n * 4), bgr = mkbuf(opt.grad, opt.n * 4);
